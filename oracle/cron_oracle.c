@@ -1,0 +1,1277 @@
+/*
+ * cron_oracle.c -- literal CPU restatement of cronsun's scheduling hot path
+ * and the Go `time` semantics it depends on.
+ *
+ * TEST INFRASTRUCTURE ONLY (see cron_oracle.h).  Written for clarity and
+ * faithfulness, not speed: every accessor recomputes the zone offset and the
+ * civil date, exactly like Go's time.Time methods do, so the per-call cost
+ * profile mirrors the reference's.
+ */
+#include "cron_oracle.h"
+
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ALPHA INT64_MIN
+#define OMEGA INT64_MAX
+#define SECS_PER_DAY 86400LL
+
+/* ------------------------------------------------------------------------ */
+/* proleptic Gregorian helpers (Go's absDate / daysSinceEpoch restated)      */
+/* ------------------------------------------------------------------------ */
+
+static int64_t floordiv(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) q--;
+    return q;
+}
+
+static int is_leap(int64_t y) {
+    return y % 4 == 0 && (y % 100 != 0 || y % 400 == 0);
+}
+
+/* days since 1970-01-01 of civil date y-m-d (m in 1..12). */
+static int64_t days_from_civil(int64_t y, int64_t m, int64_t d) {
+    y -= m <= 2;
+    int64_t era = floordiv(y, 400);
+    int64_t yoe = y - era * 400;
+    int64_t mp = (m + 9) % 12;
+    int64_t doy = (153 * mp + 2) / 5 + d - 1;
+    int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+
+static void civil_from_days(int64_t z, int64_t *y, int *m, int *d) {
+    z += 719468;
+    int64_t era = floordiv(z, 146097);
+    int64_t doe = z - era * 146097;
+    int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    int64_t yy = yoe + era * 400;
+    int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    int64_t mp = (5 * doy + 2) / 153;
+    int64_t dd = doy - (153 * mp + 2) / 5 + 1;
+    int64_t mm = mp < 10 ? mp + 3 : mp - 9;
+    *y = yy + (mm <= 2);
+    *m = (int)mm;
+    *d = (int)dd;
+}
+
+static const int days_before[13] = {0,   31,  59,  90,  120, 151, 181,
+                                    212, 243, 273, 304, 334, 365};
+
+static int days_in(int month, int64_t year) {
+    if (month == 2 && is_leap(year)) return 29;
+    return days_before[month] - days_before[month - 1];
+}
+
+/* ------------------------------------------------------------------------ */
+/* Location (time/zoneinfo.go, zoneinfo_read.go)                            */
+/* ------------------------------------------------------------------------ */
+
+typedef struct {
+    int32_t offset;
+    uint8_t is_dst;
+} or_zone;
+
+typedef struct {
+    int64_t when;
+    uint8_t index;
+} or_tx;
+
+struct or_loc {
+    int n_zone;
+    or_zone *zone;
+    int n_tx;
+    or_tx *tx;
+    char *extend; /* POSIX TZ footer, "" if none */
+};
+
+static uint32_t be32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) |
+           ((uint32_t)p[2] << 8) | p[3];
+}
+static uint64_t be64(const uint8_t *p) {
+    return ((uint64_t)be32(p) << 32) | be32(p + 4);
+}
+
+int or_loc_from_tzif(const uint8_t *data, size_t len, or_loc **out) {
+    /* LoadLocationFromTZData */
+    size_t pos = 0;
+    if (len < 44 || memcmp(data, "TZif", 4) != 0) return -1;
+    int version = data[4] == 0 ? 1 : data[4] - '0';
+    pos = 20;
+    uint32_t n[6];
+    for (int i = 0; i < 6; i++) n[i] = be32(data + pos + 4 * i);
+    pos += 24;
+    /* counts: 0 UTCLocal, 1 StdWall, 2 Leap, 3 Time, 4 Zone, 5 Char */
+    int is64 = 0;
+    if (version > 1) {
+        size_t skip = (size_t)n[3] * 4 + n[3] + (size_t)n[4] * 6 + n[5] +
+                      (size_t)n[2] * 8 + n[1] + n[0];
+        pos += skip;
+        if (pos + 44 > len || memcmp(data + pos, "TZif", 4) != 0) return -1;
+        pos += 20;
+        for (int i = 0; i < 6; i++) n[i] = be32(data + pos + 4 * i);
+        pos += 24;
+        is64 = 1;
+    }
+    size_t tsz = is64 ? 8 : 4;
+    size_t need = (size_t)n[3] * tsz + n[3] + (size_t)n[4] * 6 + n[5] +
+                  (size_t)n[2] * (tsz + 4) + n[1] + n[0];
+    if (pos + need > len) return -1;
+    const uint8_t *txtimes = data + pos;
+    const uint8_t *txzones = txtimes + (size_t)n[3] * tsz;
+    const uint8_t *zonedata = txzones + n[3];
+    const uint8_t *rest = zonedata + (size_t)n[4] * 6 + n[5] +
+                          (size_t)n[2] * (tsz + 4) + n[1] + n[0];
+    size_t rest_len = len - (size_t)(rest - data);
+
+    if (n[4] == 0 || n[4] > 255) return -1;
+    or_loc *l = (or_loc *)calloc(1, sizeof(or_loc));
+    l->n_zone = (int)n[4];
+    l->zone = (or_zone *)calloc(n[4], sizeof(or_zone));
+    for (uint32_t i = 0; i < n[4]; i++) {
+        l->zone[i].offset = (int32_t)be32(zonedata + 6 * i);
+        l->zone[i].is_dst = zonedata[6 * i + 4] != 0;
+    }
+    l->n_tx = (int)n[3];
+    l->tx = (or_tx *)calloc(n[3] ? n[3] : 1, sizeof(or_tx));
+    for (uint32_t i = 0; i < n[3]; i++) {
+        int64_t w = is64 ? (int64_t)be64(txtimes + 8 * i)
+                         : (int64_t)(int32_t)be32(txtimes + 4 * i);
+        l->tx[i].when = w;
+        if (txzones[i] >= n[4]) {
+            or_loc_free(l);
+            return -1;
+        }
+        l->tx[i].index = txzones[i];
+    }
+    if (l->n_tx == 0) { /* fake transition covering all time */
+        l->n_tx = 1;
+        l->tx[0].when = ALPHA;
+        l->tx[0].index = 0;
+    }
+    l->extend = (char *)calloc(rest_len + 1, 1);
+    if (version > 1 && rest_len > 2 && rest[0] == '\n' &&
+        rest[rest_len - 1] == '\n') {
+        memcpy(l->extend, rest + 1, rest_len - 2);
+    }
+    *out = l;
+    return 0;
+}
+
+int or_loc_fixed(int32_t offset, or_loc **out) {
+    or_loc *l = (or_loc *)calloc(1, sizeof(or_loc));
+    l->n_zone = 1;
+    l->zone = (or_zone *)calloc(1, sizeof(or_zone));
+    l->zone[0].offset = offset;
+    l->n_tx = 1;
+    l->tx = (or_tx *)calloc(1, sizeof(or_tx));
+    l->tx[0].when = ALPHA;
+    l->extend = (char *)calloc(1, 1);
+    *out = l;
+    return 0;
+}
+
+int or_loc_utc(or_loc **out) {
+    or_loc *l = (or_loc *)calloc(1, sizeof(or_loc));
+    l->extend = (char *)calloc(1, 1);
+    *out = l;
+    return 0;
+}
+
+void or_loc_free(or_loc *l) {
+    if (!l) return;
+    free(l->zone);
+    free(l->tx);
+    free(l->extend);
+    free(l);
+}
+
+/* --- tzset: POSIX TZ footer (time/zoneinfo.go tzset*) --- */
+
+static int tzset_name(const char **s) {
+    const char *p = *s;
+    if (!*p) return 0;
+    if (*p != '<') {
+        int i = 0;
+        for (; p[i]; i++) {
+            char c = p[i];
+            if ((c >= '0' && c <= '9') || c == ',' || c == '-' || c == '+') {
+                if (i < 3) return 0;
+                *s = p + i;
+                return 1;
+            }
+        }
+        if (i < 3) return 0;
+        *s = p + i;
+        return 1;
+    }
+    for (int i = 0; p[i]; i++) {
+        if (p[i] == '>') {
+            *s = p + i + 1;
+            return 1;
+        }
+    }
+    return 0;
+}
+
+static int tzset_num(const char **s, int min, int max, int *num) {
+    const char *p = *s;
+    if (!*p) return 0;
+    int v = 0, i = 0;
+    for (; p[i]; i++) {
+        char c = p[i];
+        if (c < '0' || c > '9') {
+            if (i == 0 || v < min) return 0;
+            *num = v;
+            *s = p + i;
+            return 1;
+        }
+        v = v * 10 + (c - '0');
+        if (v > max) return 0;
+    }
+    if (v < min) return 0;
+    *num = v;
+    *s = p + i;
+    return 1;
+}
+
+static int tzset_offset(const char **s, int *off) {
+    const char *p = *s;
+    if (!*p) return 0;
+    int neg = 0;
+    if (*p == '+') p++;
+    else if (*p == '-') { p++; neg = 1; }
+    int hours;
+    if (!tzset_num(&p, 0, 24 * 7, &hours)) return 0;
+    int o = hours * 3600;
+    if (*p != ':') { *off = neg ? -o : o; *s = p; return 1; }
+    p++;
+    int mins;
+    if (!tzset_num(&p, 0, 59, &mins)) return 0;
+    o += mins * 60;
+    if (*p != ':') { *off = neg ? -o : o; *s = p; return 1; }
+    p++;
+    int secs;
+    if (!tzset_num(&p, 0, 59, &secs)) return 0;
+    o += secs;
+    *off = neg ? -o : o;
+    *s = p;
+    return 1;
+}
+
+enum { RULE_JULIAN, RULE_DOY, RULE_MWD };
+typedef struct { int kind, day, week, mon, time; } tzrule;
+
+static int tzset_rule(const char **s, tzrule *r) {
+    const char *p = *s;
+    memset(r, 0, sizeof(*r));
+    if (!*p) return 0;
+    if (*p == 'J') {
+        p++;
+        int jday;
+        if (!tzset_num(&p, 1, 365, &jday)) return 0;
+        r->kind = RULE_JULIAN;
+        r->day = jday;
+    } else if (*p == 'M') {
+        p++;
+        int mon, week, day;
+        if (!tzset_num(&p, 1, 12, &mon) || *p != '.') return 0;
+        p++;
+        if (!tzset_num(&p, 1, 5, &week) || *p != '.') return 0;
+        p++;
+        if (!tzset_num(&p, 0, 6, &day)) return 0;
+        r->kind = RULE_MWD;
+        r->day = day;
+        r->week = week;
+        r->mon = mon;
+    } else {
+        int day;
+        if (!tzset_num(&p, 0, 365, &day)) return 0;
+        r->kind = RULE_DOY;
+        r->day = day;
+    }
+    if (*p != '/') {
+        r->time = 2 * 3600;
+        *s = p;
+        return 1;
+    }
+    p++;
+    int off;
+    if (!tzset_offset(&p, &off)) return 0;
+    r->time = off;
+    *s = p;
+    return 1;
+}
+
+static int64_t tzrule_time(int64_t year, const tzrule *r, int off) {
+    int64_t s = 0;
+    switch (r->kind) {
+    case RULE_JULIAN:
+        s = (int64_t)(r->day - 1) * SECS_PER_DAY;
+        if (is_leap(year) && r->day >= 60) s += SECS_PER_DAY;
+        break;
+    case RULE_DOY:
+        s = (int64_t)r->day * SECS_PER_DAY;
+        break;
+    case RULE_MWD: {
+        /* Zeller's congruence, as Go does */
+        int64_t m1 = (r->mon + 9) % 12 + 1;
+        int64_t yy0 = year;
+        if (r->mon <= 2) yy0--;
+        int64_t yy1 = yy0 / 100;
+        int64_t yy2 = yy0 % 100;
+        int64_t dow = ((26 * m1 - 2) / 10 + 1 + yy2 + yy2 / 4 + yy1 / 4 - 2 * yy1) % 7;
+        if (dow < 0) dow += 7;
+        int64_t d = r->day - dow;
+        if (d < 0) d += 7;
+        for (int i = 1; i < r->week; i++) {
+            if (d + 7 >= days_in(r->mon, year)) break;
+            d += 7;
+        }
+        d += days_before[r->mon - 1];
+        if (is_leap(year) && r->mon > 2) d++;
+        s = d * SECS_PER_DAY;
+        break;
+    }
+    }
+    return s + r->time - off;
+}
+
+/* returns 1 if ok */
+static int go_tzset(const char *s, int64_t last_tx_sec, int64_t sec, int32_t *offset,
+                 int64_t *start, int64_t *end) {
+    const char *p = s;
+    if (!tzset_name(&p)) return 0;
+    int std_off, dst_off;
+    if (!tzset_offset(&p, &std_off)) return 0;
+    std_off = -std_off;
+    if (*p == 0 || *p == ',') {
+        *offset = std_off;
+        *start = last_tx_sec;
+        *end = OMEGA;
+        return 1;
+    }
+    if (!tzset_name(&p)) return 0;
+    if (*p == 0 || *p == ',') {
+        dst_off = std_off + 3600;
+    } else {
+        if (!tzset_offset(&p, &dst_off)) return 0;
+        dst_off = -dst_off;
+    }
+    const char *rules = p;
+    if (*rules == 0) rules = ",M3.2.0,M11.1.0";
+    if (*rules != ',' && *rules != ';') return 0;
+    rules++;
+    tzrule sr, er;
+    if (!tzset_rule(&rules, &sr) || *rules != ',') return 0;
+    rules++;
+    if (!tzset_rule(&rules, &er) || *rules != 0) return 0;
+
+    /* year and yday of sec as a UTC date */
+    int64_t day = floordiv(sec, SECS_PER_DAY);
+    int64_t year;
+    int mo, dd;
+    civil_from_days(day, &year, &mo, &dd);
+    int64_t yday = day - days_from_civil(year, 1, 1);
+    int64_t ysec = yday * SECS_PER_DAY + sec % SECS_PER_DAY; /* Go's truncating % */
+    int64_t abs = days_from_civil(year, 1, 1) * SECS_PER_DAY;
+    int64_t start_sec = tzrule_time(year, &sr, std_off);
+    int64_t end_sec = tzrule_time(year, &er, dst_off);
+    if (end_sec < start_sec) {
+        int64_t t = start_sec; start_sec = end_sec; end_sec = t;
+        int x = std_off; std_off = dst_off; dst_off = x;
+    }
+    if (ysec < start_sec) {
+        *offset = std_off; *start = abs; *end = start_sec + abs;
+    } else if (ysec >= end_sec) {
+        *offset = std_off; *start = end_sec + abs; *end = abs + 365 * SECS_PER_DAY;
+    } else {
+        *offset = dst_off; *start = start_sec + abs; *end = end_sec + abs;
+    }
+    return 1;
+}
+
+static int lookup_first_zone(const or_loc *l) {
+    int used = 0;
+    for (int i = 0; i < l->n_tx; i++)
+        if (l->tx[i].index == 0) used = 1;
+    if (!used) return 0;
+    if (l->n_tx > 0 && l->zone[l->tx[0].index].is_dst) {
+        for (int zi = (int)l->tx[0].index - 1; zi >= 0; zi--)
+            if (!l->zone[zi].is_dst) return zi;
+    }
+    for (int zi = 0; zi < l->n_zone; zi++)
+        if (!l->zone[zi].is_dst) return zi;
+    return 0;
+}
+
+int32_t or_lookup(const or_loc *l, int64_t sec, int64_t *start, int64_t *end) {
+    if (l->n_zone == 0) {
+        *start = ALPHA;
+        *end = OMEGA;
+        return 0;
+    }
+    if (l->n_tx == 0 || sec < l->tx[0].when) {
+        int zi = lookup_first_zone(l);
+        *start = ALPHA;
+        *end = l->n_tx > 0 ? l->tx[0].when : OMEGA;
+        return l->zone[zi].offset;
+    }
+    int64_t e = OMEGA;
+    int lo = 0, hi = l->n_tx;
+    while (hi - lo > 1) {
+        int m = (int)((unsigned)(lo + hi) >> 1);
+        int64_t lim = l->tx[m].when;
+        if (sec < lim) {
+            e = lim;
+            hi = m;
+        } else {
+            lo = m;
+        }
+    }
+    int32_t off = l->zone[l->tx[lo].index].offset;
+    *start = l->tx[lo].when;
+    *end = e;
+    if (lo == l->n_tx - 1 && l->extend[0]) {
+        int32_t eo;
+        int64_t es, ee;
+        if (go_tzset(l->extend, *start, sec, &eo, &es, &ee)) {
+            *start = es;
+            *end = ee;
+            return eo;
+        }
+    }
+    return off;
+}
+
+static int32_t offset_at(const or_loc *l, int64_t sec) {
+    int64_t s, e;
+    return or_lookup(l, sec, &s, &e);
+}
+
+void or_fields_of(int64_t usec, const or_loc *l, or_fields *f) {
+    int64_t local = usec + offset_at(l, usec);
+    int64_t day = floordiv(local, SECS_PER_DAY);
+    int64_t tod = local - day * SECS_PER_DAY;
+    int64_t y;
+    int m, d;
+    civil_from_days(day, &y, &m, &d);
+    f->year = y;
+    f->month = m;
+    f->day = d;
+    f->hour = (int)(tod / 3600);
+    f->minute = (int)(tod / 60 % 60);
+    f->second = (int)(tod % 60);
+    int64_t wd = (day + 4) % 7;
+    if (wd < 0) wd += 7;
+    f->weekday = (int)wd;
+    f->yday = (int)(day - days_from_civil(y, 1, 1));
+}
+
+/* norm(hi, lo, base) from time.go */
+static void norm(int64_t *hi, int64_t *lo, int64_t base) {
+    if (*lo < 0) {
+        int64_t n = (-*lo - 1) / base + 1;
+        *hi -= n;
+        *lo += n * base;
+    }
+    if (*lo >= base) {
+        int64_t n = *lo / base;
+        *hi += n;
+        *lo -= n * base;
+    }
+}
+
+int64_t or_date(int64_t year, int64_t month, int64_t day, int64_t hour,
+                int64_t min, int64_t sec, const or_loc *l) {
+    int64_t m = month - 1;
+    norm(&year, &m, 12);
+    month = m + 1;
+    /* nsec == 0 */
+    norm(&min, &sec, 60);
+    norm(&hour, &min, 60);
+    norm(&day, &hour, 24);
+    int64_t d = days_from_civil(year, month, 1) + (day - 1);
+    int64_t usec = d * SECS_PER_DAY + hour * 3600 + min * 60 + sec;
+    int64_t start, end;
+    int32_t offset = or_lookup(l, usec, &start, &end);
+    if (offset != 0) {
+        int64_t utc = usec - offset;
+        if (utc < start || utc >= end) offset = offset_at(l, utc);
+        usec -= offset;
+    }
+    return usec;
+}
+
+/* ------------------------------------------------------------------------ */
+/* node/cron/spec.go                                                        */
+/* ------------------------------------------------------------------------ */
+
+static int day_matches(const or_spec *s, const or_fields *f) {
+    int dom_match = ((1ULL << f->day) & s->dom) > 0;
+    int dow_match = ((1ULL << f->weekday) & s->dow) > 0;
+    if ((s->dom & OR_STAR_BIT) || (s->dow & OR_STAR_BIT))
+        return dom_match && dow_match;
+    return dom_match || dow_match;
+}
+
+static int64_t add_date(int64_t t, int dy, int dm, int dd, const or_loc *l) {
+    or_fields f;
+    or_fields_of(t, l, &f);
+    return or_date(f.year + dy, f.month + dm, f.day + dd, f.hour, f.minute,
+                   f.second, l);
+}
+
+int64_t or_spec_next(const or_spec *s, int64_t usec, int32_t nsec,
+                     const or_loc *l) {
+    (void)nsec;
+    /* t = t.Add(1*time.Second - time.Duration(t.Nanosecond())) */
+    int64_t t = usec + 1;
+    int added = 0;
+    or_fields f;
+    or_fields_of(t, l, &f);
+    int64_t year_limit = f.year + 5;
+
+WRAP:
+    or_fields_of(t, l, &f);
+    if (f.year > year_limit) return OR_ZERO_TIME;
+
+    for (;;) { /* month */
+        or_fields_of(t, l, &f);
+        if ((1ULL << f.month) & s->month) break;
+        if (!added) {
+            added = 1;
+            t = or_date(f.year, f.month, 1, 0, 0, 0, l);
+        }
+        t = add_date(t, 0, 1, 0, l);
+        or_fields_of(t, l, &f);
+        if (f.month == 1) goto WRAP;
+    }
+    for (;;) { /* day */
+        or_fields_of(t, l, &f);
+        if (day_matches(s, &f)) break;
+        if (!added) {
+            added = 1;
+            t = or_date(f.year, f.month, f.day, 0, 0, 0, l);
+        }
+        t = add_date(t, 0, 0, 1, l);
+        or_fields_of(t, l, &f);
+        if (f.day == 1) goto WRAP;
+    }
+    for (;;) { /* hour */
+        or_fields_of(t, l, &f);
+        if ((1ULL << f.hour) & s->hour) break;
+        if (!added) {
+            added = 1;
+            t = or_date(f.year, f.month, f.day, f.hour, 0, 0, l);
+        }
+        t += 3600;
+        or_fields_of(t, l, &f);
+        if (f.hour == 0) goto WRAP;
+    }
+    for (;;) { /* minute */
+        or_fields_of(t, l, &f);
+        if ((1ULL << f.minute) & s->minute) break;
+        if (!added) {
+            added = 1;
+            /* Truncate(Minute): on absolute time since year 1 (a multiple
+             * of 60 s away from the usec epoch) */
+            t -= t - floordiv(t, 60) * 60;
+        }
+        t += 60;
+        or_fields_of(t, l, &f);
+        if (f.minute == 0) goto WRAP;
+    }
+    for (;;) { /* second */
+        or_fields_of(t, l, &f);
+        if ((1ULL << f.second) & s->second) break;
+        if (!added) {
+            added = 1; /* Truncate(Second): nsec is already 0 */
+        }
+        t += 1;
+        or_fields_of(t, l, &f);
+        if (f.second == 0) goto WRAP;
+    }
+    return t;
+}
+
+/* ------------------------------------------------------------------------ */
+/* node/cron/constantdelay.go                                               */
+/* ------------------------------------------------------------------------ */
+
+#define NS_PER_SEC 1000000000LL
+
+int64_t or_every(int64_t d) {
+    if (d < NS_PER_SEC) d = NS_PER_SEC;
+    return d - d % NS_PER_SEC;
+}
+
+int64_t or_const_next(int64_t delay_ns, int64_t usec, int32_t nsec) {
+    /* t.Add(Delay - nsec): total nanoseconds past `usec` = nsec + Delay - nsec */
+    int64_t ns = (int64_t)nsec + (delay_ns - nsec);
+    return usec + floordiv(ns, NS_PER_SEC);
+}
+
+int64_t or_sched_next(const or_sched *s, int64_t usec, int32_t nsec,
+                      const or_loc *l) {
+    if (s->kind == 1) return or_const_next(s->delay_ns, usec, nsec);
+    return or_spec_next(&s->spec, usec, nsec, l);
+}
+
+/* ------------------------------------------------------------------------ */
+/* node/cron/parser.go                                                      */
+/* ------------------------------------------------------------------------ */
+
+static void seterr(char *err, size_t cap, const char *fmt, ...) {
+    if (!err || cap == 0) return;
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(err, cap, fmt, ap);
+    va_end(ap);
+}
+
+/* strconv.Quote, restricted to what spec strings can contain */
+static void go_quote(const char *s, size_t n, char *out, size_t cap) {
+    size_t o = 0;
+#define PUT(c) do { if (o + 1 < cap) out[o++] = (c); } while (0)
+    PUT('"');
+    for (size_t i = 0; i < n; i++) {
+        unsigned char c = (unsigned char)s[i];
+        if (c == '"' || c == '\\') { PUT('\\'); PUT((char)c); }
+        else if (c >= 0x20 && c < 0x7f) PUT((char)c);
+        else if (c == '\n') { PUT('\\'); PUT('n'); }
+        else if (c == '\t') { PUT('\\'); PUT('t'); }
+        else if (c == '\r') { PUT('\\'); PUT('r'); }
+        else if (c == '\a') { PUT('\\'); PUT('a'); }
+        else if (c == '\b') { PUT('\\'); PUT('b'); }
+        else if (c == '\f') { PUT('\\'); PUT('f'); }
+        else if (c == '\v') { PUT('\\'); PUT('v'); }
+        else if (c >= 0x80) PUT((char)c); /* UTF-8 passthrough */
+        else {
+            static const char hx[] = "0123456789abcdef";
+            PUT('\\'); PUT('x'); PUT(hx[c >> 4]); PUT(hx[c & 15]);
+        }
+    }
+    PUT('"');
+    out[o < cap ? o : cap - 1] = 0;
+#undef PUT
+}
+
+/* strconv.Atoi; returns 0 ok, -1 syntax, -2 range */
+static int go_atoi(const char *s, size_t n, int64_t *out) {
+    if (n > 0 && n < 19) {
+        size_t i = 0;
+        int neg = 0;
+        if (s[0] == '-' || s[0] == '+') {
+            neg = s[0] == '-';
+            i = 1;
+            if (n < 2) return -1;
+        }
+        int64_t v = 0;
+        for (; i < n; i++) {
+            unsigned char c = (unsigned char)(s[i] - '0');
+            if (c > 9) return -1;
+            v = v * 10 + c;
+        }
+        *out = neg ? -v : v;
+        return 0;
+    }
+    /* ParseInt(s, 10, 0) */
+    if (n == 0) return -1;
+    size_t i = 0;
+    int neg = 0;
+    if (s[0] == '-' || s[0] == '+') {
+        neg = s[0] == '-';
+        i = 1;
+    }
+    if (i >= n) return -1;
+    uint64_t un = 0;
+    int range = 0;
+    for (; i < n; i++) {
+        unsigned char c = (unsigned char)(s[i] - '0');
+        if (c > 9) return -1;
+        if (range) continue;
+        if (un > UINT64_MAX / 10) { range = 1; continue; }
+        uint64_t n1 = un * 10 + c;
+        if (n1 < un * 10) { range = 1; continue; }
+        un = n1;
+    }
+    if (range) return -2;
+    uint64_t cutoff = 1ULL << 63;
+    if (!neg && un >= cutoff) return -2;
+    if (neg && un > cutoff) return -2;
+    *out = neg ? (int64_t)(0 - un) : (int64_t)un;
+    return 0;
+}
+
+static int must_parse_int(const char *s, size_t n, uint64_t *out, char *err,
+                          size_t cap) {
+    int64_t v = 0;
+    int rc = go_atoi(s, n, &v);
+    if (rc != 0) {
+        char q[256];
+        go_quote(s, n, q, sizeof q);
+        seterr(err, cap, "Failed to parse int from %.*s: strconv.Atoi: parsing %s: %s",
+               (int)n, s, q, rc == -1 ? "invalid syntax" : "value out of range");
+        return -1;
+    }
+    if (v < 0) {
+        seterr(err, cap, "Negative number (%lld) not allowed: %.*s", (long long)v,
+               (int)n, s);
+        return -1;
+    }
+    *out = (uint64_t)v; /* Go: uint(num) */
+    return 0;
+}
+
+static const char *month_names[] = {"jan", "feb", "mar", "apr", "may", "jun",
+                                    "jul", "aug", "sep", "oct", "nov", "dec"};
+static const char *dow_names[] = {"sun", "mon", "tue", "wed", "thu", "fri", "sat"};
+
+/* names: 0 none, 1 months, 2 dow */
+static int parse_int_or_name(const char *s, size_t n, int names, uint64_t *out,
+                             char *err, size_t cap) {
+    if (names && n == 3) {
+        char low[4];
+        for (int i = 0; i < 3; i++) {
+            char c = s[i];
+            low[i] = (c >= 'A' && c <= 'Z') ? (char)(c + 32) : c;
+        }
+        low[3] = 0;
+        if (names == 1) {
+            for (int i = 0; i < 12; i++)
+                if (!strcmp(low, month_names[i])) { *out = (unsigned)(i + 1); return 0; }
+        } else {
+            for (int i = 0; i < 7; i++)
+                if (!strcmp(low, dow_names[i])) { *out = (unsigned)i; return 0; }
+        }
+    }
+    return must_parse_int(s, n, out, err, cap);
+}
+
+uint64_t or_get_bits(unsigned min, unsigned max, unsigned step) {
+    if (step == 1) {
+        uint64_t hi = (max + 1 >= 64) ? 0 : (UINT64_MAX << (max + 1));
+        uint64_t lo = (min >= 64) ? 0 : (UINT64_MAX << min);
+        return ~hi & lo;
+    }
+    uint64_t bits = 0;
+    for (uint64_t i = min; i <= max; i += step) {
+        if (i < 64) bits |= 1ULL << i;
+    }
+    return bits;
+}
+
+static int get_range_names(const char *expr, size_t len, unsigned rmin,
+                           unsigned rmax, int names, uint64_t *bits, char *err,
+                           size_t cap) {
+    *bits = 0;
+    /* rangeAndStep = strings.Split(expr, "/") */
+    size_t nslash = 0, slash_pos = 0;
+    for (size_t i = 0; i < len; i++)
+        if (expr[i] == '/') { if (nslash == 0) slash_pos = i; nslash++; }
+    size_t r0len = nslash ? slash_pos : len;
+    /* lowAndHigh = strings.Split(rangeAndStep[0], "-") */
+    size_t nhyph = 0, hyph_pos = 0;
+    for (size_t i = 0; i < r0len; i++)
+        if (expr[i] == '-') { if (nhyph == 0) hyph_pos = i; nhyph++; }
+    int single_digit = nhyph == 0;
+    size_t lh0len = nhyph ? hyph_pos : r0len;
+
+    uint64_t start, end, step;
+    uint64_t extra = 0;
+    if ((lh0len == 1 && (expr[0] == '*' || expr[0] == '?'))) {
+        start = rmin;
+        end = rmax;
+        extra = OR_STAR_BIT;
+    } else {
+        if (parse_int_or_name(expr, lh0len, names, &start, err, cap)) return -1;
+        if (nhyph == 0) {
+            end = start;
+        } else if (nhyph == 1) {
+            const char *hs = expr + hyph_pos + 1;
+            size_t hl = r0len - hyph_pos - 1;
+            if (parse_int_or_name(hs, hl, names, &end, err, cap)) return -1;
+        } else {
+            seterr(err, cap, "Too many hyphens: %.*s", (int)len, expr);
+            return -1;
+        }
+    }
+    if (nslash == 0) {
+        step = 1;
+    } else if (nslash == 1) {
+        if (must_parse_int(expr + slash_pos + 1, len - slash_pos - 1, &step, err, cap))
+            return -1;
+        if (single_digit) end = rmax;
+    } else {
+        seterr(err, cap, "Too many slashes: %.*s", (int)len, expr);
+        return -1;
+    }
+    if (start < rmin) {
+        seterr(err, cap, "Beginning of range (%llu) below minimum (%u): %.*s",
+               (unsigned long long)start, rmin, (int)len, expr);
+        return -1;
+    }
+    if (end > rmax) {
+        seterr(err, cap, "End of range (%llu) above maximum (%u): %.*s",
+               (unsigned long long)end, rmax, (int)len, expr);
+        return -1;
+    }
+    if (start > end) {
+        seterr(err, cap, "Beginning of range (%llu) beyond end of range (%llu): %.*s",
+               (unsigned long long)start, (unsigned long long)end, (int)len, expr);
+        return -1;
+    }
+    if (step == 0) {
+        seterr(err, cap, "Step of range should be a positive number: %.*s", (int)len,
+               expr);
+        return -1;
+    }
+    *bits = or_get_bits((unsigned)start, (unsigned)end,
+                        step > 64 ? 64u : (unsigned)step) | extra;
+    return 0;
+}
+
+int or_get_range(const char *expr, size_t len, unsigned min, unsigned max,
+                 uint64_t *bits, char *err, size_t errcap) {
+    return get_range_names(expr, len, min, max, 0, bits, err, errcap);
+}
+
+static int get_field_names(const char *f, size_t len, unsigned min, unsigned max,
+                           int names, uint64_t *bits, char *err, size_t cap) {
+    uint64_t acc = 0;
+    size_t i = 0;
+    while (i < len) {
+        while (i < len && f[i] == ',') i++;
+        if (i >= len) break;
+        size_t j = i;
+        while (j < len && f[j] != ',') j++;
+        uint64_t b;
+        if (get_range_names(f + i, j - i, min, max, names, &b, err, cap)) {
+            *bits = acc;
+            return -1;
+        }
+        acc |= b;
+        i = j;
+    }
+    *bits = acc;
+    return 0;
+}
+
+int or_get_field(const char *expr, size_t len, unsigned min, unsigned max,
+                 uint64_t *bits, char *err, size_t errcap) {
+    return get_field_names(expr, len, min, max, 0, bits, err, errcap);
+}
+
+/* unicode.IsSpace over UTF-8; returns byte length of the space rune at p, or 0 */
+static size_t space_len(const unsigned char *p, size_t rem) {
+    unsigned char c = p[0];
+    if (c == ' ' || (c >= '\t' && c <= '\r')) return 1;
+    if (c == 0xc2 && rem >= 2 && (p[1] == 0x85 || p[1] == 0xa0)) return 2;
+    if (c == 0xe1 && rem >= 3 && p[1] == 0x9a && p[2] == 0x80) return 3;
+    if (c == 0xe2 && rem >= 3) {
+        if (p[1] == 0x80 && ((p[2] >= 0x80 && p[2] <= 0x8a) || p[2] == 0xa8 ||
+                             p[2] == 0xa9 || p[2] == 0xaf))
+            return 3;
+        if (p[1] == 0x81 && p[2] == 0x9f) return 3;
+    }
+    if (c == 0xe3 && rem >= 3 && p[1] == 0x80 && p[2] == 0x80) return 3;
+    return 0;
+}
+
+/* time.ParseDuration */
+static const struct { const char *u; int64_t ns; } unit_map[] = {
+    {"ns", 1LL}, {"us", 1000LL}, {"\xc2\xb5s", 1000LL}, {"\xce\xbcs", 1000LL},
+    {"ms", 1000000LL}, {"s", NS_PER_SEC}, {"m", 60 * NS_PER_SEC}, {"h", 3600 * NS_PER_SEC}};
+
+int or_parse_duration(const char *s0, size_t len0, int64_t *out, char *err,
+                      size_t cap) {
+    char q[512];
+    go_quote(s0, len0, q, sizeof q);
+    const char *s = s0;
+    size_t n = len0;
+    uint64_t d = 0;
+    int neg = 0;
+    if (n > 0 && (s[0] == '-' || s[0] == '+')) {
+        neg = s[0] == '-';
+        s++;
+        n--;
+    }
+    if (n == 1 && s[0] == '0') { *out = 0; return 0; }
+    if (n == 0) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+    while (n > 0) {
+        uint64_t v = 0, f = 0;
+        double scale = 1;
+        if (!(s[0] == '.' || (s[0] >= '0' && s[0] <= '9'))) {
+            seterr(err, cap, "time: invalid duration %s", q);
+            return -1;
+        }
+        size_t pl = n;
+        /* leadingInt */
+        size_t i = 0;
+        for (; i < n; i++) {
+            char c = s[i];
+            if (c < '0' || c > '9') break;
+            if (v > (1ULL << 63) / 10) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+            v = v * 10 + (uint64_t)(c - '0');
+            if (v > (1ULL << 63)) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+        }
+        s += i; n -= i;
+        int pre = pl != n;
+        int post = 0;
+        if (n > 0 && s[0] == '.') {
+            s++; n--;
+            size_t pl2 = n;
+            int overflow = 0;
+            size_t k = 0;
+            for (; k < n; k++) {
+                char c = s[k];
+                if (c < '0' || c > '9') break;
+                if (overflow) continue;
+                if (f > ((1ULL << 63) - 1) / 10) { overflow = 1; continue; }
+                uint64_t y = f * 10 + (uint64_t)(c - '0');
+                if (y > (1ULL << 63)) { overflow = 1; continue; }
+                f = y;
+                scale *= 10;
+            }
+            s += k; n -= k;
+            post = pl2 != n;
+        }
+        if (!pre && !post) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+        size_t u = 0;
+        for (; u < n; u++) {
+            char c = s[u];
+            if (c == '.' || (c >= '0' && c <= '9')) break;
+        }
+        if (u == 0) { seterr(err, cap, "time: missing unit in duration %s", q); return -1; }
+        int64_t unit = -1;
+        for (size_t k = 0; k < sizeof unit_map / sizeof unit_map[0]; k++) {
+            if (strlen(unit_map[k].u) == u && !memcmp(unit_map[k].u, s, u)) {
+                unit = unit_map[k].ns;
+                break;
+            }
+        }
+        if (unit < 0) {
+            char uq[256];
+            go_quote(s, u, uq, sizeof uq);
+            seterr(err, cap, "time: unknown unit %s in duration %s", uq, q);
+            return -1;
+        }
+        s += u; n -= u;
+        if (v > (1ULL << 63) / (uint64_t)unit) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+        v *= (uint64_t)unit;
+        if (f > 0) {
+            v += (uint64_t)((double)f * ((double)unit / scale));
+            if (v > (1ULL << 63)) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+        }
+        d += v;
+        if (d > (1ULL << 63)) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+    }
+    if (neg) { *out = (int64_t)(0 - d); return 0; }
+    if (d > (1ULL << 63) - 1) { seterr(err, cap, "time: invalid duration %s", q); return -1; }
+    *out = (int64_t)d;
+    return 0;
+}
+
+static const int places[6] = {OR_OPT_SECOND, OR_OPT_MINUTE, OR_OPT_HOUR,
+                              OR_OPT_DOM,    OR_OPT_MONTH,  OR_OPT_DOW};
+static const char *defaults[6] = {"0", "0", "0", "*", "*", "*"};
+
+static int parse_descriptor(const char *spec, size_t len, or_sched *out, char *err,
+                            size_t cap) {
+    memset(out, 0, sizeof *out);
+    or_spec *s = &out->spec;
+    uint64_t all_dom = or_get_bits(1, 31, 1) | OR_STAR_BIT;
+    uint64_t all_mon = or_get_bits(1, 12, 1) | OR_STAR_BIT;
+    uint64_t all_dow = or_get_bits(0, 6, 1) | OR_STAR_BIT;
+    uint64_t all_hour = or_get_bits(0, 23, 1) | OR_STAR_BIT;
+#define IS(lit) (len == strlen(lit) && !memcmp(spec, lit, len))
+    if (IS("@yearly") || IS("@annually")) {
+        s->second = 1; s->minute = 1; s->hour = 1; s->dom = 1ULL << 1;
+        s->month = 1ULL << 1; s->dow = all_dow;
+        return 0;
+    }
+    if (IS("@monthly")) {
+        s->second = 1; s->minute = 1; s->hour = 1; s->dom = 1ULL << 1;
+        s->month = all_mon; s->dow = all_dow;
+        return 0;
+    }
+    if (IS("@weekly")) {
+        s->second = 1; s->minute = 1; s->hour = 1; s->dom = all_dom;
+        s->month = all_mon; s->dow = 1;
+        return 0;
+    }
+    if (IS("@daily") || IS("@midnight")) {
+        s->second = 1; s->minute = 1; s->hour = 1; s->dom = all_dom;
+        s->month = all_mon; s->dow = all_dow;
+        return 0;
+    }
+    if (IS("@hourly")) {
+        s->second = 1; s->minute = 1; s->hour = all_hour; s->dom = all_dom;
+        s->month = all_mon; s->dow = all_dow;
+        return 0;
+    }
+#undef IS
+    const char *every = "@every ";
+    if (len >= 7 && !memcmp(spec, every, 7)) {
+        int64_t d;
+        char derr[600];
+        if (or_parse_duration(spec + 7, len - 7, &d, derr, sizeof derr)) {
+            seterr(err, cap, "Failed to parse duration %.*s: %s", (int)len, spec, derr);
+            return -1;
+        }
+        out->kind = 1;
+        out->delay_ns = or_every(d);
+        return 0;
+    }
+    seterr(err, cap, "Unrecognized descriptor: %.*s", (int)len, spec);
+    return -1;
+}
+
+int or_parse(int options, const char *spec, size_t len, or_sched *out, char *err,
+             size_t cap) {
+    /* NewParser */
+    int optionals = 0;
+    if (options & OR_OPT_DOWOPTIONAL) {
+        options |= OR_OPT_DOW;
+        optionals++;
+    }
+    memset(out, 0, sizeof *out);
+    if (len == 0) {
+        seterr(err, cap, "runtime error: index out of range [0] with length 0");
+        return -2; /* Go panics here; JobRule.Valid guards with ErrNilRule */
+    }
+    if (spec[0] == '@' && (options & OR_OPT_DESCRIPTOR))
+        return parse_descriptor(spec, len, out, err, cap);
+
+    int max = 0;
+    for (int i = 0; i < 6; i++)
+        if (options & places[i]) max++;
+    int min = max - optionals;
+
+    /* strings.Fields */
+    const char *fs[64];
+    size_t fl[64];
+    int count = 0;
+    const unsigned char *p = (const unsigned char *)spec;
+    size_t i = 0;
+    while (i < len) {
+        size_t sl = space_len(p + i, len - i);
+        if (sl) { i += sl; continue; }
+        size_t j = i;
+        while (j < len && !space_len(p + j, len - j)) j++;
+        if (count < 64) { fs[count] = spec + i; fl[count] = j - i; }
+        count++;
+        i = j;
+    }
+    if (count < min || count > max) {
+        if (min == max)
+            seterr(err, cap, "Expected exactly %d fields, found %d: %.*s", min, count,
+                   (int)len, spec);
+        else
+            seterr(err, cap, "Expected %d to %d fields, found %d: %.*s", min, max, count,
+                   (int)len, spec);
+        return -1;
+    }
+    /* expandFields */
+    const char *ef[6];
+    size_t el[6];
+    for (int k = 0; k < 6; k++) { ef[k] = defaults[k]; el[k] = 1; }
+    int nn = 0;
+    for (int k = 0; k < 6; k++) {
+        if (options & places[k]) {
+            ef[k] = fs[nn];
+            el[k] = fl[nn];
+            nn++;
+        }
+        if (nn == count) break;
+    }
+    static const unsigned bmin[6] = {0, 0, 0, 1, 1, 0};
+    static const unsigned bmax[6] = {59, 59, 23, 31, 12, 6};
+    static const int bnames[6] = {0, 0, 0, 0, 1, 2};
+    uint64_t v[6] = {0};
+    for (int k = 0; k < 6; k++) {
+        if (get_field_names(ef[k], el[k], bmin[k], bmax[k], bnames[k], &v[k], err, cap))
+            return -1;
+    }
+    out->kind = 0;
+    out->spec.second = v[0];
+    out->spec.minute = v[1];
+    out->spec.hour = v[2];
+    out->spec.dom = v[3];
+    out->spec.month = v[4];
+    out->spec.dow = v[5];
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* expansion loop + threaded batch                                          */
+/* ------------------------------------------------------------------------ */
+
+int64_t or_expand(const or_sched *s, int64_t t0, int64_t t1, const or_loc *l,
+                  int64_t *out, int64_t cap) {
+    int64_t n = 0;
+    int64_t t = t0;
+    for (;;) {
+        t = or_sched_next(s, t, 0, l);
+        if (t == OR_ZERO_TIME || t > t1) break;
+        if (out && n < cap) out[n] = t;
+        n++;
+    }
+    return n;
+}
+
+typedef struct {
+    const or_sched *s;
+    size_t R;
+    int64_t t0, t1;
+    const or_loc *l;
+    int64_t *counts;
+    const int64_t *offsets;
+    int64_t *times;
+    size_t next;
+    pthread_mutex_t mu;
+} batch_job;
+
+static void *batch_worker(void *arg) {
+    batch_job *b = (batch_job *)arg;
+    const size_t chunk = 64;
+    for (;;) {
+        pthread_mutex_lock(&b->mu);
+        size_t lo = b->next;
+        b->next += chunk;
+        pthread_mutex_unlock(&b->mu);
+        if (lo >= b->R) break;
+        size_t hi = lo + chunk < b->R ? lo + chunk : b->R;
+        for (size_t r = lo; r < hi; r++) {
+            if (b->times) {
+                int64_t cap = b->offsets[r + 1] - b->offsets[r];
+                or_expand(&b->s[r], b->t0, b->t1, b->l, b->times + b->offsets[r], cap);
+            } else {
+                b->counts[r] = or_expand(&b->s[r], b->t0, b->t1, b->l, NULL, 0);
+            }
+        }
+    }
+    return NULL;
+}
+
+static void run_batch(batch_job *b, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t th[512];
+    if (nthreads > 512) nthreads = 512;
+    b->next = 0;
+    pthread_mutex_init(&b->mu, NULL);
+    for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, batch_worker, b);
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&b->mu);
+}
+
+int64_t or_expand_batch(const or_sched *s, size_t R, int64_t t0, int64_t t1,
+                        const or_loc *l, int nthreads, int64_t *offsets,
+                        int64_t *times) {
+    int64_t *counts = (int64_t *)calloc(R ? R : 1, sizeof(int64_t));
+    batch_job b;
+    memset(&b, 0, sizeof b);
+    b.s = s; b.R = R; b.t0 = t0; b.t1 = t1; b.l = l; b.counts = counts;
+    run_batch(&b, nthreads);
+    offsets[0] = 0;
+    for (size_t r = 0; r < R; r++) offsets[r + 1] = offsets[r] + counts[r];
+    free(counts);
+    if (times) {
+        b.times = times;
+        b.offsets = offsets;
+        run_batch(&b, nthreads);
+    }
+    return offsets[R];
+}
+
+/* ------------------------------------------------------------------------ */
+/* rule -> node resolution                                                  */
+/* ------------------------------------------------------------------------ */
+
+static int in_list(const int32_t *a, int64_t lo, int64_t hi, int32_t x) {
+    for (int64_t i = lo; i < hi; i++)
+        if (a[i] == x) return 1;
+    return 0;
+}
+
+/* JobRule.included job.go:274-288 + Group.Included group.go:111-119 */
+static int rule_included(const or_jobset *js, int32_t r, int32_t n) {
+    if (in_list(js->nids, js->nid_off[r], js->nid_off[r + 1], n)) return 1;
+    for (int64_t k = js->gid_off[r]; k < js->gid_off[r + 1]; k++) {
+        int32_t g = js->gids[k];
+        if (g < 0 || g >= js->n_groups || !js->group_exists[g]) continue;
+        if (in_list(js->group_nodes, js->group_off[g], js->group_off[g + 1], n)) return 1;
+    }
+    return 0;
+}
+
+int or_rule_on_node(const or_jobset *js, int mode, int32_t r, int32_t n) {
+    int32_t j = js->rule_job[r];
+    if (js->job_pause[j]) return 0;          /* job.go:593 */
+    if (!rule_included(js, r, n)) return 0;
+    if (mode == 0) return 1;                 /* excludes: no-op, job.go:598-602 */
+    if (mode == 1) return !in_list(js->ex, js->ex_off[r], js->ex_off[r + 1], n);
+    /* mode 2: cumulative over the job's rules up to and including r */
+    int32_t r0 = r;
+    while (r0 > 0 && js->rule_job[r0 - 1] == j) r0--;
+    for (int32_t q = r0; q <= r; q++)
+        if (in_list(js->ex, js->ex_off[q], js->ex_off[q + 1], n)) return 0;
+    return 1;
+}
+
+int or_job_is_run_on(const or_jobset *js, int32_t job, int32_t n) {
+    for (int32_t r = 0; r < js->n_rules; r++) {
+        if (js->rule_job[r] != job) continue;
+        if (rule_included(js, r, n)) return 1;
+    }
+    return 0;
+}
+
+typedef struct { int32_t *v; int64_t n, cap; } ivec;
+static void iv_push(ivec *a, int32_t x) {
+    if (a->n == a->cap) {
+        a->cap = a->cap ? a->cap * 2 : 16;
+        a->v = (int32_t *)realloc(a->v, (size_t)a->cap * sizeof(int32_t));
+    }
+    a->v[a->n++] = x;
+}
+
+int32_t or_job_nodes(const or_jobset *js, int32_t job, int32_t *out, int32_t cap) {
+    ivec nodes = {0}, ex = {0};
+    for (int32_t r = 0; r < js->n_rules; r++) {
+        if (js->rule_job[r] != job) continue;
+        ivec in = {0};
+        for (int64_t k = 0; k < nodes.n; k++) iv_push(&in, nodes.v[k]);
+        for (int64_t k = js->nid_off[r]; k < js->nid_off[r + 1]; k++) iv_push(&in, js->nids[k]);
+        for (int64_t k = js->gid_off[r]; k < js->gid_off[r + 1]; k++) {
+            int32_t g = js->gids[k];
+            if (g < 0 || g >= js->n_groups || !js->group_exists[g]) continue;
+            for (int64_t q = js->group_off[g]; q < js->group_off[g + 1]; q++)
+                iv_push(&in, js->group_nodes[q]);
+        }
+        for (int64_t k = js->ex_off[r]; k < js->ex_off[r + 1]; k++) iv_push(&ex, js->ex[k]);
+        /* SubtractStringArray(in, ex) */
+        for (int64_t k = 0; k < in.n; k++)
+            if (!in_list(ex.v, 0, ex.n, in.v[k])) iv_push(&nodes, in.v[k]);
+        free(in.v);
+    }
+    /* UniqueStringArray: first-seen order */
+    int32_t cnt = 0;
+    ivec uniq = {0};
+    for (int64_t k = 0; k < nodes.n; k++) {
+        if (in_list(uniq.v, 0, uniq.n, nodes.v[k])) continue;
+        iv_push(&uniq, nodes.v[k]);
+        if (cnt < cap && out) out[cnt] = nodes.v[k];
+        cnt++;
+    }
+    free(uniq.v);
+    free(nodes.v);
+    free(ex.v);
+    return cnt;
+}
