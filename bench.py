@@ -1,0 +1,210 @@
+"""Benchmark: fire events materialised/sec for BASELINE.json config 2
+(1M mixed cron rules x 24 h horizon, UTC) per MI355X, weak-scaled over
+job-ID-range shards at N > 1.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+
+A step = one full expansion of the rank's rule shard over the horizon:
+count -> scan -> block map -> closed-form write -> WALK write -> offsets, with
+the specs resident in HBM and the fire times left in HBM.  At N > 1 each step
+also all-gathers the per-rank event totals (global CSR offsets) over RCCL.
+
+Prints one JSON line (rank 0).  See DESIGN.md §Measurement for the roofline
+and CPU-baseline definitions.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SPEC_BYTES = 32          # packed SoA spec per rule in HBM
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def pmc_traffic(path, kernel, rules, events):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
+    (profiles/*.json written by tools/pmc_traffic.py), if it was measured on
+    the same workload."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+        if d.get("rules") == rules and d.get("events") == events:
+            return float(k["hbm_bytes_per_launch"])
+    except Exception:
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rules", type=int, default=1_000_000, help="rules per GPU")
+    ap.add_argument("--horizon", type=int, default=86400)
+    ap.add_argument("--cpu-sample", type=int, default=40_000,
+                    help="rules in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    import numpy as np
+
+    from cronsun_amd import cron, synth
+    from cronsun_amd.engine import Engine
+
+    R, H = args.rules, args.horizon
+    t0 = synth.T0_2026
+    t1 = t0 + H
+    eng = Engine(local)
+    log(f"[rank {rank}] generating {R} rules (job-ID shard {rank})")
+    specs = synth.spec_mix(R, seed=0x5EED + rank)
+    arr, status = cron.parse_batch(specs, threads=16)
+    assert (status == 0).all()
+    sp = eng.upload_c(arr, R)
+    utc = cron.UTC()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    dev = torch.device("cuda", local)
+    tot = torch.zeros(world, dtype=torch.int64, device=dev)
+
+    def step():
+        E = eng.expand_device(sp, utc, t0, t1)
+        if world > 1:
+            # global CSR offsets of the job-ID-range shards (RCCL allgather)
+            mine = torch.tensor([E], dtype=torch.int64, device=dev)
+            dist.all_gather_into_tensor(tot, mine)
+        return E
+
+    for _ in range(args.warmup):
+        E = step()
+    log(f"[rank {rank}] warmup done: {E} events/step")
+    barrier()
+    torch.cuda.synchronize()
+    start = time.perf_counter()
+    kts = []
+    for _ in range(args.steps):
+        E = step()
+        kts.append(eng.kernel_times())
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - start
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    ev = torch.tensor([E], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(ev, op=dist.ReduceOp.SUM)
+    elapsed = float(el.item())
+    total_events = int(ev.item())
+
+    kt = np.mean(np.array(kts), axis=0)  # count, scan, map, write_cf, write_walk, offsets (ms)
+    algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
+    write_s = kt[3] / 1e3
+    achieved = algo_bytes / write_s / 1e9 if write_s > 0 else 0.0
+    ms_step = elapsed / args.steps * 1e3
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    cpu = None
+    if world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(specs[:args.cpu_sample], t0, t1, args.cpu_threads)
+
+    traffic = pmc_traffic(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"), "k_write_cf", R, E)
+    out = {
+        "metric": "fire events materialised/sec (1M rules × 24h) + HBM GB/s at 1/2/4/8 GPU",
+        "value": total_events * args.steps / elapsed,
+        "unit": "events/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded spec mix, SURVEY.md §8d config 2; parsed on host, resident in HBM)",
+        "config": {
+            "workload": "config 2: 1M mixed cron rules x 24h horizon, UTC, per GPU (job-ID-range shards)",
+            "rules_per_gpu": R,
+            "horizon_s": H,
+            "t0": t0,
+            "zone": "UTC",
+            "events_per_gpu_step": E,
+            "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard event totals)",
+        },
+        "hbm_gbps_step": algo_bytes * world / (elapsed / args.steps) / 1e9,
+        "kernel_ms": {"count": kt[0], "scan": kt[1], "block_map": kt[2], "write_cf": kt[3],
+                      "write_walk": kt[4], "offsets": kt[5]},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "k_write_cf",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBPS,
+            "traffic": traffic,
+            "algo_bytes_per_launch": algo_bytes,
+        },
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(specs, t0, t1, threads):
+    """The oracle's literal Next loop (reference semantics, port of
+    spec.go:55-158 + Go time) on this host's cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    threads = threads or min(16, os.cpu_count() or 1)
+    tp = time.perf_counter()
+    scheds = [O.parse(s)[0] for s in specs]
+    arr = O.sched_array(scheds)
+    parse_s = time.perf_counter() - tp
+    loc = O.Loc("UTC")
+    ts = time.perf_counter()
+    off, _ = O.expand_batch(arr, t0, t1, loc, threads=threads, with_times=True)
+    dt = time.perf_counter() - ts
+    ev = int(off[-1])
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"first {len(specs)} of the same rules x {t1 - t0}s horizon, UTC "
+                      f"({ev} events, {dt:.2f}s; parse excluded, +{parse_s:.2f}s parse)",
+            "value_incl_parse": ev / (dt + parse_s), "cpu_model": cpu_model,
+            "go_toolchain": "absent on the box image (oracle C port timed instead)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,168 @@
+"""ctypes binding of libcronsun_gpu.so (the C-ABI in include/cronsun_gpu.h).
+
+There is no CPU fallback: if the library is missing this module raises, and
+compute calls fail with CG_ENODEV on a host without an MI355X.
+"""
+import ctypes as C
+import importlib.util
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcronsun_gpu.so")
+
+CG_OK = 0
+CG_EINVAL = -1
+CG_ENOMEM = -2
+CG_EHIP = -3
+CG_ECAPACITY = -4
+CG_EPARSE = -5
+CG_ERANGE = -6
+CG_ENODEV = -7
+CG_EPANIC = -8
+ZERO_TIME = -62135596800
+MAX_HORIZON = 366 * 86400
+
+PARSE_SECOND, PARSE_MINUTE, PARSE_HOUR, PARSE_DOM = 1, 2, 4, 8
+PARSE_MONTH, PARSE_DOW, PARSE_DOW_OPTIONAL, PARSE_DESCRIPTOR = 16, 32, 64, 128
+PARSE_DEFAULT = 1 | 2 | 4 | 8 | 16 | 64 | 128
+PARSE_STANDARD = 2 | 4 | 8 | 16 | 32 | 128
+
+EXCLUDE_NONE, EXCLUDE_RULE, EXCLUDE_CUMULATIVE = 0, 1, 2
+
+
+class CgError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+        self.msg = msg
+
+
+class cg_schedule(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("reserved", C.c_int32),
+                ("second", C.c_uint64), ("minute", C.c_uint64), ("hour", C.c_uint64),
+                ("dom", C.c_uint64), ("month", C.c_uint64), ("dow", C.c_uint64),
+                ("delay_ns", C.c_int64)]
+
+
+class cg_spec_soa(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in
+                ("second", "minute", "hour", "dom", "month", "dow", "delay_ns")]
+
+
+class cg_csr(C.Structure):
+    _fields_ = [("offsets", C.c_void_p), ("times", C.c_void_p),
+                ("times_cap", C.c_int64), ("n_events", C.c_int64)]
+
+
+class cg_rules_in(C.Structure):
+    _fields_ = [("n_nodes", C.c_int32), ("n_groups", C.c_int32), ("n_rules", C.c_int32),
+                ("n_jobs", C.c_int32)] + [(n, C.c_void_p) for n in (
+                    "group_off", "group_nodes", "group_exists", "rule_job", "nid_off", "nids",
+                    "gid_off", "gids", "ex_off", "ex", "job_pause")]
+
+
+class cg_node_csr(C.Structure):
+    _fields_ = [("node_off", C.c_void_p), ("time", C.c_void_p), ("rule", C.c_void_p),
+                ("cap", C.c_int64), ("n_events", C.c_int64), ("nnz", C.c_int64)]
+
+
+def _preload_torch_hip():
+    """Make the process's HIP runtime the one PyTorch-ROCm ships (same SONAME
+    libamdhip64.so.7), so torch and this library never load two runtimes."""
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    p = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(p):
+        C.CDLL(p, mode=C.RTLD_GLOBAL)
+
+
+def _declare(L):
+    vp, i32, i64, u64, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_size_t
+    P = C.POINTER
+    sigs = {
+        "cg_abi_version": ([], C.c_int),
+        "cg_last_error": ([], C.c_char_p),
+        "cg_device_count": ([], C.c_int),
+        "cg_parse": ([C.c_int, C.c_char_p, sz, P(cg_schedule), C.c_char_p, sz], C.c_int),
+        "cg_parse_batch": ([C.c_int, vp, vp, sz, vp, vp, C.c_int], C.c_int),
+        "cg_get_range": ([C.c_char_p, sz, C.c_uint, C.c_uint, C.c_int, P(u64), C.c_char_p, sz], C.c_int),
+        "cg_get_field": ([C.c_char_p, sz, C.c_uint, C.c_uint, C.c_int, P(u64), C.c_char_p, sz], C.c_int),
+        "cg_get_bits": ([C.c_uint, C.c_uint, C.c_uint], u64),
+        "cg_every": ([i64], i64),
+        "cg_parse_duration": ([C.c_char_p, sz, P(i64)], C.c_int),
+        "cg_zone_from_tzif": ([C.c_char_p, sz, P(vp)], C.c_int),
+        "cg_zone_fixed": ([i32, P(vp)], C.c_int),
+        "cg_zone_utc": ([P(vp)], C.c_int),
+        "cg_zone_free": ([vp], None),
+        "cg_zone_offset": ([vp, i64, P(i32)], C.c_int),
+        "cg_zone_table": ([vp, i64, i64, vp, vp, C.c_int], C.c_int),
+        "cg_init": ([C.c_int, P(vp)], C.c_int),
+        "cg_destroy": ([vp], None),
+        "cg_sync": ([vp], C.c_int),
+        "cg_specs_upload": ([vp, P(cg_spec_soa), sz, P(vp)], C.c_int),
+        "cg_specs_upload_schedules": ([vp, vp, sz, P(vp)], C.c_int),
+        "cg_specs_slice": ([vp, sz, sz, P(vp)], C.c_int),
+        "cg_specs_count": ([vp], sz),
+        "cg_specs_free": ([vp], None),
+        "cg_next_batch": ([vp, vp, vp, vp, vp], C.c_int),
+        "cg_expand": ([vp, vp, vp, i64, i64, P(cg_csr)], C.c_int),
+        "cg_expand_device": ([vp, vp, vp, i64, i64, P(i64)], C.c_int),
+        "cg_result_device": ([vp, P(vp), P(vp), P(i64)], C.c_int),
+        "cg_result_copy_times": ([vp, i64, i64, vp], C.c_int),
+        "cg_result_copy_offsets": ([vp, vp], C.c_int),
+        "cg_last_kernel_times": ([vp, P(C.c_float), C.c_int], C.c_int),
+        "cg_expand_per_node": ([vp, vp, vp, i64, i64, P(cg_rules_in), C.c_int, P(cg_node_csr)], C.c_int),
+        "cg_expand_per_node_device": ([vp, vp, vp, i64, i64, P(cg_rules_in), C.c_int, P(i64), P(i64)], C.c_int),
+        "cg_node_result_device": ([vp, P(vp), P(vp), P(vp), P(i64)], C.c_int),
+        "cg_node_counts_to_device": ([vp, vp], C.c_int),
+        "cg_rule_nodes": ([vp, P(cg_rules_in), C.c_int, vp, vp, i64, P(i64)], C.c_int),
+        "cg_jobset_new": ([P(vp)], C.c_int),
+        "cg_jobset_free": ([vp], None),
+        "cg_jobset_add_group": ([vp, C.c_char_p, vp, sz], C.c_int),
+        "cg_jobset_add_job": ([vp, C.c_char_p, C.c_int], C.c_int),
+        "cg_jobset_add_rule": ([vp, C.c_char_p, vp, sz, vp, sz, vp, sz], C.c_int),
+        "cg_jobset_rules": ([vp, P(cg_rules_in)], C.c_int),
+        "cg_jobset_node_index": ([vp, C.c_char_p], i32),
+        "cg_jobset_node_id": ([vp, i32], C.c_char_p),
+        "cg_jobset_cmds": ([vp, i32, C.c_char_p, vp, i32], i32),
+        "cg_jobset_is_run_on": ([vp, i32, C.c_char_p], C.c_int),
+        "cg_jobset_job_nodes": ([vp, i32, vp, i32], i32),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return list(sigs)
+
+
+_L = None
+SYMBOLS = []
+
+
+def lib():
+    """The loaded library.  Raises if it has not been built."""
+    global _L, SYMBOLS
+    if _L is not None:
+        return _L
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C cronsun_amd/csrc` (there is no CPU fallback)")
+    _preload_torch_hip()
+    L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    SYMBOLS = _declare(L)
+    if L.cg_abi_version() != 1:
+        raise ImportError("libcronsun_gpu ABI mismatch")
+    _L = L
+    return L
+
+
+def check(rc):
+    if rc < 0:
+        raise CgError(rc, (lib().cg_last_error() or b"").decode(errors="replace"))
+    return rc
+
+
+def last_error():
+    return (lib().cg_last_error() or b"").decode(errors="replace")

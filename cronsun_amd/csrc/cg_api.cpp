@@ -1,0 +1,573 @@
+// cg_api.cpp -- the C-ABI of include/cronsun_gpu.h: contexts, device memory,
+// zones, spec upload, Next batches and the expansion pipeline.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/cronsun_gpu.h"
+#include "cg_api_internal.h"
+#include "cg_kernels.h"
+#include "cg_parse.h"
+#include "cg_zone.h"
+
+using namespace cg;
+
+namespace {
+thread_local std::string g_err;
+}
+
+int cg_fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int cg_hip_check(hipError_t e, const char* what) {
+  if (e == hipSuccess) return CG_OK;
+  return cg_fail(e == hipErrorOutOfMemory ? CG_ENOMEM : CG_EHIP,
+                 std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIPCHK(x)                                   \
+  do {                                              \
+    int _rc = cg_hip_check((x), #x);                \
+    if (_rc != CG_OK) return _rc;                   \
+  } while (0)
+
+struct cg_zone {
+  ZoneRules rules;
+  uint64_t serial;
+};
+
+static uint64_t next_serial() {
+  static std::mutex m;
+  static uint64_t s = 0;
+  std::lock_guard<std::mutex> g(m);
+  return ++s;
+}
+
+extern "C" {
+
+int cg_abi_version(void) { return CG_ABI_VERSION; }
+
+const char* cg_last_error(void) { return g_err.c_str(); }
+
+int cg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  int ok = 0;
+  for (int i = 0; i < n; i++) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, i) != hipSuccess) continue;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) == 0) ok++;
+  }
+  return ok;
+}
+
+// ------------------------------------------------------------------ parse
+static void fill_schedule(const Schedule& s, cg_schedule* out) {
+  std::memset(out, 0, sizeof *out);
+  out->kind = s.kind;
+  out->second = s.second;
+  out->minute = s.minute;
+  out->hour = s.hour;
+  out->dom = s.dom;
+  out->month = s.month;
+  out->dow = s.dow;
+  out->delay_ns = s.delay_ns;
+}
+
+int cg_parse(int options, const char* spec, size_t len, cg_schedule* out, char* err,
+             size_t err_cap) {
+  if (!out || (!spec && len)) return cg_fail(CG_EINVAL, "cg_parse: null argument");
+  Schedule s;
+  std::string e;
+  int rc = parse(options, std::string_view(spec ? spec : "", len), &s, &e);
+  if (rc != 0) {
+    if (err && err_cap) {
+      std::strncpy(err, e.c_str(), err_cap - 1);
+      err[err_cap - 1] = 0;
+    }
+    return cg_fail(rc == -2 ? CG_EPANIC : CG_EPARSE, e);
+  }
+  fill_schedule(s, out);
+  return CG_OK;
+}
+
+int cg_parse_batch(int options, const char* const* specs, const size_t* lens, size_t n,
+                   cg_schedule* out, int32_t* status, int nthreads) {
+  if (n && (!specs || !lens || !out || !status)) return cg_fail(CG_EINVAL, "cg_parse_batch: null");
+  if (nthreads < 1) nthreads = 1;
+  if (size_t(nthreads) > n / 1024 + 1) nthreads = int(n / 1024 + 1);
+  auto work = [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; i++) {
+      Schedule s;
+      std::string e;
+      int rc = parse(options, std::string_view(specs[i] ? specs[i] : "", lens[i]), &s, &e);
+      if (rc == 0) {
+        fill_schedule(s, &out[i]);
+        status[i] = CG_OK;
+      } else {
+        std::memset(&out[i], 0, sizeof out[i]);
+        status[i] = rc == -2 ? CG_EPANIC : CG_EPARSE;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  size_t chunk = (n + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; t++) {
+    size_t lo = t * chunk, hi = std::min(n, lo + chunk);
+    if (lo >= hi) break;
+    th.emplace_back(work, lo, hi);
+  }
+  for (auto& x : th) x.join();
+  return CG_OK;
+}
+
+static int range_common(bool field, const char* expr, size_t len, unsigned min, unsigned max,
+                        int names, uint64_t* bits, char* err, size_t err_cap) {
+  if (!bits || (!expr && len)) return cg_fail(CG_EINVAL, "cg_get_range: null");
+  std::string e;
+  std::string_view v(expr ? expr : "", len);
+  int rc = field ? get_field(v, min, max, names, bits, &e) : get_range(v, min, max, names, bits, &e);
+  if (rc) {
+    if (err && err_cap) {
+      std::strncpy(err, e.c_str(), err_cap - 1);
+      err[err_cap - 1] = 0;
+    }
+    return cg_fail(CG_EPARSE, e);
+  }
+  return CG_OK;
+}
+
+int cg_get_range(const char* expr, size_t len, unsigned min, unsigned max, int names,
+                 uint64_t* bits, char* err, size_t err_cap) {
+  return range_common(false, expr, len, min, max, names, bits, err, err_cap);
+}
+
+int cg_get_field(const char* expr, size_t len, unsigned min, unsigned max, int names,
+                 uint64_t* bits, char* err, size_t err_cap) {
+  return range_common(true, expr, len, min, max, names, bits, err, err_cap);
+}
+
+uint64_t cg_get_bits(unsigned min, unsigned max, unsigned step) { return get_bits(min, max, step); }
+
+int64_t cg_every(int64_t d) { return every(d); }
+
+int cg_parse_duration(const char* s, size_t len, int64_t* out) {
+  if (!out) return cg_fail(CG_EINVAL, "cg_parse_duration: null");
+  std::string e;
+  if (parse_duration(std::string_view(s ? s : "", len), out, &e)) return cg_fail(CG_EPARSE, e);
+  return CG_OK;
+}
+
+// ------------------------------------------------------------------ zones
+int cg_zone_from_tzif(const uint8_t* data, size_t len, cg_zone** out) {
+  if (!data || !out) return cg_fail(CG_EINVAL, "cg_zone_from_tzif: null");
+  ZoneRules r;
+  std::string e;
+  if (!zone_from_tzif(data, len, &r, &e)) return cg_fail(CG_EINVAL, "TZif: " + e);
+  *out = new cg_zone{std::move(r), next_serial()};
+  return CG_OK;
+}
+
+int cg_zone_fixed(int32_t off, cg_zone** out) {
+  if (!out) return cg_fail(CG_EINVAL, "cg_zone_fixed: null");
+  *out = new cg_zone{zone_fixed(off), next_serial()};
+  return CG_OK;
+}
+
+int cg_zone_utc(cg_zone** out) {
+  if (!out) return cg_fail(CG_EINVAL, "cg_zone_utc: null");
+  *out = new cg_zone{zone_utc(), next_serial()};
+  return CG_OK;
+}
+
+void cg_zone_free(cg_zone* z) { delete z; }
+
+int cg_zone_offset(const cg_zone* z, int64_t t, int32_t* off) {
+  if (!z || !off) return cg_fail(CG_EINVAL, "cg_zone_offset: null");
+  *off = z->rules.offset(t);
+  return CG_OK;
+}
+
+int cg_zone_table(const cg_zone* z, int64_t lo, int64_t hi, int64_t* when, int32_t* off, int cap) {
+  if (!z) return cg_fail(CG_EINVAL, "cg_zone_table: null");
+  ZoneTable t = build_table(z->rules, lo, hi);
+  int n = int(t.when.size());
+  for (int i = 0; i < n && i < cap; i++) {
+    if (when) when[i] = t.when[i];
+    if (off) off[i] = t.off[i];
+  }
+  return n;
+}
+
+// ---------------------------------------------------------------- context
+int cg_init(int device, cg_ctx** out) {
+  if (!out) return cg_fail(CG_EINVAL, "cg_init: null");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+    return cg_fail(CG_ENODEV, "no HIP device visible (this engine has no CPU fallback)");
+  if (device < 0 || device >= n) return cg_fail(CG_ENODEV, "device index out of range");
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return cg_fail(CG_ENODEV, std::string("device is ") + prop.gcnArchName + ", need gfx950");
+  HIPCHK(hipSetDevice(device));
+  cg_ctx* c = new cg_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return cg_fail(CG_EHIP, "hipStreamCreate failed");
+  }
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  *out = c;
+  return CG_OK;
+}
+
+void cg_destroy(cg_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->st);
+  c->free_all();
+  for (auto& e : c->ev) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(c->st);
+  delete c;
+}
+
+int cg_sync(cg_ctx* c) {
+  if (!c) return cg_fail(CG_EINVAL, "cg_sync: null");
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return CG_OK;
+}
+
+// ------------------------------------------------------------------ specs
+static int pack_spec(const cg_schedule& s, DSpec* d) {
+  std::memset(d, 0, sizeof *d);
+  if (s.kind == 1) {
+    if (s.delay_ns <= 0 || s.delay_ns % 1000000000LL != 0)
+      return cg_fail(CG_EINVAL,
+                     "ConstantDelaySchedule.Delay must be a positive whole number of seconds "
+                     "(cron.Every guarantees this)");
+    d->kind = KIND_EVERY;
+    d->sec = uint64_t(s.delay_ns / 1000000000LL);
+    return CG_OK;
+  }
+  if (s.kind != 0) return cg_fail(CG_EINVAL, "unknown schedule kind");
+  d->kind = KIND_SPEC;
+  d->sec = s.second & 0x0FFFFFFFFFFFFFFFull;
+  d->min = s.minute & 0x0FFFFFFFFFFFFFFFull;
+  d->hour = uint32_t(s.hour & 0xFFFFFFu);
+  d->dom = uint32_t(s.dom & 0xFFFFFFFEu) | uint32_t((s.dom >> 63) & 1u);
+  d->mondow = uint32_t(s.month & 0x1FFEu) | (uint32_t(s.dow & 0x7Fu) << 16) |
+              (uint32_t((s.dow >> 63) & 1u) << 23);
+  return CG_OK;
+}
+
+static int upload_packed(cg_ctx* c, const std::vector<DSpec>& h, cg_specs** out) {
+  HIPCHK(hipSetDevice(c->device));
+  cg_specs* s = new cg_specs();
+  s->ctx = c;
+  s->n = h.size();
+  s->owner = true;
+  if (!h.empty()) {
+    hipError_t e = hipMalloc(&s->d, h.size() * sizeof(DSpec));
+    if (e != hipSuccess) {
+      delete s;
+      return cg_hip_check(e, "hipMalloc(specs)");
+    }
+    e = hipMemcpy(s->d, h.data(), h.size() * sizeof(DSpec), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(s->d);
+      delete s;
+      return cg_hip_check(e, "hipMemcpy(specs)");
+    }
+  }
+  *out = s;
+  return CG_OK;
+}
+
+int cg_specs_upload(cg_ctx* c, const cg_spec_soa* soa, size_t n, cg_specs** out) {
+  if (!c || !soa || !out) return cg_fail(CG_EINVAL, "cg_specs_upload: null");
+  std::vector<DSpec> h(n);
+  for (size_t i = 0; i < n; i++) {
+    cg_schedule s;
+    std::memset(&s, 0, sizeof s);
+    if (soa->delay_ns && soa->delay_ns[i] > 0) {
+      s.kind = 1;
+      s.delay_ns = soa->delay_ns[i];
+    } else {
+      s.second = soa->second ? soa->second[i] : 0;
+      s.minute = soa->minute ? soa->minute[i] : 0;
+      s.hour = soa->hour ? soa->hour[i] : 0;
+      s.dom = soa->dom ? soa->dom[i] : 0;
+      s.month = soa->month ? soa->month[i] : 0;
+      s.dow = soa->dow ? soa->dow[i] : 0;
+    }
+    int rc = pack_spec(s, &h[i]);
+    if (rc) return rc;
+  }
+  return upload_packed(c, h, out);
+}
+
+int cg_specs_upload_schedules(cg_ctx* c, const cg_schedule* s, size_t n, cg_specs** out) {
+  if (!c || (!s && n) || !out) return cg_fail(CG_EINVAL, "cg_specs_upload_schedules: null");
+  std::vector<DSpec> h(n);
+  for (size_t i = 0; i < n; i++) {
+    int rc = pack_spec(s[i], &h[i]);
+    if (rc) return rc;
+  }
+  return upload_packed(c, h, out);
+}
+
+int cg_specs_slice(cg_specs* p, size_t first, size_t count, cg_specs** out) {
+  if (!p || !out) return cg_fail(CG_EINVAL, "cg_specs_slice: null");
+  if (first > p->n || count > p->n - first) return cg_fail(CG_EINVAL, "slice out of range");
+  cg_specs* s = new cg_specs();
+  s->ctx = p->ctx;
+  s->d = p->d + first;
+  s->n = count;
+  s->owner = false;
+  *out = s;
+  return CG_OK;
+}
+
+size_t cg_specs_count(const cg_specs* s) { return s ? s->n : 0; }
+
+void cg_specs_free(cg_specs* s) {
+  if (!s) return;
+  if (s->owner && s->d) {
+    (void)hipSetDevice(s->ctx->device);
+    (void)hipFree(s->d);
+  }
+  delete s;
+}
+
+}  // extern "C"
+
+// ----------------------------------------------------------- plan upload
+int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* pa) {
+  const int32_t zn = int32_t(plan.table.when.size());
+  const int32_t G = int32_t(plan.segs.size());
+  const int32_t nd = int32_t(plan.dtab.size());
+  if (G > 64) return cg_fail(CG_ERANGE, "plan has more than 64 segments (horizon too long)");
+  // one packed upload: when | off | segs | dtab
+  size_t o_when = 0, o_off = o_when + size_t(zn) * 8;
+  size_t o_seg = (o_off + size_t(zn) * 4 + 15) / 16 * 16;
+  size_t o_dt = o_seg + size_t(G) * sizeof(Segment);
+  size_t bytes = o_dt + size_t(nd) * 4 + 16;
+  std::vector<char>& h = c->plan_host;
+  h.assign(bytes, 0);
+  std::memcpy(h.data() + o_when, plan.table.when.data(), size_t(zn) * 8);
+  std::memcpy(h.data() + o_off, plan.table.off.data(), size_t(zn) * 4);
+  if (G) std::memcpy(h.data() + o_seg, plan.segs.data(), size_t(G) * sizeof(Segment));
+  if (nd) std::memcpy(h.data() + o_dt, plan.dtab.data(), size_t(nd) * 4);
+  int rc = c->plan_dev.ensure(bytes);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(c->plan_dev.p, h.data(), bytes, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));  // h is reused by the next call
+  char* base = c->plan_dev.p;
+  pa->zwhen = reinterpret_cast<const int64_t*>(base + o_when);
+  pa->zoff = reinterpret_cast<const int32_t*>(base + o_off);
+  pa->segs = reinterpret_cast<const Segment*>(base + o_seg);
+  pa->dtab = reinterpret_cast<const uint32_t*>(base + o_dt);
+  pa->zn = zn;
+  pa->G = G;
+  pa->nd = nd;
+  pa->pad = 0;
+  pa->t0 = t0;
+  pa->t1 = t1;
+  if (plan_lds_bytes(*pa) > 60 * 1024)
+    return cg_fail(CG_ERANGE, "zone table too large for LDS staging (narrow the time range)");
+  return CG_OK;
+}
+
+extern "C" {
+
+// ------------------------------------------------------------------ Next()
+int cg_next_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int64_t* t_in,
+                  int64_t* t_out) {
+  if (!c || !s || !z || (s->n && (!t_in || !t_out))) return cg_fail(CG_EINVAL, "cg_next_batch: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t n = int64_t(s->n);
+  if (n == 0) return CG_OK;
+  int64_t lo = t_in[0], hi = t_in[0];
+  for (int64_t i = 1; i < n; i++) {
+    lo = std::min(lo, t_in[i]);
+    hi = std::max(hi, t_in[i]);
+  }
+  const int64_t kDay = 86400;
+  if (lo < -(int64_t(1) << 45) || hi > (int64_t(1) << 45))
+    return cg_fail(CG_ERANGE, "input time outside +-1.1M years");
+  Plan plan;
+  // Next walks back to the month start of t+1 and forward at most ~6 years
+  plan.table = build_table(z->rules, lo - 64 * kDay, hi + (6 * 366 + 64) * kDay);
+  PlanArgs pa;
+  int rc = upload_plan(c, plan, 0, 0, &pa);
+  if (rc) return rc;
+  if ((rc = c->nb_in.ensure(n))) return rc;
+  if ((rc = c->nb_out.ensure(n))) return rc;
+  HIPCHK(hipMemcpyAsync(c->nb_in.p, t_in, n * 8, hipMemcpyHostToDevice, c->st));
+  launch_next_batch(s->d, n, pa, c->nb_in.p, c->nb_out.p, c->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(t_out, c->nb_out.p, n * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return CG_OK;
+}
+
+}  // extern "C"
+
+// --------------------------------------------------------------- expansion
+int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                         int64_t* n_events) {
+  HIPCHK(hipSetDevice(c->device));
+  if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
+    return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON");
+  const int64_t R = int64_t(s->n);
+  int rc;
+  // plan (cached across identical calls)
+  if (!(c->plan_valid && c->plan_zone == z->serial && c->plan_t0 == t0 && c->plan_t1 == t1)) {
+    c->plan = build_plan(z->rules, t0, t1);
+    if ((rc = upload_plan(c, c->plan, t0, t1, &c->pa))) {
+      c->plan_valid = false;
+      return rc;
+    }
+    c->plan_valid = true;
+    c->plan_zone = z->serial;
+    c->plan_t0 = t0;
+    c->plan_t1 = t1;
+  }
+  const PlanArgs& pa = c->pa;
+  const int64_t G = pa.G;
+  c->last_R = R;
+  c->last_G = G;
+  for (float& x : c->kt) x = 0;
+  if ((rc = c->offsets.ensure(R + 1))) return rc;
+  if (R == 0 || G == 0) {
+    HIPCHK(hipMemsetAsync(c->offsets.p, 0, (R + 1) * 8, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    c->last_E = 0;
+    *n_events = 0;
+    return CG_OK;
+  }
+  const int64_t nruns = R * G;
+  if ((rc = c->run_anchor.ensure(nruns))) return rc;
+  if ((rc = c->run_count.ensure(nruns))) return rc;
+  if ((rc = c->run_dmask.ensure(nruns))) return rc;
+  if ((rc = c->run_off.ensure(nruns + 1))) return rc;
+  if ((rc = c->scan_tmp.ensure(scan_temp_bytes(nruns)))) return rc;
+
+  if ((rc = c->stuck.ensure(1))) return rc;
+  HIPCHK(hipMemsetAsync(c->stuck.p, 0xFF, sizeof(unsigned long long), c->st));
+  (void)hipEventRecord(c->ev[0], c->st);
+  launch_count(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->stuck.p, c->st);
+  (void)hipEventRecord(c->ev[1], c->st);
+  launch_scan(c->run_count.p, c->run_off.p, nruns, c->scan_tmp.p, c->st);
+  (void)hipEventRecord(c->ev[2], c->st);
+  HIPCHK(hipGetLastError());
+  int64_t E = 0;
+  unsigned long long stuck = 0;
+  HIPCHK(hipMemcpyAsync(&E, c->run_off.p + nruns, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(&stuck, c->stuck.p, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (stuck != ~0ULL)
+    return cg_fail(CG_ERANGE, "rule " + std::to_string(stuck) +
+                                  ": the reference Next loop never terminates inside this horizon (Next "
+                                  "does not return, or returns a time <= its input and cycles)");
+  const int64_t nblocks = (E + kWriteChunk - 1) / kWriteChunk;
+  if ((rc = c->times.ensure(std::max<int64_t>(E, 1)))) return rc;
+  if ((rc = c->block_run.ensure(nblocks + 1))) return rc;
+  bool has_walk = false;
+  for (const Segment& sg : c->plan.segs) has_walk |= sg.kind != 0;
+  (void)hipEventRecord(c->ev[3], c->st);
+  if (E > 0) launch_block_map(c->run_off.p, nruns, nblocks, c->block_run.p, c->st);
+  (void)hipEventRecord(c->ev[4], c->st);
+  if (E > 0)
+    launch_write_cf(s->d, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->run_off.p,
+                    nruns, c->block_run.p, nblocks, E, c->times.p, c->st);
+  (void)hipEventRecord(c->ev[5], c->st);
+  if (E > 0 && has_walk)
+    launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_off.p, c->times.p,
+                      c->st);
+  (void)hipEventRecord(c->ev[6], c->st);
+  launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->st);
+  (void)hipEventRecord(c->ev[7], c->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipStreamSynchronize(c->st));
+  (void)hipEventElapsedTime(&c->kt[0], c->ev[0], c->ev[1]);
+  (void)hipEventElapsedTime(&c->kt[1], c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&c->kt[2], c->ev[3], c->ev[4]);
+  (void)hipEventElapsedTime(&c->kt[3], c->ev[4], c->ev[5]);
+  (void)hipEventElapsedTime(&c->kt[4], c->ev[5], c->ev[6]);
+  (void)hipEventElapsedTime(&c->kt[5], c->ev[6], c->ev[7]);
+  c->last_E = E;
+  *n_events = E;
+  return CG_OK;
+}
+
+extern "C" {
+
+int cg_expand_device(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                     int64_t* n_events) {
+  if (!c || !s || !z || !n_events) return cg_fail(CG_EINVAL, "cg_expand_device: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  return expand_device_locked(c, s, z, t0, t1, n_events);
+}
+
+int cg_expand(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+              cg_csr* out) {
+  if (!c || !s || !z || !out) return cg_fail(CG_EINVAL, "cg_expand: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  int64_t E = 0;
+  int rc = expand_device_locked(c, s, z, t0, t1, &E);
+  if (rc) return rc;
+  out->n_events = E;
+  if (out->offsets)
+    HIPCHK(hipMemcpy(out->offsets, c->offsets.p, (s->n + 1) * 8, hipMemcpyDeviceToHost));
+  if (out->times) {
+    if (out->times_cap < E) return cg_fail(CG_ECAPACITY, "times buffer too small; see n_events");
+    if (E) HIPCHK(hipMemcpy(out->times, c->times.p, E * 8, hipMemcpyDeviceToHost));
+  }
+  return CG_OK;
+}
+
+int cg_result_device(cg_ctx* c, const int64_t** d_off, const int64_t** d_times, int64_t* n) {
+  if (!c) return cg_fail(CG_EINVAL, "cg_result_device: null");
+  if (d_off) *d_off = c->offsets.p;
+  if (d_times) *d_times = c->times.p;
+  if (n) *n = c->last_E;
+  return CG_OK;
+}
+
+int cg_result_copy_times(cg_ctx* c, int64_t first, int64_t count, int64_t* host) {
+  if (!c || (count && !host)) return cg_fail(CG_EINVAL, "cg_result_copy_times: null");
+  if (first < 0 || count < 0 || first + count > c->last_E)
+    return cg_fail(CG_EINVAL, "range outside the last result");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  if (count) HIPCHK(hipMemcpy(host, c->times.p + first, count * 8, hipMemcpyDeviceToHost));
+  return CG_OK;
+}
+
+int cg_result_copy_offsets(cg_ctx* c, int64_t* host) {
+  if (!c || !host) return cg_fail(CG_EINVAL, "cg_result_copy_offsets: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipMemcpy(host, c->offsets.p, (c->last_R + 1) * 8, hipMemcpyDeviceToHost));
+  return CG_OK;
+}
+
+int cg_last_kernel_times(cg_ctx* c, float* ms, int n) {
+  if (!c || !ms) return cg_fail(CG_EINVAL, "cg_last_kernel_times: null");
+  int k = std::min(n, int(sizeof(c->kt) / sizeof(c->kt[0])));
+  for (int i = 0; i < k; i++) ms[i] = c->kt[i];
+  return k;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// cg_api_internal.h -- context/specs objects behind the C-ABI handles.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cronsun_gpu.h"
+#include "cg_kernels.h"
+#include "cg_zone.h"
+
+int cg_fail(int code, const std::string& msg);
+int cg_hip_check(hipError_t e, const char* what);
+
+// Grow-only device buffer (grows by 1.25x so repeated calls settle).
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t n) {
+    if (n <= cap) return CG_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    size_t want = std::max(n, cap + cap / 4);
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e != hipSuccess) {
+      // retry at the exact size before giving up
+      e = hipMalloc(&p, n * sizeof(T));
+      if (e != hipSuccess) {
+        p = nullptr;
+        cap = 0;
+        return cg_hip_check(e, "hipMalloc");
+      }
+      want = n;
+    }
+    cap = want;
+    return CG_OK;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct cg_ctx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  hipEvent_t ev[8] = {};
+  std::mutex mu;
+  float kt[6] = {0, 0, 0, 0, 0, 0};
+
+  // plan cache
+  cg::Plan plan;
+  cg::PlanArgs pa{};
+  bool plan_valid = false;
+  uint64_t plan_zone = 0;
+  int64_t plan_t0 = 0, plan_t1 = 0;
+  std::vector<char> plan_host;
+  DBuf<char> plan_dev;
+
+  // expansion buffers
+  DBuf<int64_t> run_anchor, run_off, offsets, times, block_run, nb_in, nb_out;
+  DBuf<int32_t> run_count;
+  DBuf<uint32_t> run_dmask;
+  DBuf<char> scan_tmp;
+  DBuf<unsigned long long> stuck;
+  int64_t last_E = 0, last_R = 0, last_G = 0;
+
+  // per-node buffers
+  DBuf<int64_t> rn_off, rn_cnt64, pair_pos, node_off, node_time, nt_off, d_nid_off, d_gid_off,
+      d_ex_off, d_group_off;
+  DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule, d_nids, d_gids, d_ex,
+      d_group_nodes, d_rule_job, node_cnt32;
+  DBuf<uint8_t> d_group_exists, d_job_pause;
+  DBuf<char> pn_tmp;
+  int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
+
+  void free_all() {
+    plan_dev.release();
+    run_anchor.release(); run_off.release(); offsets.release(); times.release();
+    block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
+    run_dmask.release(); scan_tmp.release(); stuck.release();
+    rn_off.release(); rn_cnt64.release(); pair_pos.release(); node_off.release();
+    node_time.release(); nt_off.release(); d_nid_off.release(); d_gid_off.release();
+    d_ex_off.release(); d_group_off.release(); rn_cnt.release(); rn_nodes.release();
+    pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();
+    d_nids.release(); d_gids.release(); d_ex.release(); d_group_nodes.release();
+    d_rule_job.release(); node_cnt32.release(); d_group_exists.release();
+    d_job_pause.release(); pn_tmp.release();
+  }
+};
+
+struct cg_specs {
+  cg_ctx* ctx = nullptr;
+  cg::DSpec* d = nullptr;
+  size_t n = 0;
+  bool owner = false;
+};
+
+int upload_plan(cg_ctx* c, const cg::Plan& plan, int64_t t0, int64_t t1, cg::PlanArgs* pa);
+int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                         int64_t* n_events);

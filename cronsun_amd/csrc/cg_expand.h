@@ -1,0 +1,183 @@
+// cg_expand.h -- per-rule expansion logic shared by the kernels (and by the
+// host-side algorithm check in tests/native): the closed form inside a
+// constant-offset CF segment, and the per-rule run planner of k_count.
+//
+// Expansion of one rule over (T0, T1] is the reference loop
+//   t = T0; loop { t = Next(t); if t.IsZero() || t > T1 break; emit t }
+// (cron.go:212-215 batched).  Per plan segment the engine records a run:
+//   CF   segment: first fire f = Next(previous fire) by the exact walk, then
+//                 the closed form: every later matching local time in the
+//                 segment (DESIGN.md §3 proves these coincide with Next).
+//   WALK segment: fires produced one by one by the exact walk.
+#pragma once
+#include "cg_time.h"
+#include "cg_zone.h"
+
+namespace cg {
+
+struct CFRule {
+  uint64_t M, S;
+  uint32_t H, nM, nS, nMS, C;
+};
+
+CG_HD CFRule cf_rule(const DSpec& sp) {
+  CFRule c;
+  c.H = sp.hour & 0xFFFFFFu;
+  c.M = sp.min & 0x0FFFFFFFFFFFFFFFull;
+  c.S = sp.sec & 0x0FFFFFFFFFFFFFFFull;
+  c.nM = (uint32_t)__builtin_popcountll(c.M);
+  c.nS = (uint32_t)__builtin_popcountll(c.S);
+  c.nMS = c.nM * c.nS;
+  c.C = (uint32_t)__builtin_popcount(c.H) * c.nMS;
+  return c;
+}
+
+CG_HD uint32_t cf_rank(const CFRule& c, int32_t tod) {
+  return tod_rank(c.H, c.M, c.S, c.nM, c.nS, tod);
+}
+
+// matching local days of a CF segment (Month bit + dayMatches), bit j = day0 + j
+CG_HD uint32_t seg_daymask(const DSpec& sp, const Segment& sg, const uint32_t* dtab) {
+  uint32_t m = 0;
+  for (int j = 0; j < sg.ndays; j++) {
+    uint32_t e = dtab[sg.dt_off + j];
+    int mo = e & 15, dom = (e >> 4) & 31, dow = (e >> 9) & 7;
+    if (month_ok(sp, mo) && day_matches(sp, dom, dow)) m |= 1u << j;
+  }
+  return m;
+}
+
+// # of matching instants in (uf, ue], both inside CF segment sg
+CG_HD int64_t cf_count(const CFRule& c, const Segment& sg, uint32_t dmask, int64_t uf,
+                       int64_t ue) {
+  if (c.C == 0 || ue <= uf) return 0;
+  int32_t rf = (int32_t)(uf - sg.base), re = (int32_t)(ue - sg.base);
+  int32_t jf = rf / 86400, tf = rf - jf * 86400;
+  int32_t je = re / 86400, te = re - je * 86400;
+  uint64_t dm = dmask;
+  if (jf == je) return ((dm >> jf) & 1) ? (int64_t)cf_rank(c, te) - (int64_t)cf_rank(c, tf) : 0;
+  int64_t n = 0;
+  if ((dm >> jf) & 1) n += (int64_t)c.C - (int64_t)cf_rank(c, tf);
+  uint64_t mid = dm & ~((2ull << jf) - 1ull) & ((1ull << je) - 1ull);
+  n += (int64_t)c.C * __builtin_popcountll(mid);
+  if ((dm >> je) & 1) n += cf_rank(c, te);
+  return n;
+}
+
+struct CFIter {
+  int32_t day, h, m, s;
+};
+
+// iterator state of the k-th (k >= 0) fire counted from the anchor fire uf
+CG_HD CFIter cf_seek(const CFRule& c, const Segment& sg, uint32_t dmask, int64_t uf, int64_t k) {
+  int32_t rf = (int32_t)(uf - sg.base);
+  int32_t jf = rf / 86400, tf = rf - jf * 86400;
+  uint64_t idx = (uint64_t)cf_rank(c, tf) - 1 + (uint64_t)k;
+  CFIter it;
+  it.day = jf;
+  if (idx >= c.C) {
+    idx -= c.C;
+    uint32_t dskip = (uint32_t)(idx / c.C);
+    idx -= (uint64_t)dskip * c.C;
+    uint64_t above = (uint64_t)dmask & ~((2ull << jf) - 1ull);
+    it.day = select64(above, dskip);
+  }
+  uint32_t i32 = (uint32_t)idx;
+  uint32_t hi = i32 / c.nMS;
+  uint32_t rem = i32 - hi * c.nMS;
+  uint32_t mi = rem / c.nS;
+  uint32_t si = rem - mi * c.nS;
+  it.h = select64(c.H, hi);
+  it.m = select64(c.M, mi);
+  it.s = select64(c.S, si);
+  return it;
+}
+
+CG_HD void cf_next(const CFRule& c, uint32_t dmask, CFIter& it) {
+  int32_t s = next_bit64(c.S, it.s);
+  if (s < 64) { it.s = s; return; }
+  it.s = __builtin_ctzll(c.S);
+  int32_t m = next_bit64(c.M, it.m);
+  if (m < 64) { it.m = m; return; }
+  it.m = __builtin_ctzll(c.M);
+  int32_t h = next_bit32(c.H, it.h);
+  if (h < 32) { it.h = h; return; }
+  it.h = __builtin_ctz(c.H);
+  it.day = next_bit32(dmask, it.day);
+}
+
+CG_HD int64_t cf_value(const Segment& sg, const CFIter& it) {
+  return sg.base + (int64_t)(it.day * 86400 + it.h * 3600 + it.m * 60 + it.s);
+}
+
+// Run records of one rule over the plan's G segments (k_count's body).
+// Writes anchor/count/dmask at stride 1 from the given pointers.  Returns
+// false where the reference loop never terminates: Next never returns
+// (CG_NO_PROGRESS) or returns a time <= its input (it then cycles forever,
+// e.g. Pacific/Chatham's 45-minute fall-back).
+CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, int G,
+                      const uint32_t* dtab, int64_t t0, int64_t t1, int64_t* anchor_out,
+                      int32_t* count_out, uint32_t* dmask_out) {
+  if (sp.kind == KIND_EVERY) {
+    // ConstantDelaySchedule: T0 + k*D for k >= 1 (constantdelay.go:25-27)
+    int64_t D = (int64_t)sp.sec;
+    anchor_out[0] = t0;
+    count_out[0] = (int32_t)((t1 - t0) / D);
+    dmask_out[0] = 0;
+    for (int s = 1; s < G; s++) {
+      anchor_out[s] = 0;
+      count_out[s] = 0;
+      dmask_out[s] = 0;
+    }
+    return true;
+  }
+  const CFRule c = cf_rule(sp);
+  int64_t pos = t0;             // last fire so far (or T0)
+  int64_t pending = INT64_MIN;  // Next(pos) if already computed
+  bool done = false, ok = true;
+  for (int s = 0; s < G; s++) {
+    const Segment& sg = segs[s];
+    int64_t anchor = 0, cnt = 0;
+    uint32_t dm = 0;
+    if (!done) {
+      const int64_t b = sg.b < t1 ? sg.b : t1;
+      if (sg.kind == 0) {
+        int64_t e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
+        pending = INT64_MIN;
+        if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;  // backwards: the loop cycles
+        if (e == CG_NO_PROGRESS) {
+          done = true;
+          ok = false;
+        } else if (e == CG_ZERO_TIME || e == CG_BEYOND) {
+          done = true;
+        } else if (e > b) {
+          pending = e;
+        } else {
+          dm = seg_daymask(sp, sg, dtab);
+          cnt = 1 + cf_count(c, sg, dm, e, b);
+          anchor = e;
+          pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
+        }
+      } else {
+        anchor = pos;
+        int64_t e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
+        pending = INT64_MIN;
+        for (;;) {
+          if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;  // backwards: the loop cycles
+          if (e == CG_NO_PROGRESS) { done = true; ok = false; break; }
+          if (e == CG_ZERO_TIME || e == CG_BEYOND) { done = true; break; }
+          if (e > b) { pending = e; break; }
+          cnt++;
+          pos = e;
+          e = next_exact(sp, z, pos, t1);
+        }
+      }
+    }
+    anchor_out[s] = anchor;
+    count_out[s] = (int32_t)cnt;
+    dmask_out[s] = dm;
+  }
+  return ok;
+}
+
+}  // namespace cg

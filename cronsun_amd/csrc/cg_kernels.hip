@@ -1,0 +1,414 @@
+// cg_kernels.hip -- gfx950 kernels for batched cron fire-time expansion.
+//
+// Pipeline for Expand(specs, zone, T0, T1):
+//   k_count      one lane per rule: per plan segment, the first fire (exact
+//                Go walk, next_exact) and the closed-form count of the rest,
+//                or the walked count inside WALK windows -> run records
+//   k_scan_*     exclusive scan of run counts -> run offsets (int64)
+//   k_block_map  first run touched by each 2048-event output block
+//   k_write_cf   output-parallel: each lane materialises 8 consecutive fire
+//                times from the closed form, staged in LDS, then the block
+//                stores its 16 KiB slice with coalesced 16-B stores
+//   k_write_walk re-walks the (rare) WALK-window runs
+//   k_rule_offs  rule-major CSR offsets
+// Integer and HBM-bound throughout: no MFMA.
+#include <hip/hip_runtime.h>
+
+#include "cg_expand.h"
+#include "cg_kernels.h"
+
+namespace cg {
+
+namespace {
+
+constexpr uint64_t kMask60 = 0x0FFFFFFFFFFFFFFFull;
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---- plan staging into LDS --------------------------------------------
+struct PlanView {
+  ZoneView z;
+  const Segment* segs;
+  const uint32_t* dtab;
+};
+
+__device__ PlanView stage_plan(const PlanArgs& p, char* lds) {
+  int64_t* w = reinterpret_cast<int64_t*>(lds);
+  int32_t* o = reinterpret_cast<int32_t*>(lds + align_up(size_t(p.zn) * 8, 16));
+  Segment* s = reinterpret_cast<Segment*>(lds + align_up(size_t(p.zn) * 8, 16) +
+                                          align_up(size_t(p.zn) * 4, 16));
+  uint32_t* d = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s) +
+                                            align_up(size_t(p.G) * sizeof(Segment), 16));
+  for (int i = threadIdx.x; i < p.zn; i += blockDim.x) {
+    w[i] = p.zwhen[i];
+    o[i] = p.zoff[i];
+  }
+  const int64_t* sg = reinterpret_cast<const int64_t*>(p.segs);
+  int64_t* sd = reinterpret_cast<int64_t*>(s);
+  for (int i = threadIdx.x; i < p.G * int(sizeof(Segment) / 8); i += blockDim.x) sd[i] = sg[i];
+  for (int i = threadIdx.x; i < p.nd; i += blockDim.x) d[i] = p.dtab[i];
+  __syncthreads();
+  PlanView v;
+  v.z.when = w;
+  v.z.off = o;
+  v.z.n = p.zn;
+  v.segs = s;
+  v.dtab = d;
+  return v;
+}
+
+__device__ __forceinline__ DSpec load_spec(const DSpec* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1];
+  DSpec s;
+  s.sec = (uint64_t(a.y) << 32) | a.x;
+  s.min = (uint64_t(a.w) << 32) | a.z;
+  s.hour = b.x;
+  s.dom = b.y;
+  s.mondow = b.z;
+  s.kind = b.w;
+  return s;
+}
+
+// ---------------------------------------------------------------- kernels --
+
+__global__ __launch_bounds__(256) void k_next_batch(const DSpec* __restrict__ specs, int64_t n,
+                                                     PlanArgs p, const int64_t* __restrict__ t_in,
+                                                     int64_t* __restrict__ t_out) {
+  extern __shared__ __align__(16) char lds[];
+  PlanView v = stage_plan(p, lds);
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    DSpec sp = load_spec(specs + i);
+    int64_t t = t_in[i];
+    if (sp.kind == KIND_EVERY) t_out[i] = t + int64_t(sp.sec);  // constantdelay.go:25-27
+    else t_out[i] = next_exact(sp, v.z, t, INT64_MAX);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, int64_t R,
+                                                PlanArgs p, int64_t* __restrict__ run_anchor,
+                                                int32_t* __restrict__ run_count,
+                                                uint32_t* __restrict__ run_dmask,
+                                                unsigned long long* __restrict__ stuck_rule) {
+  extern __shared__ __align__(16) char lds[];
+  PlanView v = stage_plan(p, lds);
+  const int G = p.G;
+  for (int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; r < R;
+       r += int64_t(gridDim.x) * blockDim.x) {
+    DSpec sp = load_spec(specs + r);
+    const int64_t j0 = r * G;
+    if (!count_rule(sp, v.z, v.segs, G, v.dtab, p.t0, p.t1, run_anchor + j0, run_count + j0,
+                    run_dmask + j0))
+      atomicMin(stuck_rule, (unsigned long long)r);
+  }
+}
+
+// ---- scan: int32 counts -> int64 exclusive offsets -----------------------
+constexpr int kScanThreads = 256;
+constexpr int kScanPerThread = 16;
+constexpr int kScanTile = kScanThreads * kScanPerThread;
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    int64_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// block-wide exclusive scan of x (256 threads); returns prefix, total in *tot
+__device__ int64_t block_excl_scan(int64_t x, int64_t* tot) {
+  __shared__ int64_t wsum[kScanThreads / 64];
+  int64_t inc = wave_incl_scan(x);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int64_t base = 0, all = 0;
+  for (int i = 0; i < kScanThreads / 64; i++) {
+    if (i < w) base += wsum[i];
+    all += wsum[i];
+  }
+  __syncthreads();
+  *tot = all;
+  return base + inc - x;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const int32_t* __restrict__ in,
+                                                               int64_t n,
+                                                               int64_t* __restrict__ partial) {
+  int64_t base = int64_t(blockIdx.x) * kScanTile;
+  int64_t acc = 0;
+  for (int i = 0; i < kScanPerThread; i++) {
+    int64_t idx = base + int64_t(i) * kScanThreads + threadIdx.x;
+    if (idx < n) acc += in[idx];
+  }
+  int64_t tot;
+  block_excl_scan(acc, &tot);
+  if (threadIdx.x == 0) partial[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_top(int64_t* __restrict__ partial,
+                                                            int64_t nb) {
+  int64_t carry = 0;
+  for (int64_t base = 0; base < nb; base += kScanThreads) {
+    int64_t idx = base + threadIdx.x;
+    int64_t x = idx < nb ? partial[idx] : 0;
+    int64_t tot;
+    int64_t pre = block_excl_scan(x, &tot);
+    if (idx < nb) partial[idx] = carry + pre;
+    carry += tot;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __restrict__ in,
+                                                              int64_t n,
+                                                              const int64_t* __restrict__ partial,
+                                                              int64_t* __restrict__ out) {
+  int64_t base = int64_t(blockIdx.x) * kScanTile + int64_t(threadIdx.x) * kScanPerThread;
+  int32_t v[kScanPerThread];
+  int64_t acc = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; i++) {
+    int64_t idx = base + i;
+    v[i] = idx < n ? in[idx] : 0;
+    acc += v[i];
+  }
+  int64_t tot;
+  int64_t run = partial[blockIdx.x] + block_excl_scan(acc, &tot);
+  if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; i++) {
+    int64_t idx = base + i;
+    run += v[i];
+    if (idx < n) out[idx + 1] = run;
+  }
+}
+
+// largest j in [lo, hi] with off[j] <= x
+__device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, int64_t lo,
+                                              int64_t hi, int64_t x) {
+  while (lo < hi) {
+    int64_t mid = (lo + hi + 1) >> 1;
+    if (off[mid] <= x) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void k_block_map(const int64_t* __restrict__ run_off, int64_t nruns, int64_t nblocks,
+                            int64_t* __restrict__ block_run) {
+  int64_t b = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (b > nblocks) return;
+  if (b == nblocks) {
+    block_run[b] = nruns - 1;
+    return;
+  }
+  block_run[b] = search_run(run_off, 0, nruns - 1, b * int64_t(kWriteChunk));
+}
+
+constexpr int kStageStride = kWritePerThread + 1;  // pad: conflict-free ds_write_b64
+
+__global__ __launch_bounds__(kWriteThreads) void k_write_cf(
+    const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
+    const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
+    const int64_t* __restrict__ run_off, int64_t nruns, const int64_t* __restrict__ block_run,
+    int64_t E, int64_t* __restrict__ times) {
+  __shared__ int64_t stage[kWriteThreads * kStageStride];
+  __shared__ Segment segs[64];
+  extern __shared__ __align__(16) char dyn[];
+  uint32_t* dtab = reinterpret_cast<uint32_t*>(dyn);
+  for (int i = threadIdx.x; i < p.G * int(sizeof(Segment) / 8); i += blockDim.x)
+    reinterpret_cast<int64_t*>(segs)[i] = reinterpret_cast<const int64_t*>(p.segs)[i];
+  for (int i = threadIdx.x; i < p.nd; i += blockDim.x) dtab[i] = p.dtab[i];
+  __syncthreads();
+
+  const int G = p.G;
+  const int64_t B0 = int64_t(blockIdx.x) * kWriteChunk;
+  int64_t i = B0 + int64_t(threadIdx.x) * kWritePerThread;
+  if (i < E) {
+    int64_t j = search_run(run_off, block_run[blockIdx.x], block_run[blockIdx.x + 1], i);
+    int64_t k = i - run_off[j];
+    int64_t n = run_count[j];
+    // per-run state
+    int kind = 0;  // 0 CF, 1 EVERY, 2 WALK (written later)
+    DSpec sp;
+    CFRule c;
+    CFIter it;
+    const Segment* sg = nullptr;
+    uint32_t dm = 0;
+    int64_t anchor = 0, D = 0;
+    bool fresh = true;
+#pragma unroll 1
+    for (int q = 0; q < kWritePerThread && i < E; q++, i++, k++) {
+      while (k >= n) {  // step to the next non-empty run
+        j++;
+        k = 0;
+        n = run_count[j];
+        fresh = true;
+      }
+      if (fresh) {
+        fresh = false;
+        int64_t r = j / G;
+        int s = int(j - r * G);
+        sp = load_spec(specs + r);
+        anchor = run_anchor[j];
+        sg = &segs[s];
+        if (sp.kind == KIND_EVERY) {
+          kind = 1;
+          D = int64_t(sp.sec);
+        } else if (sg->kind != 0) {
+          kind = 2;
+        } else {
+          kind = 0;
+          c = cf_rule(sp);
+          dm = run_dmask[j];
+          it = cf_seek(c, *sg, dm, anchor, k);
+        }
+      } else if (kind == 0) {
+        cf_next(c, dm, it);
+      }
+      int64_t val;
+      if (kind == 0) val = cf_value(*sg, it);
+      else if (kind == 1) val = anchor + (k + 1) * D;
+      else val = 0;
+      stage[threadIdx.x * kStageStride + q] = val;
+    }
+  }
+  __syncthreads();
+  // coalesced store of the block's slice: lane l writes events (2l, 2l+1)
+  const int64_t lim = E - B0;
+  for (int e = threadIdx.x * 2; e < kWriteChunk; e += kWriteThreads * 2) {
+    if (e >= lim) break;
+    int t0 = e / kWritePerThread, q0 = e % kWritePerThread;
+    int64_t a = stage[t0 * kStageStride + q0];
+    if (e + 1 < lim) {
+      int64_t b = stage[t0 * kStageStride + q0 + 1];
+      longlong2 v;
+      v.x = a;
+      v.y = b;
+      *reinterpret_cast<longlong2*>(times + B0 + e) = v;
+    } else {
+      times[B0 + e] = a;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ specs, int64_t R,
+                                                     PlanArgs p,
+                                                     const int64_t* __restrict__ run_anchor,
+                                                     const int32_t* __restrict__ run_count,
+                                                     const int64_t* __restrict__ run_off,
+                                                     int64_t* __restrict__ times) {
+  extern __shared__ __align__(16) char lds[];
+  PlanView v = stage_plan(p, lds);
+  const int G = p.G;
+  for (int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; r < R;
+       r += int64_t(gridDim.x) * blockDim.x) {
+    DSpec sp;
+    bool loaded = false;
+    for (int s = 0; s < G; s++) {
+      if (v.segs[s].kind == 0) continue;
+      const int64_t j = r * G + s;
+      int32_t n = run_count[j];
+      if (n == 0) continue;
+      if (!loaded) {
+        sp = load_spec(specs + r);
+        loaded = true;
+      }
+      if (sp.kind == KIND_EVERY) break;
+      int64_t t = run_anchor[j];
+      int64_t o = run_off[j];
+      for (int32_t q = 0; q < n; q++) {
+        t = next_exact(sp, v.z, t, p.t1);
+        times[o + q] = t;
+      }
+    }
+  }
+}
+
+__global__ void k_rule_offsets(const int64_t* __restrict__ run_off, int64_t R, int32_t G,
+                               int64_t* __restrict__ offsets) {
+  int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (r <= R) offsets[r] = run_off[r * G];
+}
+
+int grid_for(int64_t n, int threads, int max_blocks) {
+  int64_t b = (n + threads - 1) / threads;
+  if (b < 1) b = 1;
+  return int(b < max_blocks ? b : max_blocks);
+}
+
+}  // namespace
+
+size_t plan_lds_bytes(const PlanArgs& p) {
+  return align_up(size_t(p.zn) * 8, 16) + align_up(size_t(p.zn) * 4, 16) +
+         align_up(size_t(p.G) * sizeof(Segment), 16) + align_up(size_t(p.nd) * 4, 16);
+}
+
+void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,
+                       int64_t* t_out, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_next_batch, dim3(grid_for(n, 256, 256 * 16)), dim3(256),
+                     plan_lds_bytes(p), st, specs, n, p, t_in, t_out);
+}
+
+void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run_anchor,
+                  int32_t* run_count, uint32_t* run_dmask, unsigned long long* stuck_rule,
+                  hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(k_count, dim3(grid_for(R, 256, 256 * 16)), dim3(256), plan_lds_bytes(p), st,
+                     specs, R, p, run_anchor, run_count, run_dmask, stuck_rule);
+}
+
+size_t scan_temp_bytes(int64_t n) {
+  int64_t nb = (n + kScanTile - 1) / kScanTile;
+  return size_t(nb + 1) * sizeof(int64_t);
+}
+
+void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st) {
+  if (n <= 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
+    return;
+  }
+  int64_t nb = (n + kScanTile - 1) / kScanTile;
+  int64_t* partial = static_cast<int64_t*>(temp);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanThreads), 0, st, partial, nb);
+  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out);
+}
+
+void launch_block_map(const int64_t* run_off, int64_t nruns, int64_t nblocks, int64_t* block_run,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(k_block_map, dim3(grid_for(nblocks + 1, 256, 1 << 30)), dim3(256), 0, st,
+                     run_off, nruns, nblocks, block_run);
+}
+
+void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
+                     const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
+                     int64_t nruns, const int64_t* block_run, int64_t nblocks, int64_t E,
+                     int64_t* times, hipStream_t st) {
+  if (E <= 0) return;
+  hipLaunchKernelGGL(k_write_cf, dim3(nblocks), dim3(kWriteThreads),
+                     align_up(size_t(p.nd) * 4, 16), st, specs, p, run_anchor, run_count,
+                     run_dmask, run_off, nruns, block_run, E, times);
+}
+
+void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
+                       const int32_t* run_count, const int64_t* run_off, int64_t* times,
+                       hipStream_t st) {
+  if (R <= 0) return;
+  hipLaunchKernelGGL(k_write_walk, dim3(grid_for(R, 256, 256 * 16)), dim3(256),
+                     plan_lds_bytes(p), st, specs, R, p, run_anchor, run_count, run_off, times);
+}
+
+void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(k_rule_offsets, dim3(grid_for(R + 1, 256, 1 << 30)), dim3(256), 0, st,
+                     run_off, R, G, offsets);
+}
+
+}  // namespace cg

@@ -1,0 +1,239 @@
+"""Batch engine over one MI355X: the node/cron/gpu package of the design,
+seen from Python.  Wraps a cg_ctx (one HIP device + stream + HBM buffers).
+
+  Engine.upload(schedules)                  -> Specs (SoA packed in HBM)
+  Engine.next_batch(specs, loc, t)          Schedule.Next for every rule
+  Engine.expand(specs, loc, t0, t1)         rule-major CSR of fire times
+  Engine.expand_device(specs, loc, t0, t1)  same, left in HBM (bench)
+  Engine.expand_per_node(specs, loc, t0, t1, rules, mode)
+                                            per-node (time, rule) CSR
+"""
+import ctypes as C
+import threading
+
+import numpy as np
+
+from . import _lib
+from ._lib import CgError, check, lib
+
+
+class Specs:
+    """An uploaded rule set (device-resident, 32 B per rule)."""
+
+    def __init__(self, engine, handle, n, parent=None):
+        self.engine = engine
+        self._h = handle
+        self.n = n
+        self._parent = parent  # keeps the parent of a slice alive
+
+    def __len__(self):
+        return self.n
+
+    def slice(self, first, count):
+        h = C.c_void_p()
+        check(lib().cg_specs_slice(self._h, first, count, C.byref(h)))
+        return Specs(self.engine, h, count, parent=self)
+
+    def free(self):
+        if self._h:
+            lib().cg_specs_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def _as_c_schedules(schedules):
+    arr = (_lib.cg_schedule * max(len(schedules), 1))()
+    for i, s in enumerate(schedules):
+        arr[i] = s.to_c() if hasattr(s, "to_c") else s
+    return arr
+
+
+class RulesIn:
+    """Integer-interned jobs/groups (cg_rules_in).  Arrays are numpy and kept
+    alive by this object."""
+
+    FIELDS = ("group_off", "group_nodes", "group_exists", "rule_job", "nid_off", "nids",
+              "gid_off", "gids", "ex_off", "ex", "job_pause")
+    DTYPES = {"group_off": np.int64, "group_nodes": np.int32, "group_exists": np.uint8,
+              "rule_job": np.int32, "nid_off": np.int64, "nids": np.int32, "gid_off": np.int64,
+              "gids": np.int32, "ex_off": np.int64, "ex": np.int32, "job_pause": np.uint8}
+
+    def __init__(self, n_nodes, n_groups, n_rules, n_jobs, **arrays):
+        self.n_nodes, self.n_groups, self.n_rules, self.n_jobs = n_nodes, n_groups, n_rules, n_jobs
+        for f in self.FIELDS:
+            a = np.ascontiguousarray(arrays[f], dtype=self.DTYPES[f])
+            if a.size == 0:
+                a = np.zeros(1, dtype=self.DTYPES[f])
+            setattr(self, f, a)
+
+    def to_c(self):
+        s = _lib.cg_rules_in()
+        s.n_nodes, s.n_groups, s.n_rules, s.n_jobs = (
+            self.n_nodes, self.n_groups, self.n_rules, self.n_jobs)
+        for f in self.FIELDS:
+            setattr(s, f, getattr(self, f).ctypes.data)
+        return s
+
+
+class Engine:
+    def __init__(self, device=0):
+        self._lock = threading.Lock()
+        h = C.c_void_p()
+        check(lib().cg_init(device, C.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().cg_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ specs
+    def upload(self, schedules):
+        arr = _as_c_schedules(schedules)
+        h = C.c_void_p()
+        check(lib().cg_specs_upload_schedules(self._h, C.cast(arr, C.c_void_p), len(schedules),
+                                              C.byref(h)))
+        return Specs(self, h, len(schedules))
+
+    def upload_c(self, arr, n):
+        """Upload a ctypes array of cg_schedule (e.g. from cron.parse_batch)."""
+        h = C.c_void_p()
+        check(lib().cg_specs_upload_schedules(self._h, C.cast(arr, C.c_void_p), n, C.byref(h)))
+        return Specs(self, h, n)
+
+    def upload_soa(self, second, minute, hour, dom, month, dow, delay_ns):
+        cols = [np.ascontiguousarray(x, dtype=np.uint64) for x in (second, minute, hour, dom, month, dow)]
+        d = np.ascontiguousarray(delay_ns, dtype=np.int64)
+        soa = _lib.cg_spec_soa(*[c.ctypes.data for c in cols], d.ctypes.data)
+        h = C.c_void_p()
+        check(lib().cg_specs_upload(self._h, C.byref(soa), len(d), C.byref(h)))
+        return Specs(self, h, len(d))
+
+    def _specs(self, specs):
+        return specs if isinstance(specs, Specs) else self.upload(specs)
+
+    @staticmethod
+    def _loc(loc):
+        if loc is None:
+            from .cron import UTC
+            return UTC()
+        return loc
+
+    # ------------------------------------------------------------- Next
+    def next_batch(self, specs, loc, t_in):
+        sp = self._specs(specs)
+        t = np.ascontiguousarray(t_in, dtype=np.int64)
+        if t.shape[0] != sp.n:
+            raise ValueError("one input time per rule")
+        out = np.empty_like(t)
+        check(lib().cg_next_batch(self._h, sp._h, self._loc(loc).handle, t.ctypes.data,
+                                  out.ctypes.data))
+        return out
+
+    # -------------------------------------------------------- expansion
+    def expand(self, specs, loc, t0, t1):
+        sp = self._specs(specs)
+        n = C.c_int64()
+        check(lib().cg_expand_device(self._h, sp._h, self._loc(loc).handle, int(t0), int(t1),
+                                     C.byref(n)))
+        off = np.empty(sp.n + 1, dtype=np.int64)
+        check(lib().cg_result_copy_offsets(self._h, off.ctypes.data))
+        times = np.empty(max(n.value, 1), dtype=np.int64)
+        check(lib().cg_result_copy_times(self._h, 0, n.value, times.ctypes.data))
+        return off, times[:n.value]
+
+    def expand_device(self, specs, loc, t0, t1):
+        n = C.c_int64()
+        check(lib().cg_expand_device(self._h, specs._h, self._loc(loc).handle, int(t0), int(t1),
+                                     C.byref(n)))
+        return n.value
+
+    def result_device(self):
+        off, times, n = C.c_void_p(), C.c_void_p(), C.c_int64()
+        check(lib().cg_result_device(self._h, C.byref(off), C.byref(times), C.byref(n)))
+        return off.value, times.value, n.value
+
+    def copy_times(self, first, count):
+        out = np.empty(max(count, 1), dtype=np.int64)
+        check(lib().cg_result_copy_times(self._h, int(first), int(count), out.ctypes.data))
+        return out[:count]
+
+    def kernel_times(self):
+        """ms per phase of the last expansion: count, scan, block map,
+        write(closed form), write(walk), offsets."""
+        buf = (C.c_float * 6)()
+        k = lib().cg_last_kernel_times(self._h, buf, 6)
+        return list(buf)[:k]
+
+    def sync(self):
+        check(lib().cg_sync(self._h))
+
+    # --------------------------------------------------------- per node
+    def rule_nodes(self, rules, mode=_lib.EXCLUDE_NONE):
+        rin = rules.to_c()
+        nnz = C.c_int64()
+        check(lib().cg_rule_nodes(self._h, C.byref(rin), mode, None, None, 0, C.byref(nnz)))
+        off = np.empty(rules.n_rules + 1, dtype=np.int64)
+        nodes = np.empty(max(nnz.value, 1), dtype=np.int32)
+        check(lib().cg_rule_nodes(self._h, C.byref(rin), mode, off.ctypes.data, nodes.ctypes.data,
+                                  nnz.value, C.byref(nnz)))
+        return off, nodes[:nnz.value]
+
+    def expand_per_node(self, specs, loc, t0, t1, rules, mode=_lib.EXCLUDE_NONE):
+        sp = self._specs(specs)
+        rin = rules.to_c()
+        En, nnz = C.c_int64(), C.c_int64()
+        check(lib().cg_expand_per_node_device(self._h, sp._h, self._loc(loc).handle, int(t0),
+                                              int(t1), C.byref(rin), mode, C.byref(En),
+                                              C.byref(nnz)))
+        out = _lib.cg_node_csr()
+        node_off = np.empty(rules.n_nodes + 1, dtype=np.int64)
+        time = np.empty(max(En.value, 1), dtype=np.int64)
+        rule = np.empty(max(En.value, 1), dtype=np.int32)
+        out.node_off, out.time, out.rule = node_off.ctypes.data, time.ctypes.data, rule.ctypes.data
+        out.cap = En.value
+        check(lib().cg_expand_per_node(self._h, sp._h, self._loc(loc).handle, int(t0), int(t1),
+                                       C.byref(rin), mode, C.byref(out)))
+        return node_off, time[:En.value], rule[:En.value]
+
+    def expand_per_node_device(self, specs, loc, t0, t1, rules, mode=_lib.EXCLUDE_NONE):
+        rin = rules.to_c()
+        En, nnz = C.c_int64(), C.c_int64()
+        check(lib().cg_expand_per_node_device(self._h, specs._h, self._loc(loc).handle, int(t0),
+                                              int(t1), C.byref(rin), mode, C.byref(En),
+                                              C.byref(nnz)))
+        return En.value, nnz.value
+
+    def node_counts_to_device(self, d_ptr):
+        check(lib().cg_node_counts_to_device(self._h, C.c_void_p(d_ptr)))
+
+
+_default = None
+_default_lock = threading.Lock()
+
+
+def default_engine():
+    global _default
+    with _default_lock:
+        if _default is None:
+            _default = Engine(0)
+        return _default
+
+
+def device_count():
+    return lib().cg_device_count()
+
+
+__all__ = ["Engine", "Specs", "RulesIn", "default_engine", "device_count", "CgError"]

@@ -1,0 +1,279 @@
+/*
+ * cronsun_gpu.h -- C-ABI of the MI355X fire-time expansion engine for
+ * cronsun's scheduling path (library: cronsun_amd/libcronsun_gpu.so).
+ *
+ * This is the boundary a Go cgo package `node/cron/gpu` binds (see
+ * INTEGRATION.md).  Plain pointers and sizes only; no C++ or torch types.
+ * Every entry point names the reference interface it replaces
+ * (paths relative to qlchan/cronsun).
+ *
+ * Conventions
+ *   - Return value: CG_OK (0) or a negative CG_E* code; cg_last_error()
+ *     returns a thread-local message for the last failure on this thread.
+ *   - Times are int64 unix seconds.  Go's zero time.Time{} (the "never fires"
+ *     result of Schedule.Next) is CG_ZERO_TIME = -62135596800.
+ *   - Input buffers are owned by the caller and only read during the call;
+ *     nothing is retained (cgo rule: Go memory is never kept).
+ *   - A cg_ctx owns one HIP device, its stream and its device buffers.  Calls
+ *     on one ctx are serialised internally; calls block the calling thread.
+ *   - There is no CPU fallback: compute entry points fail with CG_ENODEV
+ *     when no MI355X (gfx950) device is usable.
+ */
+#ifndef CRONSUN_GPU_H
+#define CRONSUN_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CG_ABI_VERSION 1
+
+#define CG_OK 0
+#define CG_EINVAL (-1)    /* bad argument */
+#define CG_ENOMEM (-2)    /* host or device allocation failed */
+#define CG_EHIP (-3)      /* HIP runtime error */
+#define CG_ECAPACITY (-4) /* output buffer too small; required size reported */
+#define CG_EPARSE (-5)    /* spec did not parse; message via cg_last_error */
+#define CG_ERANGE (-6)    /* time range/horizon outside supported bounds */
+#define CG_ENODEV (-7)    /* no usable gfx950 device */
+#define CG_EPANIC (-8)    /* input on which the reference Go code panics */
+
+#define CG_ZERO_TIME (-62135596800LL)
+
+/* ParseOption bits -- node/cron/parser.go:17-26 */
+#define CG_PARSE_SECOND 1
+#define CG_PARSE_MINUTE 2
+#define CG_PARSE_HOUR 4
+#define CG_PARSE_DOM 8
+#define CG_PARSE_MONTH 16
+#define CG_PARSE_DOW 32
+#define CG_PARSE_DOW_OPTIONAL 64
+#define CG_PARSE_DESCRIPTOR 128
+/* defaultParser, parser.go:171-173 (cron.Parse) */
+#define CG_PARSE_DEFAULT (1 | 2 | 4 | 8 | 16 | 64 | 128)
+/* standardParser, parser.go:155-157 (cron.ParseStandard) */
+#define CG_PARSE_STANDARD (2 | 4 | 8 | 16 | 32 | 128)
+
+#define CG_STAR_BIT (1ULL << 63) /* spec.go:48-51 */
+
+/* A parsed cron.Schedule: *SpecSchedule (spec.go:7-9) or
+ * ConstantDelaySchedule (constantdelay.go:7-9). */
+typedef struct {
+  int32_t kind; /* 0 = SpecSchedule, 1 = ConstantDelaySchedule */
+  int32_t reserved;
+  uint64_t second, minute, hour, dom, month, dow; /* SpecSchedule fields */
+  int64_t delay_ns;                               /* ConstantDelaySchedule.Delay */
+} cg_schedule;
+
+typedef struct cg_ctx cg_ctx;
+typedef struct cg_zone cg_zone;
+typedef struct cg_specs cg_specs;
+typedef struct cg_jobset cg_jobset;
+
+/* ---------------------------------------------------------------- misc --- */
+int cg_abi_version(void);
+const char* cg_last_error(void);
+/* number of gfx950 devices visible (0 on a host without one) */
+int cg_device_count(void);
+
+/* ------------------------------------------------------ parse (host) --- */
+/* Parser{options}.Parse(spec) -- parser.go:78-136; cron.Parse is options =
+ * CG_PARSE_DEFAULT (parser.go:181-183), cron.ParseStandard CG_PARSE_STANDARD
+ * (parser.go:167-169).  On error returns CG_EPARSE and copies Go's message
+ * into err (NUL-terminated, truncated to err_cap) and cg_last_error(). */
+int cg_parse(int options, const char* spec, size_t len, cg_schedule* out, char* err,
+             size_t err_cap);
+/* Batch form: n specs, status[i] = 0 or a CG_E* code. */
+int cg_parse_batch(int options, const char* const* specs, const size_t* lens, size_t n,
+                   cg_schedule* out, int32_t* status, int nthreads);
+/* Parser internals, exposed for the reference's parser KATs
+ * (parser_test.go TestRange/TestField/TestBits): getRange (parser.go:204-267),
+ * getField (parser.go:188-199), getBits (parser.go:293-306).  names: 0 none,
+ * 1 month names, 2 day-of-week names. */
+int cg_get_range(const char* expr, size_t len, unsigned min, unsigned max, int names,
+                 uint64_t* bits, char* err, size_t err_cap);
+int cg_get_field(const char* expr, size_t len, unsigned min, unsigned max, int names,
+                 uint64_t* bits, char* err, size_t err_cap);
+uint64_t cg_get_bits(unsigned min, unsigned max, unsigned step);
+/* Every(d).Delay -- constantdelay.go:14-21 */
+int64_t cg_every(int64_t duration_ns);
+/* time.ParseDuration (used by "@every", parser.go:368-373) */
+int cg_parse_duration(const char* s, size_t len, int64_t* out_ns);
+
+/* ------------------------------------------------------------- zones --- */
+/* time.LoadLocationFromTZData (TZif v1-v4 incl. the POSIX footer). */
+int cg_zone_from_tzif(const uint8_t* data, size_t len, cg_zone** out);
+/* time.FixedZone("", offset_sec) */
+int cg_zone_fixed(int32_t offset_sec, cg_zone** out);
+/* time.UTC */
+int cg_zone_utc(cg_zone** out);
+void cg_zone_free(cg_zone* z);
+/* Location.lookup(unix).offset (host, for inspection/tests) */
+int cg_zone_offset(const cg_zone* z, int64_t unix_sec, int32_t* offset_sec);
+/* The flat breakpoint table the kernels use for [lo, hi]: when[0] is
+ * INT64_MIN, then every instant in (lo, hi] where the offset changes.
+ * Returns the entry count (writes at most cap). */
+int cg_zone_table(const cg_zone* z, int64_t lo, int64_t hi, int64_t* when, int32_t* off,
+                  int cap);
+
+/* ----------------------------------------------------------- context --- */
+int cg_init(int device, cg_ctx** out);
+void cg_destroy(cg_ctx* ctx);
+/* wait for all work queued on the ctx's stream */
+int cg_sync(cg_ctx* ctx);
+
+/* -------------------------------------------------- specs (HBM SoA) --- */
+/* SoA upload of SpecSchedule/ConstantDelaySchedule values (spec.go:7-9,
+ * constantdelay.go:7-9).  delay_ns[i] > 0 marks rule i as @every; the mask
+ * arrays are then ignored for it. Any array may be NULL if unused. */
+typedef struct {
+  const uint64_t* second;
+  const uint64_t* minute;
+  const uint64_t* hour;
+  const uint64_t* dom;
+  const uint64_t* month;
+  const uint64_t* dow;
+  const int64_t* delay_ns;
+} cg_spec_soa;
+int cg_specs_upload(cg_ctx* ctx, const cg_spec_soa* soa, size_t n_rules, cg_specs** out);
+int cg_specs_upload_schedules(cg_ctx* ctx, const cg_schedule* s, size_t n_rules,
+                              cg_specs** out);
+/* rules [first, first+count) of an uploaded set, as a view (no copy) -- used
+ * to shard rules by job-ID range across ranks.  Free views with
+ * cg_specs_free as well; the view must not outlive its parent. */
+int cg_specs_slice(cg_specs* specs, size_t first, size_t count, cg_specs** out);
+size_t cg_specs_count(const cg_specs* specs);
+void cg_specs_free(cg_specs* specs);
+
+/* --------------------------------------------------------- Next() ------ */
+/* out[i] = Schedule.Next(t_in[i]) for rule i, evaluated in zone z
+ * (spec.go:55-145, constantdelay.go:25-27).  Host arrays of n = rule count.
+ * Never-firing specs give CG_ZERO_TIME.  Replaces per-entry calls in
+ * Cron.run (cron.go:212-215, 242-243) and Cmd.lockTtl (job.go:196-197). */
+int cg_next_batch(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, const int64_t* t_in,
+                  int64_t* t_out);
+
+/* --------------------------------------------------------- expansion --- */
+/* Fire times of every rule over (t0, t1]: for each rule,
+ *   t = t0; loop { t = Next(t); if t.IsZero() || t > t1 break; emit t }
+ * i.e. the reference Next loop, batched.  Output is a rule-major CSR:
+ *   offsets[R+1] (int64), times[offsets[R]] (int64, ascending per rule).
+ * t1 - t0 must be <= CG_MAX_HORIZON seconds. */
+#define CG_MAX_HORIZON (366LL * 86400)
+typedef struct {
+  int64_t* offsets;  /* [R+1], caller-allocated (may be NULL) */
+  int64_t* times;    /* [times_cap], caller-allocated (may be NULL) */
+  int64_t times_cap;
+  int64_t n_events;  /* out: total events (always set, also on CG_ECAPACITY) */
+} cg_csr;
+int cg_expand(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0, int64_t t1,
+              cg_csr* out);
+
+/* Device-resident variant: runs the whole expansion on the ctx's stream and
+ * leaves offsets/times in device memory owned by the ctx (valid until the next
+ * expansion call on this ctx).  *n_events is set.  Used for benchmarks and by
+ * multi-GPU drivers that keep results in HBM. */
+int cg_expand_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
+                     int64_t t1, int64_t* n_events);
+/* device pointers of the last device-resident result */
+int cg_result_device(cg_ctx* ctx, const int64_t** d_offsets, const int64_t** d_times,
+                     int64_t* n_events);
+/* copy [first, first+count) of the last result's times to host */
+int cg_result_copy_times(cg_ctx* ctx, int64_t first, int64_t count, int64_t* host_out);
+int cg_result_copy_offsets(cg_ctx* ctx, int64_t* host_offsets /* [R+1] */);
+
+/* Per-kernel device time of the last expansion (ms, HIP events on the ctx
+ * stream): [0] count, [1] scan, [2] block map, [3] write (closed form),
+ * [4] write (walk), [5] offsets.  n = entries written. */
+int cg_last_kernel_times(cg_ctx* ctx, float* ms, int n);
+
+/* --------------------------------------------- rule -> node resolution --- */
+/* Integer-interned jobs/groups (host interns string IDs; see cg_jobset_*).
+ * Resolution modes:
+ *   CG_EXCLUDE_NONE       reference scheduling semantics, Job.Cmds/IsRunOn
+ *                         (job.go:591-630): ExcludeNodeIDs has no effect (the
+ *                         inner-loop `continue`, job.go:598-602); Pause => none.
+ *   CG_EXCLUDE_RULE       per-rule exclusion N_r \ E_r; Pause => none.
+ *   CG_EXCLUDE_CUMULATIVE web/job.go:222-257 GetJobNodes: N_r \ U_{q<=r} E_q
+ *                         over the job's rules in order; Pause => none. */
+#define CG_EXCLUDE_NONE 0
+#define CG_EXCLUDE_RULE 1
+#define CG_EXCLUDE_CUMULATIVE 2
+typedef struct {
+  int32_t n_nodes, n_groups, n_rules, n_jobs;
+  const int64_t* group_off;     /* [G+1] group -> node CSR (Group.NodeIDs, group.go:17-22) */
+  const int32_t* group_nodes;
+  const uint8_t* group_exists;  /* [G] 0 = gid referenced but absent from the groups map */
+  const int32_t* rule_job;      /* [R] owning job; a job's rules are contiguous, in order */
+  const int64_t* nid_off;       /* [R+1] JobRule.NodeIDs */
+  const int32_t* nids;
+  const int64_t* gid_off;       /* [R+1] JobRule.GroupIDs */
+  const int32_t* gids;
+  const int64_t* ex_off;        /* [R+1] JobRule.ExcludeNodeIDs */
+  const int32_t* ex;
+  const uint8_t* job_pause;     /* [J] Job.Pause */
+} cg_rules_in;
+
+/* Per-node fire lists: for every node n, the (time, rule) events of the rules
+ * scheduled on n (per `mode`), rule-major in ascending rule index, times
+ * ascending within a rule.  Output CSR: node_off[N+1], time[], rule[].
+ * Replaces every node's Node.loadJobs -> addJob -> Job.Cmds filter
+ * (node/node.go:121-158) plus its Cron entries' Next loop. */
+typedef struct {
+  int64_t* node_off;  /* [N+1] caller-allocated (may be NULL) */
+  int64_t* time;      /* [cap] */
+  int32_t* rule;      /* [cap] */
+  int64_t cap;
+  int64_t n_events;   /* out */
+  int64_t nnz;        /* out: sum over rules of |nodes(rule)| */
+} cg_node_csr;
+int cg_expand_per_node(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
+                       int64_t t1, const cg_rules_in* rules, int mode, cg_node_csr* out);
+/* device-resident variant (bench / multi-GPU); results stay in ctx memory */
+int cg_expand_per_node_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
+                              int64_t t1, const cg_rules_in* rules, int mode,
+                              int64_t* n_events, int64_t* nnz);
+/* device pointers of the last per-node result */
+int cg_node_result_device(cg_ctx* ctx, const int64_t** d_node_off, const int64_t** d_time,
+                          const int32_t** d_rule, int64_t* n_events);
+/* per-node event counts of the last per-node result, copied to a DEVICE
+ * buffer of N int64 (e.g. a torch tensor for an RCCL allgather) */
+int cg_node_counts_to_device(cg_ctx* ctx, int64_t* d_counts);
+
+/* rule -> node CSR only (GPU join), host output */
+int cg_rule_nodes(cg_ctx* ctx, const cg_rules_in* rules, int mode, int64_t* rn_off /*[R+1]*/,
+                  int32_t* rn_nodes, int64_t cap, int64_t* nnz);
+
+/* ----------------------------------- string-keyed job model (host) --- */
+/* Host interning of cronsun's string IDs (Job/JobRule/Group, job.go:38-84,
+ * group.go:17-22) into cg_rules_in.  Job IDs, rule IDs, group IDs and node
+ * IDs are arbitrary byte strings (NUL-terminated here). */
+int cg_jobset_new(cg_jobset** out);
+void cg_jobset_free(cg_jobset* js);
+int cg_jobset_add_group(cg_jobset* js, const char* gid, const char* const* nids, size_t n);
+int cg_jobset_add_job(cg_jobset* js, const char* job_id, int pause);
+/* appends a rule to the last added job */
+int cg_jobset_add_rule(cg_jobset* js, const char* rule_id, const char* const* gids, size_t ng,
+                       const char* const* nids, size_t nn, const char* const* ex, size_t ne);
+/* freeze and expose the interned arrays (valid until the jobset is freed) */
+int cg_jobset_rules(cg_jobset* js, cg_rules_in* out);
+/* node index of a node ID (-1 if unknown) / node ID of an index */
+int32_t cg_jobset_node_index(const cg_jobset* js, const char* nid);
+const char* cg_jobset_node_id(const cg_jobset* js, int32_t idx);
+/* Job.Cmds(nid, groups) keys (job.go:591-614): writes the rule indices of
+ * the job's Cmds on node nid -- after the map's last-writer-wins dedup of
+ * Job.ID+Rule.ID -- and returns their count (host reference semantics). */
+int32_t cg_jobset_cmds(const cg_jobset* js, int32_t job, const char* nid, int32_t* rules_out,
+                       int32_t cap);
+/* Job.IsRunOn(nid, groups) (job.go:616-630) */
+int cg_jobset_is_run_on(const cg_jobset* js, int32_t job, const char* nid);
+/* Job.GetJobNodes (web/job.go:222-257): node indices in first-seen order */
+int32_t cg_jobset_job_nodes(const cg_jobset* js, int32_t job, int32_t* nodes_out, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CRONSUN_GPU_H */

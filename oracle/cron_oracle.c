@@ -559,7 +559,11 @@ WRAP:
             added = 1;
             t = or_date(f.year, f.month, f.day, 0, 0, 0, l);
         }
+        int64_t prev = t;
         t = add_date(t, 0, 0, 1, l);
+        /* Test-infrastructure guard: Go's walk is stuck from here on (the
+         * same t repeats forever, e.g. Pacific/Apia's skipped 2011-12-30). */
+        if (t <= prev) return OR_NO_PROGRESS;
         or_fields_of(t, l, &f);
         if (f.day == 1) goto WRAP;
     }
@@ -1118,8 +1122,14 @@ int64_t or_expand(const or_sched *s, int64_t t0, int64_t t1, const or_loc *l,
     int64_t n = 0;
     int64_t t = t0;
     for (;;) {
+        int64_t prev = t;
         t = or_sched_next(s, t, 0, l);
+        if (t == OR_NO_PROGRESS) return -1; /* the reference never returns */
         if (t == OR_ZERO_TIME || t > t1) break;
+        /* Next went backwards (e.g. an hour reset landing on the first pass
+         * of a repeated local hour, Pacific/Chatham): the reference loop
+         * revisits a fire it already emitted and cycles forever. */
+        if (t <= prev) return -1;
         if (out && n < cap) out[n] = t;
         n++;
     }
@@ -1180,8 +1190,13 @@ int64_t or_expand_batch(const or_sched *s, size_t R, int64_t t0, int64_t t1,
     b.s = s; b.R = R; b.t0 = t0; b.t1 = t1; b.l = l; b.counts = counts;
     run_batch(&b, nthreads);
     offsets[0] = 0;
-    for (size_t r = 0; r < R; r++) offsets[r + 1] = offsets[r] + counts[r];
+    int stuck = 0;
+    for (size_t r = 0; r < R; r++) {
+        if (counts[r] < 0) { stuck = 1; counts[r] = 0; }
+        offsets[r + 1] = offsets[r] + counts[r];
+    }
     free(counts);
+    if (stuck) return -1;
     if (times) {
         b.times = times;
         b.offsets = offsets;

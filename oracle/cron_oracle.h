@@ -37,6 +37,8 @@ extern "C" {
 #endif
 
 #define OR_ZERO_TIME (-62135596800LL)
+/* returned where the reference's Next never terminates (see or_spec_next) */
+#define OR_NO_PROGRESS (INT64_MIN + 1)
 
 /* ---- Go *time.Location restatement ---- */
 typedef struct or_loc or_loc;
@@ -112,11 +114,14 @@ int or_parse_duration(const char *s, size_t len, int64_t *out, char *err,
 
 /* ---- expansion loop (build-defined batch form of cron.go:212-215) ----
  * t = T0; loop { t = Next(t); if t.IsZero() || t > T1 break; emit t }
- * Returns the number of events; writes at most cap of them. */
+ * Returns the number of events (writes at most cap of them), or -1 when the
+ * reference loop never terminates: Next never returns (OR_NO_PROGRESS) or
+ * returns a time <= its input, after which the loop cycles. */
 int64_t or_expand(const or_sched *s, int64_t t0, int64_t t1, const or_loc *l,
                   int64_t *out, int64_t cap);
 /* Batch over R rules with nthreads POSIX threads.  offsets[R+1] is filled;
- * times may be NULL (count only).  Returns total events. */
+ * times may be NULL (count only).  Returns total events, or -1 if any rule
+ * hit OR_NO_PROGRESS (its count is then 0). */
 int64_t or_expand_batch(const or_sched *s, size_t R, int64_t t0, int64_t t1,
                         const or_loc *l, int nthreads, int64_t *offsets,
                         int64_t *times);

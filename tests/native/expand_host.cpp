@@ -1,0 +1,133 @@
+// Host-side check of the expansion algorithm (cg_expand.h: count_rule +
+// closed-form iteration + WALK re-walk, exactly what k_count/k_write_cf/
+// k_write_walk run) against the oracle's literal Next loop.  Test
+// infrastructure; the GPU tests check the kernels themselves.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../cronsun_amd/csrc/cg_expand.h"
+#include "../../oracle/cron_oracle.h"
+
+using namespace cg;
+
+static std::vector<uint8_t> slurp(const char* p) {
+  FILE* f = fopen(p, "rb");
+  if (!f) { perror(p); exit(2); }
+  std::vector<uint8_t> d;
+  uint8_t b[4096];
+  size_t n;
+  while ((n = fread(b, 1, sizeof b, f)) > 0) d.insert(d.end(), b, b + n);
+  fclose(f);
+  return d;
+}
+
+static const char* atoms[6][12] = {
+    {"*/7", "0", "5", "*/20", "15/35", "10-40/3", "7,30,45", "59", "0/15", "3-3", "0", "58-59"},
+    {"*", "0", "30", "*/5", "20-35/15", "1,31,59", "5-7/2", "*/59", "10-12", "0", "0", "59"},
+    {"*", "0", "9", "23", "*/2", "1/2", "9-17", "22,23,0", "2", "1", "3", "0-23/5"},
+    {"*", "?", "1", "15", "31", "29", "30", "1,15", "*/2", "9-20", "28-31", "5/7"},
+    {"*", "?", "1", "2", "Feb", "Jan,Jul", "Apr-Oct", "*/3", "Mar", "Nov", "Dec", "*"},
+    {"*", "?", "0", "1-5", "Mon", "Sun", "mon/2", "Sat,Sun", "*/2", "3", "fri-sat", "*"}};
+
+static DSpec pack(const or_sched& s) {
+  DSpec d{};
+  if (s.kind == 1) { d.kind = KIND_EVERY; d.sec = uint64_t(s.delay_ns / 1000000000LL); return d; }
+  d.sec = s.spec.second & 0x0FFFFFFFFFFFFFFFull;
+  d.min = s.spec.minute & 0x0FFFFFFFFFFFFFFFull;
+  d.hour = uint32_t(s.spec.hour & 0xFFFFFF);
+  d.dom = uint32_t(s.spec.dom & 0xFFFFFFFEu) | uint32_t(s.spec.dom >> 63);
+  d.mondow = uint32_t(s.spec.month & 0x1FFE) | (uint32_t(s.spec.dow & 0x7F) << 16) |
+             (uint32_t(s.spec.dow >> 63) << 23);
+  return d;
+}
+
+int main(int argc, char** argv) {
+  const char* zone = argc > 1 ? argv[1] : "UTC";
+  int nspec = argc > 2 ? atoi(argv[2]) : 400;
+  ZoneRules zr;
+  or_loc* ol = nullptr;
+  if (!strcmp(zone, "UTC")) { zr = zone_utc(); or_loc_utc(&ol); }
+  else {
+    auto d = slurp((std::string("tests/golden/zoneinfo/") + zone).c_str());
+    std::string e;
+    zone_from_tzif(d.data(), d.size(), &zr, &e);
+    or_loc_from_tzif(d.data(), d.size(), &ol);
+  }
+  std::mt19937_64 rng(777);
+  std::vector<or_sched> scheds;
+  std::vector<std::string> names;
+  while ((int)scheds.size() < nspec) {
+    std::string spec;
+    if (rng() % 10 == 0) spec = "@every " + std::to_string(1 + rng() % 7200) + "s";
+    else for (int f = 0; f < 6; f++) { if (f) spec += " "; spec += atoms[f][rng() % 12]; }
+    or_sched s;
+    char err[256];
+    if (or_parse(OR_OPT_DEFAULT, spec.c_str(), spec.size(), &s, err, sizeof err)) continue;
+    scheds.push_back(s);
+    names.push_back(spec);
+  }
+  // horizons: around each zone transition in 2025-2027 and plain ones
+  ZoneTable tt = build_table(zr, 1735689600, 1830297600);
+  std::vector<std::pair<int64_t, int64_t>> hz = {{1767571200, 1767571200 + 86400},
+                                                 {1767571200 - 77, 1767571200 + 40 * 86400}};
+  for (size_t i = 1; i < tt.when.size() && i < 5; i++) {
+    hz.push_back({tt.when[i] - 43217, tt.when[i] + 43200});
+    hz.push_back({tt.when[i] - 3 * 86400, tt.when[i] + 4 * 86400});
+  }
+  int bad = 0;
+  long long total = 0;
+  for (auto [t0, t1] : hz) {
+    Plan plan = build_plan(zr, t0, t1);
+    ZoneView zv{plan.table.when.data(), plan.table.off.data(), int32_t(plan.table.when.size())};
+    int G = int(plan.segs.size());
+    for (size_t r = 0; r < scheds.size(); r++) {
+      DSpec d = pack(scheds[r]);
+      std::vector<int64_t> anc(G);
+      std::vector<int32_t> cnt(G);
+      std::vector<uint32_t> dm(G);
+      std::vector<int64_t> got;
+      bool ok = G == 0 || count_rule(d, zv, plan.segs.data(), G, plan.dtab.data(), t0, t1, anc.data(), cnt.data(), dm.data());
+      for (int s = 0; s < G && ok; s++) {
+        const Segment& sg = plan.segs[s];
+        if (d.kind == KIND_EVERY) {
+          for (int k = 0; k < cnt[s]; k++) got.push_back(anc[s] + int64_t(k + 1) * int64_t(d.sec));
+        } else if (sg.kind == 0) {
+          CFRule c = cf_rule(d);
+          // mimic the writer: seek at a random start, then step
+          int k0 = cnt[s] ? int(rng() % cnt[s]) : 0;
+          std::vector<int64_t> part(cnt[s]);
+          for (int k = 0; k < k0; k++) part[k] = cf_value(sg, cf_seek(c, sg, dm[s], anc[s], k));
+          if (cnt[s]) {
+            CFIter it = cf_seek(c, sg, dm[s], anc[s], k0);
+            for (int k = k0; k < cnt[s]; k++) {
+              if (k > k0) cf_next(c, dm[s], it);
+              part[k] = cf_value(sg, it);
+            }
+          }
+          got.insert(got.end(), part.begin(), part.end());
+        } else {
+          int64_t t = anc[s];
+          for (int k = 0; k < cnt[s]; k++) { t = next_exact(d, zv, t, t1); got.push_back(t); }
+        }
+      }
+      int64_t n = or_expand(&scheds[r], t0, t1, ol, nullptr, 0);
+      if (n < 0) { if (ok) { if (bad++ < 10) printf("NOPROGRESS mismatch %s\n", names[r].c_str()); } continue; }
+      std::vector<int64_t> exp(n);
+      or_expand(&scheds[r], t0, t1, ol, exp.data(), n);
+      total += n;
+      if (got != exp && bad++ < 10) {
+        size_t i = 0;
+        while (i < got.size() && i < exp.size() && got[i] == exp[i]) i++;
+        printf("MISMATCH %s [%s] (%lld,%lld] n=%zu/%zu first diff idx %zu: %lld vs %lld (G=%d)\n", zone,
+               names[r].c_str(), (long long)t0, (long long)t1, got.size(), exp.size(), i,
+               (long long)(i < got.size() ? got[i] : -1), (long long)(i < exp.size() ? exp[i] : -1), G);
+      }
+    }
+  }
+  printf("%s: %d mismatches, %lld events checked\n", zone, bad, total);
+  return bad ? 1 : 0;
+}

@@ -1,0 +1,139 @@
+"""Batch expansion on the GPU (cg_expand*) vs the oracle's literal Next loop:
+t = T0; loop { t = Next(t); if t.IsZero() || t > T1 break; emit t }.
+Bit-exact CSR (offsets and times) on seeded inputs; size-independent
+properties at the BASELINE config-2 scale."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from common import ZONES, oracle_zone, product_zone, random_spec, to_oracle_sched
+from cronsun_amd import _lib, cron, synth
+
+pytestmark = pytest.mark.gpu
+
+DAY = 86400
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from cronsun_amd.engine import Engine
+    return Engine(0)
+
+
+def oracle_csr(scheds, zone, t0, t1):
+    arr = O.sched_array([to_oracle_sched(s.to_c()) for s in scheds])
+    return O.expand_batch(arr, t0, t1, oracle_zone(zone), threads=8)
+
+
+def check_same(eng, scheds, zone, t0, t1, specs=None):
+    off, times = eng.expand(scheds, product_zone(zone), t0, t1)
+    eo, et = oracle_csr(scheds, zone, t0, t1)
+    if not np.array_equal(off, eo):
+        bad = np.nonzero(np.diff(off) != np.diff(eo))[0][:5]
+        msg = [(specs[i] if specs else i, int(off[i + 1] - off[i]), int(eo[i + 1] - eo[i])) for i in bad]
+        raise AssertionError(f"counts differ {zone} ({t0},{t1}]: {msg}")
+    if not np.array_equal(times, et):
+        i = int(np.nonzero(times != et)[0][0])
+        r = int(np.searchsorted(off, i, side="right") - 1)
+        raise AssertionError(f"times differ {zone} rule {specs[r] if specs else r} idx {i}: "
+                             f"{int(times[i])} vs {int(et[i])}")
+    return off, times
+
+
+def _horizons(zone):
+    from test_zone import _table
+    z = product_zone(zone)
+    when, _ = _table(z, 1735689600, 1830297600)  # 2025..2027
+    hs = [(synth.T0_2026, synth.T0_2026 + 3600), (synth.T0_2026 + 1234, synth.T0_2026 + DAY)]
+    for w in when[1:5]:
+        w = int(w)
+        hs.append((w - DAY // 2 - 17, w + DAY // 2))          # straddles a transition
+        hs.append((w - 3 * DAY, w + 4 * DAY))                  # 7 days around it
+    return hs
+
+
+@pytest.mark.parametrize("zone", ZONES)
+def test_random_specs_vs_oracle(eng, zone):
+    rng = np.random.default_rng(abs(hash("x" + zone)) % 2**32)
+    specs = [random_spec(rng) for _ in range(300)]
+    scheds = [cron.Parse(s) for s in specs]
+    for t0, t1 in _horizons(zone):
+        check_same(eng, scheds, zone, t0, t1, specs)
+
+
+@pytest.mark.parametrize("zone", ["UTC", "America/New_York", "Australia/Lord_Howe"])
+def test_synthetic_mix_vs_oracle(eng, zone):
+    specs = synth.spec_mix(2000, seed=3)
+    scheds = [cron.Parse(s) for s in specs]
+    check_same(eng, scheds, zone, synth.T0_2026, synth.T0_2026 + DAY, specs)
+    ny_spring = 1772953200  # 2026-03-08T07:00Z
+    check_same(eng, scheds, zone, ny_spring - 6 * 3600, ny_spring + 6 * 3600, specs)
+
+
+def test_long_horizon_multi_chunk(eng):
+    # > 30 days: several closed-form chunks, each re-anchored by an exact Next
+    rng = np.random.default_rng(5)
+    specs = ["0 0 9 * * 1-5", "0 0 0 29 Feb ?", "0 15 10 15 * ?", "@weekly", "@monthly",
+             "0 0 0 1 Jan,Jul ?", "0 0 12 * * Sun", "@every 6h", "0 30 2 * * *", "@daily"]
+    specs += [random_spec(rng) for _ in range(40) if True]
+    specs = [s for s in specs if not s.startswith("@every") or True]
+    scheds = [cron.Parse(s) for s in specs]
+    for zone in ("UTC", "America/New_York", "Australia/Sydney", "America/Havana"):
+        check_same(eng, scheds, zone, synth.T0_2026 - 17, synth.T0_2026 + 100 * DAY, specs)
+
+
+def test_edge_cases(eng):
+    scheds = [cron.Parse(s) for s in ["0 0 0 30 Feb ?", "* * * * * *", "@every 1s", "0 0 0 * * *"]]
+    z = product_zone("UTC")
+    # empty horizon and reversed horizon
+    off, times = eng.expand(scheds, z, synth.T0_2026, synth.T0_2026)
+    assert off.tolist() == [0, 0, 0, 0, 0] and times.size == 0
+    off, times = eng.expand(scheds, z, synth.T0_2026, synth.T0_2026 - 5)
+    assert off[-1] == 0
+    # one second horizon: the every-second spec and @every 1s fire once
+    off, times = eng.expand(scheds, z, synth.T0_2026, synth.T0_2026 + 1)
+    assert off.tolist() == [0, 0, 1, 2, 2]
+    # empty rule set
+    off, times = eng.expand([], z, 0, 100)
+    assert off.tolist() == [0] and times.size == 0
+    # the horizon limit is enforced
+    with pytest.raises(_lib.CgError) as e:
+        eng.expand(scheds, z, 0, _lib.MAX_HORIZON + 1)
+    assert e.value.code == _lib.CG_ERANGE
+
+
+def test_feb29_across_leap_years(eng):
+    scheds = [cron.Parse("0 0 0 29 Feb ?"), cron.Parse("59 59 23 28,29 Feb ?")]
+    t0 = 1704067200  # 2024-01-01
+    check_same(eng, scheds, "UTC", t0, t0 + 365 * DAY, ["feb29", "feb28/29"])
+    check_same(eng, scheds, "America/New_York", t0 + 40 * DAY, t0 + 70 * DAY, ["feb29", "feb28/29"])
+
+
+def test_config2_scale_properties(eng):
+    """BASELINE config 2 (1M mixed rules x 24 h, UTC) at full size: the
+    size-independent invariants, plus bit-exact rows on a seeded sample."""
+    n = 1_000_000
+    specs = synth.spec_mix(n, seed=0x5EED)
+    arr, status = cron.parse_batch(specs)
+    assert (status == 0).all()
+    sp = eng.upload_c(arr, n)
+    t0, t1 = synth.T0_2026, synth.T0_2026 + DAY
+    E = eng.expand_device(sp, None, t0, t1)
+    off = np.empty(n + 1, dtype=np.int64)
+    from cronsun_amd._lib import check, lib
+    check(lib().cg_result_copy_offsets(eng._h, off.ctypes.data))
+    assert off[0] == 0 and off[-1] == E and (np.diff(off) >= 0).all()
+    times = eng.copy_times(0, E)
+    assert ((times > t0) & (times <= t1)).all()
+    # strictly increasing inside every rule: the only non-increasing steps are at rule starts
+    steps = np.nonzero(np.diff(times) <= 0)[0] + 1
+    assert np.isin(steps, off[1:-1]).all()
+    # bit-exact on a seeded sample of rules
+    rng = np.random.default_rng(9)
+    idx = np.sort(rng.choice(n, 3000, replace=False))
+    sample = [cron.Parse(specs[i]) for i in idx]
+    eo, et = oracle_csr(sample, "UTC", t0, t1)
+    for k, i in enumerate(idx):
+        got = times[off[i]:off[i + 1]]
+        exp = et[eo[k]:eo[k + 1]]
+        assert np.array_equal(got, exp), specs[i]
