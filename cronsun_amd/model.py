@@ -60,6 +60,9 @@ class JobRule:
         return None
 
 
+GroupMap = Dict[str, Group]  # Job has a field named Group
+
+
 @dataclass
 class Job:
     ID: str
@@ -79,16 +82,16 @@ class Job:
         for r in self.Rules:
             r.Valid()
 
-    def Cmds(self, nid, gs: Dict[str, Group]):
+    def Cmds(self, nid, gs: GroupMap):
         """job.go:591-614 -> {Job.ID + Rule.ID: (job, rule)}"""
         js = JobSet([self], gs)
         idx = js.cmds(0, nid)
         return {self.ID + js.rules[i].ID: (self, js.rules[i]) for i in idx}
 
-    def IsRunOn(self, nid, gs: Dict[str, Group]):
+    def IsRunOn(self, nid, gs: GroupMap):
         return JobSet([self], gs).is_run_on(0, nid)
 
-    def GetJobNodes(self, gs: Dict[str, Group]):
+    def GetJobNodes(self, gs: GroupMap):
         return JobSet([self], gs).job_nodes(0)
 
 
@@ -101,7 +104,7 @@ def _cstr_array(strs):
 class JobSet:
     """All jobs + groups interned by the C++ host layer (cg_jobset)."""
 
-    def __init__(self, jobs, groups: Dict[str, Group]):
+    def __init__(self, jobs, groups: GroupMap):
         L = lib()
         h = C.c_void_p()
         check(L.cg_jobset_new(C.byref(h)))
