@@ -483,7 +483,9 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   const int64_t nblocks = (E + kWriteChunk - 1) / kWriteChunk;
   if ((rc = c->times.ensure(std::max<int64_t>(E, 1)))) return rc;
   if ((rc = c->block_run.ensure(nblocks + 1))) return rc;
-  bool has_walk = false;
+  // walked runs: WALK windows, or CF segments whose entry fire does not fully
+  // match (only possible when the plan has zone transitions)
+  bool has_walk = c->plan.segs.size() > 0 && c->plan.table.when.size() > 1;
   for (const Segment& sg : c->plan.segs) has_walk |= sg.kind != 0;
   (void)hipEventRecord(c->ev[3], c->st);
   if (E > 0) launch_block_map(c->run_off.p, nruns, nblocks, c->block_run.p, c->st);
@@ -493,8 +495,8 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
                     nruns, c->block_run.p, nblocks, E, c->times.p, c->st);
   (void)hipEventRecord(c->ev[5], c->st);
   if (E > 0 && has_walk)
-    launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_off.p, c->times.p,
-                      c->st);
+    launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->run_off.p,
+                      c->times.p, c->st);
   (void)hipEventRecord(c->ev[6], c->st);
   launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->st);
   (void)hipEventRecord(c->ev[7], c->st);

@@ -115,6 +115,26 @@ CG_HD int64_t cf_value(const Segment& sg, const CFIter& it) {
 // false where the reference loop never terminates: Next never returns
 // (CG_NO_PROGRESS) or returns a time <= its input (it then cycles forever,
 // e.g. Pacific/Chatham's 45-minute fall-back).
+//
+// A CF segment's run switches to the closed form only at a fire whose fields
+// all match in the segment's offset (premise (i)).  The walk can
+// emit fires that do not (America/Havana: the hour walk misses the wrap when
+// local midnight does not exist, so the day is never re-checked); such a
+// segment is walked fire by fire instead and flagged with kRunWalked in its
+// daymask word.
+constexpr uint32_t kRunWalked = 0x80000000u;
+
+CG_HD bool cf_full_match(const DSpec& sp, const CFRule& c, const Segment& sg,
+                         const uint32_t* dtab, int64_t u) {
+  int32_t r = (int32_t)(u - sg.base);
+  int32_t j = r / 86400, tod = r - j * 86400;
+  uint32_t e = dtab[sg.dt_off + j];
+  int mo = e & 15, dom = (e >> 4) & 31, dow = (e >> 9) & 7;
+  if (!month_ok(sp, mo) || !day_matches(sp, dom, dow)) return false;
+  int32_t h = tod / 3600, m = (tod / 60) % 60, s = tod % 60;
+  return ((c.H >> h) & 1u) && ((c.M >> m) & 1ull) && ((c.S >> s) & 1ull);
+}
+
 CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, int G,
                       const uint32_t* dtab, int64_t t0, int64_t t1, int64_t* anchor_out,
                       int32_t* count_out, uint32_t* dmask_out) {
@@ -141,29 +161,22 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
     uint32_t dm = 0;
     if (!done) {
       const int64_t b = sg.b < t1 ? sg.b : t1;
-      if (sg.kind == 0) {
-        int64_t e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
-        pending = INT64_MIN;
-        if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;  // backwards: the loop cycles
-        if (e == CG_NO_PROGRESS) {
-          done = true;
-          ok = false;
-        } else if (e == CG_ZERO_TIME || e == CG_BEYOND) {
-          done = true;
-        } else if (e > b) {
-          pending = e;
-        } else {
-          dm = seg_daymask(sp, sg, dtab);
-          cnt = 1 + cf_count(c, sg, dm, e, b);
-          anchor = e;
-          pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
-        }
+      int64_t e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
+      pending = INT64_MIN;
+      if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;  // backwards: the loop cycles
+      if (sg.kind == 0 && e != CG_NO_PROGRESS && e != CG_ZERO_TIME && e != CG_BEYOND &&
+          e <= b && cf_full_match(sp, c, sg, dtab, e)) {
+        dm = seg_daymask(sp, sg, dtab);
+        cnt = 1 + cf_count(c, sg, dm, e, b);
+        anchor = e;
+        pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
       } else {
+        // walked run: a WALK segment, or a CF segment entered by a fire the
+        // closed form cannot continue from
         anchor = pos;
-        int64_t e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
-        pending = INT64_MIN;
+        if (sg.kind == 0) dm = kRunWalked;
         for (;;) {
-          if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;  // backwards: the loop cycles
+          if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;
           if (e == CG_NO_PROGRESS) { done = true; ok = false; break; }
           if (e == CG_ZERO_TIME || e == CG_BEYOND) { done = true; break; }
           if (e > b) { pending = e; break; }
@@ -171,6 +184,7 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
           pos = e;
           e = next_exact(sp, z, pos, t1);
         }
+        if (cnt == 0) dm = 0;
       }
     }
     anchor_out[s] = anchor;
@@ -178,6 +192,11 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
     dmask_out[s] = dm;
   }
   return ok;
+}
+
+// does run (segment kind, daymask word) hold walked fires?
+CG_HD bool run_is_walked(const Segment& sg, uint32_t dmask) {
+  return sg.kind != 0 || (dmask & kRunWalked) != 0;
 }
 
 }  // namespace cg

@@ -45,8 +45,8 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
                      int64_t* times, hipStream_t st);
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
-                       const int32_t* run_count, const int64_t* run_off, int64_t* times,
-                       hipStream_t st);
+                       const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
+                       int64_t* times, hipStream_t st);
 
 void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,
                          hipStream_t st);

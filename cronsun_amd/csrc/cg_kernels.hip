@@ -257,15 +257,15 @@ __global__ __launch_bounds__(kWriteThreads) void k_write_cf(
         sp = load_spec(specs + r);
         anchor = run_anchor[j];
         sg = &segs[s];
+        dm = run_dmask[j];
         if (sp.kind == KIND_EVERY) {
           kind = 1;
           D = int64_t(sp.sec);
-        } else if (sg->kind != 0) {
-          kind = 2;
+        } else if (run_is_walked(*sg, dm)) {
+          kind = 2;  // written by k_write_walk
         } else {
           kind = 0;
           c = cf_rule(sp);
-          dm = run_dmask[j];
           it = cf_seek(c, *sg, dm, anchor, k);
         }
       } else if (kind == 0) {
@@ -301,6 +301,7 @@ __global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ sp
                                                      PlanArgs p,
                                                      const int64_t* __restrict__ run_anchor,
                                                      const int32_t* __restrict__ run_count,
+                                                     const uint32_t* __restrict__ run_dmask,
                                                      const int64_t* __restrict__ run_off,
                                                      int64_t* __restrict__ times) {
   extern __shared__ __align__(16) char lds[];
@@ -311,10 +312,9 @@ __global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ sp
     DSpec sp;
     bool loaded = false;
     for (int s = 0; s < G; s++) {
-      if (v.segs[s].kind == 0) continue;
       const int64_t j = r * G + s;
       int32_t n = run_count[j];
-      if (n == 0) continue;
+      if (n == 0 || !run_is_walked(v.segs[s], run_dmask[j])) continue;
       if (!loaded) {
         sp = load_spec(specs + r);
         loaded = true;
@@ -398,11 +398,12 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
 }
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
-                       const int32_t* run_count, const int64_t* run_off, int64_t* times,
-                       hipStream_t st) {
+                       const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
+                       int64_t* times, hipStream_t st) {
   if (R <= 0) return;
   hipLaunchKernelGGL(k_write_walk, dim3(grid_for(R, 256, 256 * 16)), dim3(256),
-                     plan_lds_bytes(p), st, specs, R, p, run_anchor, run_count, run_off, times);
+                     plan_lds_bytes(p), st, specs, R, p, run_anchor, run_count, run_dmask, run_off,
+                     times);
 }
 
 void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,

@@ -25,13 +25,13 @@ static std::vector<uint8_t> slurp(const char* p) {
   return d;
 }
 
-static const char* atoms[6][12] = {
-    {"*/7", "0", "5", "*/20", "15/35", "10-40/3", "7,30,45", "59", "0/15", "3-3", "0", "58-59"},
-    {"*", "0", "30", "*/5", "20-35/15", "1,31,59", "5-7/2", "*/59", "10-12", "0", "0", "59"},
-    {"*", "0", "9", "23", "*/2", "1/2", "9-17", "22,23,0", "2", "1", "3", "0-23/5"},
-    {"*", "?", "1", "15", "31", "29", "30", "1,15", "*/2", "9-20", "28-31", "5/7"},
-    {"*", "?", "1", "2", "Feb", "Jan,Jul", "Apr-Oct", "*/3", "Mar", "Nov", "Dec", "*"},
-    {"*", "?", "0", "1-5", "Mon", "Sun", "mon/2", "Sat,Sun", "*/2", "3", "fri-sat", "*"}};
+static const char* atoms[6][16] = {
+    {"*/7", "0", "5", "*/20", "15/35", "10-40/3", "7,30,45", "59", "0/15", "3-3", "0", "58-59", "0", "0", "30", "*/30"},
+    {"*", "0", "30", "*/5", "20-35/15", "1,31,59", "5-7/2", "*/59", "10-12", "0", "0", "59", "45", "15", "0,30", "*/15"},
+    {"*", "0", "9", "23", "*/2", "1/2", "9-17", "22,23,0", "2", "1", "3", "0-23/5", "0", "1", "0,1", "23"},
+    {"*", "?", "1", "15", "31", "29", "30", "1,15", "*/2", "9-20", "28-31", "5/7", "8", "*", "?", "1-7"},
+    {"*", "?", "1", "2", "Feb", "Jan,Jul", "Apr-Oct", "*/3", "Mar", "Nov", "Dec", "*", "*", "*", "Oct", "Sep-Dec"},
+    {"*", "?", "0", "1-5", "Mon", "Sun", "mon/2", "Sat,Sun", "*/2", "3", "fri-sat", "*", "*", "0", "6", "?"}};
 
 static DSpec pack(const or_sched& s) {
   DSpec d{};
@@ -57,13 +57,13 @@ int main(int argc, char** argv) {
     zone_from_tzif(d.data(), d.size(), &zr, &e);
     or_loc_from_tzif(d.data(), d.size(), &ol);
   }
-  std::mt19937_64 rng(777);
+  std::mt19937_64 rng(argc > 3 ? strtoull(argv[3], nullptr, 10) : 777);
   std::vector<or_sched> scheds;
   std::vector<std::string> names;
   while ((int)scheds.size() < nspec) {
     std::string spec;
     if (rng() % 10 == 0) spec = "@every " + std::to_string(1 + rng() % 7200) + "s";
-    else for (int f = 0; f < 6; f++) { if (f) spec += " "; spec += atoms[f][rng() % 12]; }
+    else for (int f = 0; f < 6; f++) { if (f) spec += " "; spec += atoms[f][rng() % 16]; }
     or_sched s;
     char err[256];
     if (or_parse(OR_OPT_DEFAULT, spec.c_str(), spec.size(), &s, err, sizeof err)) continue;
@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
         const Segment& sg = plan.segs[s];
         if (d.kind == KIND_EVERY) {
           for (int k = 0; k < cnt[s]; k++) got.push_back(anc[s] + int64_t(k + 1) * int64_t(d.sec));
-        } else if (sg.kind == 0) {
+        } else if (!run_is_walked(sg, dm[s])) {
           CFRule c = cf_rule(d);
           // mimic the writer: seek at a random start, then step
           int k0 = cnt[s] ? int(rng() % cnt[s]) : 0;

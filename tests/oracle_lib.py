@@ -149,13 +149,29 @@ def sched_array(scheds):
 
 
 def expand_batch(arr, t0, t1, loc, threads=8, with_times=True):
-    """-> (offsets int64[R+1], times int64[E])"""
+    """-> (offsets int64[R+1], times int64[E]).  Raises NonTerminating if the
+    reference loop never ends for some rule (see stuck_rules)."""
     R = len(arr)
     off = np.zeros(R + 1, dtype=np.int64)
     L = lib()
     total = L.or_expand_batch(arr, R, t0, t1, loc.h, threads, off.ctypes.data, None)
+    if total < 0:
+        raise NonTerminating(stuck_rules(arr, t0, t1, loc))
     if not with_times:
         return off, None
     times = np.zeros(max(total, 1), dtype=np.int64)
     L.or_expand_batch(arr, R, t0, t1, loc.h, threads, off.ctypes.data, times.ctypes.data)
     return off, times[:total]
+
+
+class NonTerminating(Exception):
+    """The reference Next loop never terminates for these rule indices."""
+
+    def __init__(self, rules):
+        super().__init__(f"non-terminating reference loop for rules {rules[:10]}")
+        self.rules = rules
+
+
+def stuck_rules(arr, t0, t1, loc):
+    L = lib()
+    return [i for i in range(len(arr)) if L.or_expand(C.byref(arr[i]), t0, t1, loc.h, None, 0) < 0]
