@@ -220,6 +220,7 @@ int cg_init(int device, cg_ctx** out) {
   HIPCHK(hipSetDevice(device));
   cg_ctx* c = new cg_ctx();
   c->device = device;
+  c->write_blocks = std::max(1, prop.multiProcessorCount) * 4;  // 4 blocks x 4 waves per CU
   if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return cg_fail(CG_EHIP, "hipStreamCreate failed");
@@ -471,37 +472,48 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   launch_scan(c->run_count.p, c->run_off.p, nruns, c->scan_tmp.p, c->st);
   (void)hipEventRecord(c->ev[2], c->st);
   HIPCHK(hipGetLastError());
-  int64_t E = 0;
-  unsigned long long stuck = 0;
-  HIPCHK(hipMemcpyAsync(&E, c->run_off.p + nruns, 8, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipMemcpyAsync(&stuck, c->stuck.p, 8, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));
-  if (stuck != ~0ULL)
-    return cg_fail(CG_ERANGE, "rule " + std::to_string(stuck) +
-                                  ": the reference Next loop never terminates inside this horizon (Next "
-                                  "does not return, or returns a time <= its input and cycles)");
-  const int64_t nblocks = (E + kWriteChunk - 1) / kWriteChunk;
-  if ((rc = c->times.ensure(std::max<int64_t>(E, 1)))) return rc;
-  if ((rc = c->block_run.ensure(nblocks + 1))) return rc;
+  // Write phase without a host round trip: the chunk map and writers read the
+  // event total from device memory and size their work from it.  Output
+  // capacity comes from earlier calls; the first call (or a larger result)
+  // syncs once to size the buffers and relaunches the write phase.
+  if (c->times.cap == 0) {
+    int64_t E0 = 0;
+    HIPCHK(hipMemcpyAsync(&E0, c->run_off.p + nruns, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if ((rc = c->times.ensure(std::max<int64_t>(E0, 1)))) return rc;
+  }
   // walked runs: WALK windows, or CF segments whose entry fire does not fully
   // match (only possible when the plan has zone transitions)
-  bool has_walk = c->plan.segs.size() > 0 && c->plan.table.when.size() > 1;
+  bool has_walk = c->plan.table.when.size() > 1;
   for (const Segment& sg : c->plan.segs) has_walk |= sg.kind != 0;
-  (void)hipEventRecord(c->ev[3], c->st);
-  if (E > 0) launch_block_map(c->run_off.p, nruns, nblocks, c->block_run.p, c->st);
-  (void)hipEventRecord(c->ev[4], c->st);
-  if (E > 0)
-    launch_write_cf(s->d, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->run_off.p,
-                    nruns, c->block_run.p, nblocks, E, c->times.p, c->st);
-  (void)hipEventRecord(c->ev[5], c->st);
-  if (E > 0 && has_walk)
-    launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->run_off.p,
-                      c->times.p, c->st);
-  (void)hipEventRecord(c->ev[6], c->st);
-  launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->st);
-  (void)hipEventRecord(c->ev[7], c->st);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipStreamSynchronize(c->st));
+  int64_t E = 0;
+  unsigned long long stuck = 0;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const int64_t cap = int64_t(c->times.cap);
+    if ((rc = c->block_run.ensure(cap / kChunk + 2))) return rc;
+    (void)hipEventRecord(c->ev[3], c->st);
+    launch_chunk_map(c->run_off.p, nruns, cap, c->block_run.p, c->st);
+    (void)hipEventRecord(c->ev[4], c->st);
+    launch_write_cf(s->d, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->run_off.p, nruns,
+                    c->block_run.p, cap, c->times.p, c->write_blocks, c->st);
+    (void)hipEventRecord(c->ev[5], c->st);
+    if (has_walk)
+      launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p,
+                        c->run_off.p, cap, c->times.p, c->st);
+    (void)hipEventRecord(c->ev[6], c->st);
+    launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->st);
+    (void)hipEventRecord(c->ev[7], c->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(&E, c->run_off.p + nruns, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(&stuck, c->stuck.p, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipStreamSynchronize(c->st));
+    if (stuck != ~0ULL)
+      return cg_fail(CG_ERANGE, "rule " + std::to_string(stuck) +
+                                    ": the reference Next loop never terminates inside this horizon "
+                                    "(Next does not return, or returns a time <= its input and cycles)");
+    if (E <= cap) break;
+    if ((rc = c->times.ensure(E))) return rc;  // grow and redo the write phase
+  }
   (void)hipEventElapsedTime(&c->kt[0], c->ev[0], c->ev[1]);
   (void)hipEventElapsedTime(&c->kt[1], c->ev[1], c->ev[2]);
   (void)hipEventElapsedTime(&c->kt[2], c->ev[3], c->ev[4]);

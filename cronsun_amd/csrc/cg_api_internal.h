@@ -46,6 +46,7 @@ struct DBuf {
 
 struct cg_ctx {
   int device = 0;
+  int write_blocks = 1024;  // persistent k_write_cf grid (set from the CU count)
   hipStream_t st = nullptr;
   hipEvent_t ev[8] = {};
   std::mutex mu;

@@ -18,9 +18,14 @@ struct PlanArgs {
   int64_t t0, t1;
 };
 
+// per-node writer (cg_pernode.hip): 256 threads x 8 events per block
 constexpr int kWriteThreads = 256;
 constexpr int kWritePerThread = 8;
-constexpr int kWriteChunk = kWriteThreads * kWritePerThread;  // events per write block
+constexpr int kWriteChunk = kWriteThreads * kWritePerThread;
+// closed-form writer: 4 waves per block, 16 events per lane, 1024 per wave-chunk
+constexpr int kWriteWaves = 4;
+constexpr int kLaneEvents = 16;
+constexpr int kChunk = 64 * kLaneEvents;
 
 size_t plan_lds_bytes(const PlanArgs& p);
 
@@ -36,17 +41,18 @@ void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run
 size_t scan_temp_bytes(int64_t n);
 void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st);
 
-void launch_block_map(const int64_t* run_off, int64_t nruns, int64_t nblocks, int64_t* block_run,
+// chunk_run needs cap / kChunk + 2 entries; both read E = run_off[nruns] on
+// the device (no host sync) and do nothing when E > cap
+void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
                       hipStream_t st);
-
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
-                     int64_t nruns, const int64_t* block_run, int64_t nblocks, int64_t E,
-                     int64_t* times, hipStream_t st);
+                     int64_t nruns, const int64_t* chunk_run, int64_t cap, int64_t* times,
+                     int n_blocks, hipStream_t st);
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
                        const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
-                       int64_t* times, hipStream_t st);
+                       int64_t cap, int64_t* times, hipStream_t st);
 
 void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,
                          hipStream_t st);

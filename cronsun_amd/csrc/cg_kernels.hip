@@ -5,10 +5,11 @@
 //                Go walk, next_exact) and the closed-form count of the rest,
 //                or the walked count inside WALK windows -> run records
 //   k_scan_*     exclusive scan of run counts -> run offsets (int64)
-//   k_block_map  first run touched by each 2048-event output block
-//   k_write_cf   output-parallel: each lane materialises 8 consecutive fire
-//                times from the closed form, staged in LDS, then the block
-//                stores its 16 KiB slice with coalesced 16-B stores
+//   k_chunk_map  first run touched by each 1024-event output chunk
+//   k_write_cf   persistent, output-parallel: per wave-chunk each lane
+//                materialises 16 consecutive fire times from the closed form,
+//                staged in the wave's LDS slice, then stored as coalesced
+//                1 KiB wave-instructions
 //   k_write_walk re-walks the (rare) WALK-window runs
 //   k_rule_offs  rule-major CSR offsets
 // Integer and HBM-bound throughout: no MFMA.
@@ -199,25 +200,36 @@ __device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, i
   return lo;
 }
 
-__global__ void k_block_map(const int64_t* __restrict__ run_off, int64_t nruns, int64_t nblocks,
-                            int64_t* __restrict__ block_run) {
-  int64_t b = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (b > nblocks) return;
-  if (b == nblocks) {
-    block_run[b] = nruns - 1;
-    return;
-  }
-  block_run[b] = search_run(run_off, 0, nruns - 1, b * int64_t(kWriteChunk));
+// first run touched by each kChunk-event output chunk; E is read on the device
+// so the launch needs no host sync (grid sized by capacity, extra threads exit)
+__global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns,
+                            int64_t* __restrict__ chunk_run) {
+  const int64_t E = run_off[nruns];
+  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c <= nchunks;
+       c += int64_t(gridDim.x) * blockDim.x)
+    chunk_run[c] = c == nchunks ? nruns - 1 : search_run(run_off, 0, nruns - 1, c * int64_t(kChunk));
 }
 
-constexpr int kStageStride = kWritePerThread + 1;  // pad: conflict-free ds_write_b64
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
 
-__global__ __launch_bounds__(kWriteThreads) void k_write_cf(
+constexpr int kStageStride = kLaneEvents + 1;  // pad: conflict-free ds_write_b64 / ds_read_b64
+
+// Persistent, wave-granular closed-form writer.  Each wave takes 1024-event
+// output chunks (grid-stride); lane l materialises events [16l, 16l+16) of the
+// chunk: it locates its run with a 6-step shuffle search over the chunk's run
+// window, seeks once (rank/select), then steps the (day, h, m, s) iterator.
+// The chunk is staged in the wave's private LDS slice and stored as eight
+// coalesced 1 KiB wave-instructions (16 B/lane).
+__global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
     const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
-    const int64_t* __restrict__ run_off, int64_t nruns, const int64_t* __restrict__ block_run,
-    int64_t E, int64_t* __restrict__ times) {
-  __shared__ int64_t stage[kWriteThreads * kStageStride];
+    const int64_t* __restrict__ run_off, int64_t nruns, const int64_t* __restrict__ chunk_run,
+    int64_t cap, int64_t* __restrict__ times) {
+  __shared__ int64_t stage_all[kWriteWaves][64 * kStageStride];
   __shared__ Segment segs[64];
   extern __shared__ __align__(16) char dyn[];
   uint32_t* dtab = reinterpret_cast<uint32_t*>(dyn);
@@ -227,73 +239,96 @@ __global__ __launch_bounds__(kWriteThreads) void k_write_cf(
   __syncthreads();
 
   const int G = p.G;
-  const int64_t B0 = int64_t(blockIdx.x) * kWriteChunk;
-  int64_t i = B0 + int64_t(threadIdx.x) * kWritePerThread;
-  if (i < E) {
-    int64_t j = search_run(run_off, block_run[blockIdx.x], block_run[blockIdx.x + 1], i);
-    int64_t k = i - run_off[j];
-    int64_t n = run_count[j];
-    // per-run state
-    int kind = 0;  // 0 CF, 1 EVERY, 2 WALK (written later)
-    DSpec sp;
-    CFRule c;
-    CFIter it;
-    const Segment* sg = nullptr;
-    uint32_t dm = 0;
-    int64_t anchor = 0, D = 0;
-    bool fresh = true;
-#pragma unroll 1
-    for (int q = 0; q < kWritePerThread && i < E; q++, i++, k++) {
-      while (k >= n) {  // step to the next non-empty run
-        j++;
-        k = 0;
-        n = run_count[j];
-        fresh = true;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int64_t* stage = stage_all[wave];
+  const int64_t E = run_off[nruns];
+  if (E > cap) return;  // output buffer too small: host grows it and relaunches
+  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
+  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nchunks; c += nwaves) {
+    const int64_t base = c * kChunk;
+    int64_t i = base + int64_t(lane) * kLaneEvents;
+    const int64_t lo = chunk_run[c], hi = chunk_run[c + 1];
+    int64_t j;
+    if (hi - lo < 64) {
+      // largest j in [lo, hi] with run_off[j] <= i, by shuffles over 64 lanes
+      int64_t mine = (lo + lane <= hi) ? run_off[lo + lane] : INT64_MAX;
+      int pos = 0;
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1) {
+        int64_t v = __shfl(mine, pos + step, 64);
+        if (pos + step < 64 && v <= i) pos += step;
       }
-      if (fresh) {
-        fresh = false;
-        int64_t r = j / G;
-        int s = int(j - r * G);
-        sp = load_spec(specs + r);
-        anchor = run_anchor[j];
-        sg = &segs[s];
-        dm = run_dmask[j];
-        if (sp.kind == KIND_EVERY) {
-          kind = 1;
-          D = int64_t(sp.sec);
-        } else if (run_is_walked(*sg, dm)) {
-          kind = 2;  // written by k_write_walk
-        } else {
-          kind = 0;
-          c = cf_rule(sp);
-          it = cf_seek(c, *sg, dm, anchor, k);
-        }
-      } else if (kind == 0) {
-        cf_next(c, dm, it);
-      }
-      int64_t val;
-      if (kind == 0) val = cf_value(*sg, it);
-      else if (kind == 1) val = anchor + (k + 1) * D;
-      else val = 0;
-      stage[threadIdx.x * kStageStride + q] = val;
-    }
-  }
-  __syncthreads();
-  // coalesced store of the block's slice: lane l writes events (2l, 2l+1)
-  const int64_t lim = E - B0;
-  for (int e = threadIdx.x * 2; e < kWriteChunk; e += kWriteThreads * 2) {
-    if (e >= lim) break;
-    int t0 = e / kWritePerThread, q0 = e % kWritePerThread;
-    int64_t a = stage[t0 * kStageStride + q0];
-    if (e + 1 < lim) {
-      int64_t b = stage[t0 * kStageStride + q0 + 1];
-      longlong2 v;
-      v.x = a;
-      v.y = b;
-      *reinterpret_cast<longlong2*>(times + B0 + e) = v;
+      j = lo + pos;
     } else {
-      times[B0 + e] = a;
+      j = search_run(run_off, lo, hi, i < E ? i : E - 1);
     }
+    if (i < E) {
+      int64_t k = i - run_off[j];
+      int64_t n = run_count[j];
+      int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
+      DSpec sp;
+      CFRule cr;
+      CFIter it;
+      const Segment* sg = nullptr;
+      uint32_t dm = 0;
+      int64_t anchor = 0, D = 0;
+      bool fresh = true;
+#pragma unroll 1
+      for (int q = 0; q < kLaneEvents && i < E; q++, i++, k++) {
+        while (k >= n) {  // next non-empty run
+          j++;
+          k = 0;
+          n = run_count[j];
+          fresh = true;
+        }
+        if (fresh) {
+          fresh = false;
+          int64_t r = j / G;
+          int s = int(j - r * G);
+          sp = load_spec(specs + r);
+          anchor = run_anchor[j];
+          sg = &segs[s];
+          dm = run_dmask[j];
+          if (sp.kind == KIND_EVERY) {
+            kind = 1;
+            D = int64_t(sp.sec);
+          } else if (run_is_walked(*sg, dm)) {
+            kind = 2;
+          } else {
+            kind = 0;
+            cr = cf_rule(sp);
+            it = cf_seek(cr, *sg, dm, anchor, k);
+          }
+        } else if (kind == 0) {
+          cf_next(cr, dm, it);
+        }
+        int64_t val;
+        if (kind == 0) val = cf_value(*sg, it);
+        else if (kind == 1) val = anchor + (k + 1) * D;
+        else val = 0;
+        stage[lane * kStageStride + q] = val;
+      }
+    }
+    wave_lds_fence();
+    const int64_t lim = E - base;
+#pragma unroll
+    for (int it2 = 0; it2 < kChunk / 128; it2++) {
+      const int e = it2 * 128 + lane * 2;
+      if (e < lim) {
+        const int t = e >> 4, q = e & 15;
+        int64_t a = stage[t * kStageStride + q];
+        if (e + 1 < lim) {
+          longlong2 v;
+          v.x = a;
+          v.y = stage[t * kStageStride + q + 1];
+          *reinterpret_cast<longlong2*>(times + base + e) = v;
+        } else {
+          times[base + e] = a;
+        }
+      }
+    }
+    wave_lds_fence();
   }
 }
 
@@ -303,10 +338,11 @@ __global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ sp
                                                      const int32_t* __restrict__ run_count,
                                                      const uint32_t* __restrict__ run_dmask,
                                                      const int64_t* __restrict__ run_off,
-                                                     int64_t* __restrict__ times) {
+                                                     int64_t cap, int64_t* __restrict__ times) {
   extern __shared__ __align__(16) char lds[];
   PlanView v = stage_plan(p, lds);
   const int G = p.G;
+  if (run_off[int64_t(R) * G] > cap) return;
   for (int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; r < R;
        r += int64_t(gridDim.x) * blockDim.x) {
     DSpec sp;
@@ -381,29 +417,29 @@ void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStre
   hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out);
 }
 
-void launch_block_map(const int64_t* run_off, int64_t nruns, int64_t nblocks, int64_t* block_run,
+void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
                       hipStream_t st) {
-  hipLaunchKernelGGL(k_block_map, dim3(grid_for(nblocks + 1, 256, 1 << 30)), dim3(256), 0, st,
-                     run_off, nruns, nblocks, block_run);
+  int64_t max_chunks = cap / kChunk + 1;
+  hipLaunchKernelGGL(k_chunk_map, dim3(grid_for(max_chunks + 1, 256, 4096)), dim3(256), 0, st,
+                     run_off, nruns, chunk_run);
 }
 
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
-                     int64_t nruns, const int64_t* block_run, int64_t nblocks, int64_t E,
-                     int64_t* times, hipStream_t st) {
-  if (E <= 0) return;
-  hipLaunchKernelGGL(k_write_cf, dim3(nblocks), dim3(kWriteThreads),
+                     int64_t nruns, const int64_t* chunk_run, int64_t cap, int64_t* times,
+                     int n_blocks, hipStream_t st) {
+  hipLaunchKernelGGL(k_write_cf, dim3(n_blocks), dim3(kWriteWaves * 64),
                      align_up(size_t(p.nd) * 4, 16), st, specs, p, run_anchor, run_count,
-                     run_dmask, run_off, nruns, block_run, E, times);
+                     run_dmask, run_off, nruns, chunk_run, cap, times);
 }
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
                        const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
-                       int64_t* times, hipStream_t st) {
+                       int64_t cap, int64_t* times, hipStream_t st) {
   if (R <= 0) return;
   hipLaunchKernelGGL(k_write_walk, dim3(grid_for(R, 256, 256 * 16)), dim3(256),
                      plan_lds_bytes(p), st, specs, R, p, run_anchor, run_count, run_dmask, run_off,
-                     times);
+                     cap, times);
 }
 
 void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,
