@@ -211,19 +211,14 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns,
     chunk_run[c] = c == nchunks ? nruns - 1 : search_run(run_off, 0, nruns - 1, c * int64_t(kChunk));
 }
 
-__device__ __forceinline__ void wave_lds_fence() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-}
-
 constexpr int kStageStride = kLaneEvents + 1;  // pad: conflict-free ds_write_b64 / ds_read_b64
 
-// Persistent, wave-granular closed-form writer.  Each wave takes 1024-event
-// output chunks (grid-stride); lane l materialises events [16l, 16l+16) of the
-// chunk: it locates its run with a 6-step shuffle search over the chunk's run
-// window, seeks once (rank/select), then steps the (day, h, m, s) iterator.
-// The chunk is staged in the wave's private LDS slice and stored as eight
-// coalesced 1 KiB wave-instructions (16 B/lane).
+// Persistent closed-form writer.  Each wave owns one 1024-event output chunk
+// per iteration (grid-stride over groups of 4 chunks); lane l materialises
+// events [16l, 16l+16) of the chunk: it locates its run with a 6-step shuffle
+// search over the chunk's run window, seeks once (rank/select), then steps the
+// (day, h, m, s) iterator.  The chunk is staged in the wave's LDS slice and,
+// after a block barrier, stored as eight coalesced 1 KiB wave-instructions.
 __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
     const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
@@ -244,91 +239,97 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
   const int64_t E = run_off[nruns];
   if (E > cap) return;  // output buffer too small: host grows it and relaunches
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
-  const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
-  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nchunks; c += nwaves) {
+  // block-synchronous grid-stride over groups of kWriteWaves chunks: every
+  // wave reaches both barriers on every iteration
+  for (int64_t cb = blockIdx.x; cb * kWriteWaves < nchunks; cb += gridDim.x) {
+    const int64_t c = cb * kWriteWaves + wave;
     const int64_t base = c * kChunk;
-    int64_t i = base + int64_t(lane) * kLaneEvents;
-    const int64_t lo = chunk_run[c], hi = chunk_run[c + 1];
-    int64_t j;
-    if (hi - lo < 64) {
-      // largest j in [lo, hi] with run_off[j] <= i, by shuffles over 64 lanes
-      int64_t mine = (lo + lane <= hi) ? run_off[lo + lane] : INT64_MAX;
-      int pos = 0;
+    if (c < nchunks) {
+      int64_t i = base + int64_t(lane) * kLaneEvents;
+      const int64_t lo = chunk_run[c], hi = chunk_run[c + 1];
+      int64_t j;
+      if (hi - lo < 64) {
+        // largest j in [lo, hi] with run_off[j] <= i, by shuffles over 64 lanes
+        int64_t mine = (lo + lane <= hi) ? run_off[lo + lane] : INT64_MAX;
+        int pos = 0;
 #pragma unroll
-      for (int step = 32; step > 0; step >>= 1) {
-        int64_t v = __shfl(mine, pos + step, 64);
-        if (pos + step < 64 && v <= i) pos += step;
+        for (int step = 32; step > 0; step >>= 1) {
+          int64_t v = __shfl(mine, (pos + step) & 63, 64);
+          if (pos + step < 64 && v <= i) pos += step;
+        }
+        j = lo + pos;
+      } else {
+        j = search_run(run_off, lo, hi, i < E ? i : E - 1);
       }
-      j = lo + pos;
-    } else {
-      j = search_run(run_off, lo, hi, i < E ? i : E - 1);
-    }
-    if (i < E) {
-      int64_t k = i - run_off[j];
-      int64_t n = run_count[j];
-      int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
-      DSpec sp;
-      CFRule cr;
-      CFIter it;
-      const Segment* sg = nullptr;
-      uint32_t dm = 0;
-      int64_t anchor = 0, D = 0;
-      bool fresh = true;
+      if (i < E) {
+        int64_t k = i - run_off[j];
+        int64_t n = run_count[j];
+        int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
+        DSpec sp;
+        CFRule cr;
+        CFIter it;
+        const Segment* sg = nullptr;
+        uint32_t dm = 0;
+        int64_t anchor = 0, D = 0;
+        bool fresh = true;
 #pragma unroll 1
-      for (int q = 0; q < kLaneEvents && i < E; q++, i++, k++) {
-        while (k >= n) {  // next non-empty run
-          j++;
-          k = 0;
-          n = run_count[j];
-          fresh = true;
-        }
-        if (fresh) {
-          fresh = false;
-          int64_t r = j / G;
-          int s = int(j - r * G);
-          sp = load_spec(specs + r);
-          anchor = run_anchor[j];
-          sg = &segs[s];
-          dm = run_dmask[j];
-          if (sp.kind == KIND_EVERY) {
-            kind = 1;
-            D = int64_t(sp.sec);
-          } else if (run_is_walked(*sg, dm)) {
-            kind = 2;
-          } else {
-            kind = 0;
-            cr = cf_rule(sp);
-            it = cf_seek(cr, *sg, dm, anchor, k);
+        for (int q = 0; q < kLaneEvents && i < E; q++, i++, k++) {
+          while (k >= n) {  // next non-empty run
+            j++;
+            k = 0;
+            n = run_count[j];
+            fresh = true;
           }
-        } else if (kind == 0) {
-          cf_next(cr, dm, it);
+          if (fresh) {
+            fresh = false;
+            int64_t r = j / G;
+            int s = int(j - r * G);
+            sp = load_spec(specs + r);
+            anchor = run_anchor[j];
+            sg = &segs[s];
+            dm = run_dmask[j];
+            if (sp.kind == KIND_EVERY) {
+              kind = 1;
+              D = int64_t(sp.sec);
+            } else if (run_is_walked(*sg, dm)) {
+              kind = 2;
+            } else {
+              kind = 0;
+              cr = cf_rule(sp);
+              it = cf_seek(cr, *sg, dm, anchor, k);
+            }
+          } else if (kind == 0) {
+            cf_next(cr, dm, it);
+          }
+          int64_t val;
+          if (kind == 0) val = cf_value(*sg, it);
+          else if (kind == 1) val = anchor + (k + 1) * D;
+          else val = 0;
+          stage[lane * kStageStride + q] = val;
         }
-        int64_t val;
-        if (kind == 0) val = cf_value(*sg, it);
-        else if (kind == 1) val = anchor + (k + 1) * D;
-        else val = 0;
-        stage[lane * kStageStride + q] = val;
       }
     }
-    wave_lds_fence();
-    const int64_t lim = E - base;
+    __syncthreads();
+    if (c < nchunks) {
+      const int64_t lim = E - base;
 #pragma unroll
-    for (int it2 = 0; it2 < kChunk / 128; it2++) {
-      const int e = it2 * 128 + lane * 2;
-      if (e < lim) {
-        const int t = e >> 4, q = e & 15;
-        int64_t a = stage[t * kStageStride + q];
-        if (e + 1 < lim) {
-          longlong2 v;
-          v.x = a;
-          v.y = stage[t * kStageStride + q + 1];
-          *reinterpret_cast<longlong2*>(times + base + e) = v;
-        } else {
-          times[base + e] = a;
+      for (int it2 = 0; it2 < kChunk / 128; it2++) {
+        const int e = it2 * 128 + lane * 2;
+        if (e < lim) {
+          const int t = e >> 4, q = e & 15;
+          int64_t a = stage[t * kStageStride + q];
+          if (e + 1 < lim) {
+            longlong2 v;
+            v.x = a;
+            v.y = stage[t * kStageStride + q + 1];
+            *reinterpret_cast<longlong2*>(times + base + e) = v;
+          } else {
+            times[base + e] = a;
+          }
         }
       }
     }
-    wave_lds_fence();
+    __syncthreads();
   }
 }
 

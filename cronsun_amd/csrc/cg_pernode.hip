@@ -47,9 +47,12 @@ struct RulesDev {
   int32_t R, G, N, words;
 };
 
+// wave-local LDS hand-off (the rules of HIP's __syncwarp: release fence,
+// wave barrier, acquire fence)
 __device__ __forceinline__ void wave_sync_lds() {
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 __device__ __forceinline__ void bm_set(uint32_t* bm, int32_t n, int32_t N) {
