@@ -202,9 +202,10 @@ __device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, i
 
 // first run touched by each kChunk-event output chunk; E is read on the device
 // so the launch needs no host sync (grid sized by capacity, extra threads exit)
-__global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns,
+__global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, int64_t cap,
                             int64_t* __restrict__ chunk_run) {
   const int64_t E = run_off[nruns];
+  if (E > cap) return;  // chunk_run holds cap / kChunk + 2 entries
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
   for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c <= nchunks;
        c += int64_t(gridDim.x) * blockDim.x)
@@ -422,7 +423,7 @@ void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_
                       hipStream_t st) {
   int64_t max_chunks = cap / kChunk + 1;
   hipLaunchKernelGGL(k_chunk_map, dim3(grid_for(max_chunks + 1, 256, 4096)), dim3(256), 0, st,
-                     run_off, nruns, chunk_run);
+                     run_off, nruns, cap, chunk_run);
 }
 
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
