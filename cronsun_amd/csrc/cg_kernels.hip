@@ -15,6 +15,8 @@
 // Integer and HBM-bound throughout: no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "cg_expand.h"
 #include "cg_kernels.h"
 
@@ -220,6 +222,10 @@ constexpr int kStageStride = kLaneEvents + 1;  // pad: conflict-free ds_write_b6
 // search over the chunk's run window, seeks once (rank/select), then steps the
 // (day, h, m, s) iterator.  The chunk is staged in the wave's LDS slice and,
 // after a block barrier, stored as eight coalesced 1 KiB wave-instructions.
+// ABLATE (diagnostic builds of the same kernel, selected by CG_ABLATE):
+//   0 normal; 1 generate but skip the global stores; 2 store without
+//   generating; 3 locate only.
+template <int ABLATE>
 __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
     const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
@@ -262,7 +268,8 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
       } else {
         j = search_run(run_off, lo, hi, i < E ? i : E - 1);
       }
-      if (i < E) {
+      if (ABLATE == 3 && i < E) stage[lane * kStageStride] = j;
+      if ((ABLATE == 0 || ABLATE == 1) && i < E) {
         int64_t k = i - run_off[j];
         int64_t n = run_count[j];
         int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
@@ -311,7 +318,10 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
       }
     }
     __syncthreads();
-    if (c < nchunks) {
+    if (ABLATE == 1 || ABLATE == 3) {
+      // keep the generated values live without storing them
+      if (c < nchunks && stage[lane * kStageStride] == INT64_MIN + 7) times[base] = 0;
+    } else if (c < nchunks) {
       const int64_t lim = E - base;
 #pragma unroll
       for (int it2 = 0; it2 < kChunk / 128; it2++) {
@@ -430,9 +440,25 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
                      int64_t nruns, const int64_t* chunk_run, int64_t cap, int64_t* times,
                      int n_blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_write_cf, dim3(n_blocks), dim3(kWriteWaves * 64),
-                     align_up(size_t(p.nd) * 4, 16), st, specs, p, run_anchor, run_count,
-                     run_dmask, run_off, nruns, chunk_run, cap, times);
+  static const int ablate = [] {
+    const char* e = getenv("CG_ABLATE");
+    return e ? atoi(e) : 0;
+  }();
+  size_t lds = align_up(size_t(p.nd) * 4, 16);
+  if (ablate == 4) {  // reference: plain fill of the same output bytes
+    (void)hipMemsetAsync(times, 0, size_t(cap) * 8, st);
+    return;
+  }
+#define CG_LAUNCH_WCF(A)                                                                     \
+  hipLaunchKernelGGL(k_write_cf<A>, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p, \
+                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times)
+  switch (ablate) {
+    case 1: CG_LAUNCH_WCF(1); break;
+    case 2: CG_LAUNCH_WCF(2); break;
+    case 3: CG_LAUNCH_WCF(3); break;
+    default: CG_LAUNCH_WCF(0); break;
+  }
+#undef CG_LAUNCH_WCF
 }
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
