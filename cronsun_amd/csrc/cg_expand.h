@@ -18,6 +18,7 @@ namespace cg {
 struct CFRule {
   uint64_t M, S;
   uint32_t H, nM, nS, nMS, C;
+  int32_t s0, m0, h0;  // lowest set bit of S, M, H
 };
 
 CG_HD CFRule cf_rule(const DSpec& sp) {
@@ -29,6 +30,9 @@ CG_HD CFRule cf_rule(const DSpec& sp) {
   c.nS = (uint32_t)__builtin_popcountll(c.S);
   c.nMS = c.nM * c.nS;
   c.C = (uint32_t)__builtin_popcount(c.H) * c.nMS;
+  c.s0 = c.S ? __builtin_ctzll(c.S) : 0;
+  c.m0 = c.M ? __builtin_ctzll(c.M) : 0;
+  c.h0 = c.H ? __builtin_ctz(c.H) : 0;
   return c;
 }
 
@@ -68,23 +72,37 @@ struct CFIter {
   int32_t day, h, m, s;
 };
 
-// iterator state of the k-th (k >= 0) fire counted from the anchor fire uf
-CG_HD CFIter cf_seek(const CFRule& c, const Segment& sg, uint32_t dmask, int64_t uf, int64_t k) {
-  int32_t rf = (int32_t)(uf - sg.base);
-  int32_t jf = rf / 86400, tf = rf - jf * 86400;
-  uint64_t idx = (uint64_t)cf_rank(c, tf) - 1 + (uint64_t)k;
+// iterator state of the anchor fire itself (k = 0): plain decode, no rank/select
+CG_HD CFIter cf_decode(const Segment& sg, int64_t uf) {
+  uint32_t rf = (uint32_t)(uf - sg.base);
+  uint32_t day = rf / 86400u, tod = rf - day * 86400u;
   CFIter it;
-  it.day = jf;
+  it.day = (int32_t)day;
+  it.h = (int32_t)(tod / 3600u);
+  uint32_t r = tod - (uint32_t)it.h * 3600u;
+  it.m = (int32_t)(r / 60u);
+  it.s = (int32_t)(r - (uint32_t)it.m * 60u);
+  return it;
+}
+
+// iterator state of the k-th (k >= 0) fire counted from the anchor fire uf
+// (32-bit: a segment holds at most 31 days x 86400 combinations)
+CG_HD CFIter cf_seek(const CFRule& c, const Segment& sg, uint32_t dmask, int64_t uf, int64_t k) {
+  if (k == 0) return cf_decode(sg, uf);
+  uint32_t rf = (uint32_t)(uf - sg.base);
+  uint32_t jf = rf / 86400u, tf = rf - jf * 86400u;
+  uint32_t idx = cf_rank(c, (int32_t)tf) - 1u + (uint32_t)k;
+  CFIter it;
+  it.day = (int32_t)jf;
   if (idx >= c.C) {
     idx -= c.C;
-    uint32_t dskip = (uint32_t)(idx / c.C);
-    idx -= (uint64_t)dskip * c.C;
+    uint32_t dskip = idx / c.C;
+    idx -= dskip * c.C;
     uint64_t above = (uint64_t)dmask & ~((2ull << jf) - 1ull);
     it.day = select64(above, dskip);
   }
-  uint32_t i32 = (uint32_t)idx;
-  uint32_t hi = i32 / c.nMS;
-  uint32_t rem = i32 - hi * c.nMS;
+  uint32_t hi = idx / c.nMS;
+  uint32_t rem = idx - hi * c.nMS;
   uint32_t mi = rem / c.nS;
   uint32_t si = rem - mi * c.nS;
   it.h = select64(c.H, hi);
@@ -93,21 +111,28 @@ CG_HD CFIter cf_seek(const CFRule& c, const Segment& sg, uint32_t dmask, int64_t
   return it;
 }
 
+// next matching (day, h, m, s), branch-free: the carries are selects, so lanes
+// of a wave at different phases of the same (or another) rule do not diverge
 CG_HD void cf_next(const CFRule& c, uint32_t dmask, CFIter& it) {
-  int32_t s = next_bit64(c.S, it.s);
-  if (s < 64) { it.s = s; return; }
-  it.s = __builtin_ctzll(c.S);
-  int32_t m = next_bit64(c.M, it.m);
-  if (m < 64) { it.m = m; return; }
-  it.m = __builtin_ctzll(c.M);
-  int32_t h = next_bit32(c.H, it.h);
-  if (h < 32) { it.h = h; return; }
-  it.h = __builtin_ctz(c.H);
-  it.day = next_bit32(dmask, it.day);
+  uint64_t rs = c.S & (~0ull << (it.s + 1));   // it.s <= 59
+  uint64_t rm = c.M & (~0ull << (it.m + 1));   // it.m <= 59
+  uint32_t rh = c.H & (~0u << (it.h + 1));      // it.h <= 23
+  uint32_t rd = (it.day >= 31) ? 0u : (dmask & (~0u << (it.day + 1)));
+  int32_t s1 = rs ? __builtin_ctzll(rs) : 64;
+  int32_t m1 = rm ? __builtin_ctzll(rm) : 64;
+  int32_t h1 = rh ? __builtin_ctz(rh) : 32;
+  int32_t d1 = rd ? __builtin_ctz(rd) : 32;
+  bool os = s1 >= 64;
+  bool om = os && m1 >= 64;
+  bool oh = om && h1 >= 32;
+  it.s = os ? c.s0 : s1;
+  it.m = os ? (om ? c.m0 : m1) : it.m;
+  it.h = om ? (oh ? c.h0 : h1) : it.h;
+  it.day = oh ? d1 : it.day;
 }
 
 CG_HD int64_t cf_value(const Segment& sg, const CFIter& it) {
-  return sg.base + (int64_t)(it.day * 86400 + it.h * 3600 + it.m * 60 + it.s);
+  return sg.base + (int64_t)(uint32_t)(it.day * 86400 + it.h * 3600 + it.m * 60 + it.s);
 }
 
 // Run records of one rule over the plan's G segments (k_count's body).

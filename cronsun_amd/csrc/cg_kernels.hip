@@ -270,53 +270,51 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
       }
       if (ABLATE == 3 && i < E) stage[lane * kStageStride] = j;
       if ((ABLATE == 0 || ABLATE == 1) && i < E) {
-        int64_t k = i - run_off[j];
-        int64_t n = run_count[j];
+        const int32_t qmax = int32_t(E - i < kLaneEvents ? E - i : kLaneEvents);
+        int32_t k = int32_t(i - run_off[j]);
+        int32_t n = run_count[j];
         int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
-        DSpec sp;
         CFRule cr;
         CFIter it;
-        const Segment* sg = nullptr;
+        const Segment* sg = &segs[0];
         uint32_t dm = 0;
         int64_t anchor = 0, D = 0;
-        bool fresh = true;
+        // enter run j at its k-th fire
+        auto enter = [&]() {
+          int64_t r = G == 1 ? j : j / G;
+          int s = int(j - r * G);
+          DSpec sp = load_spec(specs + r);
+          anchor = run_anchor[j];
+          sg = &segs[s];
+          dm = run_dmask[j];
+          if (sp.kind == KIND_EVERY) {
+            kind = 1;
+            D = int64_t(sp.sec);
+          } else if (run_is_walked(*sg, dm)) {
+            kind = 2;
+          } else {
+            kind = 0;
+            cr = cf_rule(sp);
+            it = cf_seek(cr, *sg, dm, anchor, k);
+          }
+        };
+        enter();
 #pragma unroll 1
-        for (int q = 0; q < kLaneEvents && i < E; q++, i++, k++) {
-          while (k >= n) {  // next non-empty run
-            j++;
+        for (int q = 0; q < qmax; q++) {
+          if (k >= n) {  // next non-empty run (its first fire)
+            do {
+              j++;
+              n = run_count[j];
+            } while (n == 0);
             k = 0;
-            n = run_count[j];
-            fresh = true;
+            enter();
           }
-          if (fresh) {
-            fresh = false;
-            int64_t r = j / G;
-            int s = int(j - r * G);
-            sp = load_spec(specs + r);
-            anchor = run_anchor[j];
-            sg = &segs[s];
-            dm = run_dmask[j];
-            if (sp.kind == KIND_EVERY) {
-              kind = 1;
-              D = int64_t(sp.sec);
-            } else if (run_is_walked(*sg, dm)) {
-              kind = 2;
-            } else {
-              kind = 0;
-              cr = cf_rule(sp);
-              it = cf_seek(cr, *sg, dm, anchor, k);
-            }
-          } else if (kind == 0) {
-            cf_next(cr, dm, it);
-          }
-          int64_t val;
-          if (kind == 0) val = cf_value(*sg, it);
-          else if (kind == 1) val = anchor + (k + 1) * D;
-          else val = 0;
+          int64_t val = kind == 0 ? cf_value(*sg, it) : (kind == 1 ? anchor + int64_t(k + 1) * D : 0);
           stage[lane * kStageStride + q] = val;
+          if (kind == 0) cf_next(cr, dm, it);
+          k++;
         }
       }
-    }
     __syncthreads();
     if (ABLATE == 1 || ABLATE == 3) {
       // keep the generated values live without storing them
