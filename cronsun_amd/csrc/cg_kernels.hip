@@ -315,6 +315,7 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
           k++;
         }
       }
+    }
     __syncthreads();
     if (ABLATE == 1 || ABLATE == 3) {
       // keep the generated values live without storing them
