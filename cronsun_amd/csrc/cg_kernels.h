@@ -22,9 +22,9 @@ struct PlanArgs {
 constexpr int kWriteThreads = 256;
 constexpr int kWritePerThread = 8;
 constexpr int kWriteChunk = kWriteThreads * kWritePerThread;
-// closed-form writer: 4 waves per block, 16 events per lane, 1024 per wave-chunk
+// closed-form writer: 4 waves per block, 8 events per lane, 512 per wave-chunk
 constexpr int kWriteWaves = 4;
-constexpr int kLaneEvents = 16;
+constexpr int kLaneEvents = 8;
 constexpr int kChunk = 64 * kLaneEvents;
 
 size_t plan_lds_bytes(const PlanArgs& p);

@@ -216,15 +216,29 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 
 constexpr int kStageStride = kLaneEvents + 1;  // pad: conflict-free ds_write_b64 / ds_read_b64
 
-// Persistent closed-form writer.  Each wave owns one 1024-event output chunk
-// per iteration (grid-stride over groups of 4 chunks); lane l materialises
-// events [16l, 16l+16) of the chunk: it locates its run with a 6-step shuffle
-// search over the chunk's run window, seeks once (rank/select), then steps the
-// (day, h, m, s) iterator.  The chunk is staged in the wave's LDS slice and,
-// after a block barrier, stored as eight coalesced 1 KiB wave-instructions.
+// run data of a chunk's run window, staged once per chunk in the wave's LDS
+struct WinRun {
+  int64_t off;     // run_off[j]
+  int64_t anchor;  // run_anchor[j]
+  DSpec sp;        // specs[j / G]
+  int32_t count;   // run_count[j]
+  uint32_t dmask;  // run_dmask[j]
+  int32_t seg;     // j % G
+  int32_t pad;
+};
+
+// Persistent closed-form writer.  Waves work independently: each takes
+// kChunk-event output chunks grid-stride.  Per chunk it loads the window of
+// (at most 64) runs the chunk touches with one round of coalesced loads into
+// its LDS slice, so a lane entering a run reads LDS instead of chasing
+// dependent global loads.  Lane l then materialises events [8l, 8l+8) of the
+// chunk (seek once, then the branch-free iterator), stages them in LDS, and
+// the wave stores the chunk as coalesced 1 KiB wave-instructions.  Chunks
+// touching more than 64 runs (long stretches of empty or single-fire rules)
+// take a slower per-lane path with direct global loads.
+//
 // ABLATE (diagnostic builds of the same kernel, selected by CG_ABLATE):
-//   0 normal; 1 generate but skip the global stores; 2 store without
-//   generating; 3 locate only.
+//   0 normal; 1 generate but skip the global stores; 3 locate only.
 template <int ABLATE>
 __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
@@ -232,6 +246,7 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
     const int64_t* __restrict__ run_off, int64_t nruns, const int64_t* __restrict__ chunk_run,
     int64_t cap, int64_t* __restrict__ times) {
   __shared__ int64_t stage_all[kWriteWaves][64 * kStageStride];
+  __shared__ WinRun win_all[kWriteWaves][64];
   __shared__ Segment segs[64];
   extern __shared__ __align__(16) char dyn[];
   uint32_t* dtab = reinterpret_cast<uint32_t*>(dyn);
@@ -243,90 +258,112 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
   const int G = p.G;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int64_t* stage = stage_all[wave];
+  WinRun* win = win_all[wave];
   const int64_t E = run_off[nruns];
   if (E > cap) return;  // output buffer too small: host grows it and relaunches
   const int64_t nchunks = (E + kChunk - 1) / kChunk;
-  // block-synchronous grid-stride over groups of kWriteWaves chunks: every
-  // wave reaches both barriers on every iteration
-  for (int64_t cb = blockIdx.x; cb * kWriteWaves < nchunks; cb += gridDim.x) {
-    const int64_t c = cb * kWriteWaves + wave;
+  const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
+  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nchunks; c += nwaves) {
     const int64_t base = c * kChunk;
-    if (c < nchunks) {
-      int64_t i = base + int64_t(lane) * kLaneEvents;
-      const int64_t lo = chunk_run[c], hi = chunk_run[c + 1];
-      int64_t j;
-      if (hi - lo < 64) {
-        // largest j in [lo, hi] with run_off[j] <= i, by shuffles over 64 lanes
-        int64_t mine = (lo + lane <= hi) ? run_off[lo + lane] : INT64_MAX;
-        int pos = 0;
+    const int64_t lo = chunk_run[c], hi = chunk_run[c + 1];
+    int64_t i = base + int64_t(lane) * kLaneEvents;
+    const bool fast = hi - lo < 64;
+    int64_t j;
+    if (fast) {
+      // window: one coalesced round of loads, then LDS
+      const int64_t jl = lo + lane <= hi ? lo + lane : hi;
+      WinRun w;
+      w.off = run_off[jl];
+      w.count = lo + lane <= hi ? run_count[jl] : 0;
+      w.anchor = run_anchor[jl];
+      w.dmask = run_dmask[jl];
+      const int64_t r = G == 1 ? jl : jl / G;
+      w.seg = int32_t(jl - r * G);
+      w.sp = load_spec(specs + r);
+      w.pad = 0;
+      win[lane] = w;
+      // largest j in [lo, hi] with run_off[j] <= i, by shuffles over 64 lanes
+      const int64_t mine = lo + lane <= hi ? w.off : INT64_MAX;
+      int pos = 0;
 #pragma unroll
-        for (int step = 32; step > 0; step >>= 1) {
-          int64_t v = __shfl(mine, (pos + step) & 63, 64);
-          if (pos + step < 64 && v <= i) pos += step;
-        }
-        j = lo + pos;
-      } else {
-        j = search_run(run_off, lo, hi, i < E ? i : E - 1);
+      for (int step = 32; step > 0; step >>= 1) {
+        int64_t v = __shfl(mine, (pos + step) & 63, 64);
+        if (pos + step < 64 && v <= i) pos += step;
       }
-      if (ABLATE == 3 && i < E) stage[lane * kStageStride] = j;
-      if ((ABLATE == 0 || ABLATE == 1) && i < E) {
-        const int32_t qmax = int32_t(E - i < kLaneEvents ? E - i : kLaneEvents);
-        int32_t k = int32_t(i - run_off[j]);
-        int32_t n = run_count[j];
-        int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
-        CFRule cr;
-        CFIter it;
-        const Segment* sg = &segs[0];
-        uint32_t dm = 0;
-        int64_t anchor = 0, D = 0;
-        // enter run j at its k-th fire
-        auto enter = [&]() {
-          int64_t r = G == 1 ? j : j / G;
-          int s = int(j - r * G);
-          DSpec sp = load_spec(specs + r);
-          anchor = run_anchor[j];
-          sg = &segs[s];
-          dm = run_dmask[j];
-          if (sp.kind == KIND_EVERY) {
-            kind = 1;
-            D = int64_t(sp.sec);
-          } else if (run_is_walked(*sg, dm)) {
-            kind = 2;
-          } else {
-            kind = 0;
-            cr = cf_rule(sp);
-            it = cf_seek(cr, *sg, dm, anchor, k);
-          }
-        };
-        enter();
-#pragma unroll 1
-        for (int q = 0; q < qmax; q++) {
-          if (k >= n) {  // next non-empty run (its first fire)
-            do {
-              j++;
-              n = run_count[j];
-            } while (n == 0);
-            k = 0;
-            enter();
-          }
-          int64_t val = kind == 0 ? cf_value(*sg, it) : (kind == 1 ? anchor + int64_t(k + 1) * D : 0);
-          stage[lane * kStageStride + q] = val;
-          if (kind == 0) cf_next(cr, dm, it);
-          k++;
+      j = pos;  // window-relative
+    } else {
+      j = search_run(run_off, lo, hi, i < E ? i : E - 1);
+    }
+    __syncwarp();
+    if (ABLATE == 3 && i < E) stage[lane * kStageStride] = j;
+    if (ABLATE != 3 && i < E) {
+      const int32_t qmax = int32_t(E - i < kLaneEvents ? E - i : kLaneEvents);
+      int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
+      CFRule cr;
+      CFIter it;
+      const Segment* sg = &segs[0];
+      uint32_t dm = 0;
+      int64_t anchor = 0, D = 0;
+      int32_t k, n;
+      // enter run j (window-relative when fast) at its k-th fire
+      auto enter = [&](const DSpec& sp) {
+        if (sp.kind == KIND_EVERY) {
+          kind = 1;
+          D = int64_t(sp.sec);
+        } else if (run_is_walked(*sg, dm)) {
+          kind = 2;
+        } else {
+          kind = 0;
+          cr = cf_rule(sp);
+          it = cf_seek(cr, *sg, dm, anchor, k);
         }
+      };
+      auto load_run = [&]() {
+        if (fast) {
+          const WinRun& w = win[j];
+          n = w.count;
+          anchor = w.anchor;
+          dm = w.dmask;
+          sg = &segs[w.seg];
+          enter(w.sp);
+        } else {
+          const int64_t r = G == 1 ? j : j / G;
+          n = run_count[j];
+          anchor = run_anchor[j];
+          dm = run_dmask[j];
+          sg = &segs[int(j - r * G)];
+          enter(load_spec(specs + r));
+        }
+      };
+      k = int32_t(i - (fast ? win[j].off : run_off[j]));
+      load_run();
+#pragma unroll 1
+      for (int q = 0; q < qmax; q++) {
+        if (k >= n) {  // next non-empty run, entered at its first fire
+          do {
+            j++;
+            n = fast ? win[j].count : run_count[j];
+          } while (n == 0);
+          k = 0;
+          load_run();
+        }
+        int64_t val = kind == 0 ? cf_value(*sg, it) : (kind == 1 ? anchor + int64_t(k + 1) * D : 0);
+        stage[lane * kStageStride + q] = val;
+        if (kind == 0) cf_next(cr, dm, it);
+        k++;
       }
     }
-    __syncthreads();
+    __syncwarp();
     if (ABLATE == 1 || ABLATE == 3) {
       // keep the generated values live without storing them
-      if (c < nchunks && stage[lane * kStageStride] == INT64_MIN + 7) times[base] = 0;
-    } else if (c < nchunks) {
+      if (stage[lane * kStageStride] == INT64_MIN + 7) times[base] = 0;
+    } else {
       const int64_t lim = E - base;
 #pragma unroll
       for (int it2 = 0; it2 < kChunk / 128; it2++) {
         const int e = it2 * 128 + lane * 2;
         if (e < lim) {
-          const int t = e >> 4, q = e & 15;
+          const int t = e / kLaneEvents, q = e % kLaneEvents;
           int64_t a = stage[t * kStageStride + q];
           if (e + 1 < lim) {
             longlong2 v;
@@ -339,7 +376,7 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
         }
       }
     }
-    __syncthreads();
+    __syncwarp();
   }
 }
 
@@ -453,7 +490,6 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
                      run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times)
   switch (ablate) {
     case 1: CG_LAUNCH_WCF(1); break;
-    case 2: CG_LAUNCH_WCF(2); break;
     case 3: CG_LAUNCH_WCF(3); break;
     default: CG_LAUNCH_WCF(0); break;
   }
