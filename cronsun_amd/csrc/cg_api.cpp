@@ -490,7 +490,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   unsigned long long stuck = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(c->times.cap);
-    if ((rc = c->block_run.ensure(cap / kChunk + 2))) return rc;
+    if ((rc = c->block_run.ensure(cap / kSuper + 2))) return rc;
     (void)hipEventRecord(c->ev[3], c->st);
     launch_chunk_map(c->run_off.p, nruns, cap, c->block_run.p, c->st);
     (void)hipEventRecord(c->ev[4], c->st);

@@ -22,10 +22,12 @@ struct PlanArgs {
 constexpr int kWriteThreads = 256;
 constexpr int kWritePerThread = 8;
 constexpr int kWriteChunk = kWriteThreads * kWritePerThread;
-// closed-form writer: 4 waves per block, 8 events per lane, 512 per wave-chunk
+// closed-form writer: 4 waves per block; a wave owns kSuper-event output
+// slices, and writes small-run regions in kChunk pieces (8 events per lane)
 constexpr int kWriteWaves = 4;
 constexpr int kLaneEvents = 8;
 constexpr int kChunk = 64 * kLaneEvents;
+constexpr int kSuper = 32 * kChunk;
 
 size_t plan_lds_bytes(const PlanArgs& p);
 

@@ -5,17 +5,15 @@
 //                Go walk, next_exact) and the closed-form count of the rest,
 //                or the walked count inside WALK windows -> run records
 //   k_scan_*     exclusive scan of run counts -> run offsets (int64)
-//   k_chunk_map  first run touched by each 1024-event output chunk
-//   k_write_cf   persistent, output-parallel: per wave-chunk each lane
-//                materialises 16 consecutive fire times from the closed form,
-//                staged in the wave's LDS slice, then stored as coalesced
-//                1 KiB wave-instructions
+//   k_chunk_map  first run touched by each 16384-event output slice
+//   k_write_cf   persistent, output-parallel: each wave walks its slices;
+//                long runs are written wave-cooperatively (64 consecutive
+//                fires per store instruction, mixed-radix digits + lane rank
+//                tables), stretches of short runs lane-parallel via LDS staging
 //   k_write_walk re-walks the (rare) WALK-window runs
 //   k_rule_offs  rule-major CSR offsets
 // Integer and HBM-bound throughout: no MFMA.
 #include <hip/hip_runtime.h>
-
-#include <cstdlib>
 
 #include "cg_expand.h"
 #include "cg_kernels.h"
@@ -23,8 +21,6 @@
 namespace cg {
 
 namespace {
-
-constexpr uint64_t kMask60 = 0x0FFFFFFFFFFFFFFFull;
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -202,21 +198,23 @@ __device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, i
   return lo;
 }
 
-// first run touched by each kChunk-event output chunk; E is read on the device
+// first run touched by each kSuper-event output slice; E is read on the device
 // so the launch needs no host sync (grid sized by capacity, extra threads exit)
 __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, int64_t cap,
                             int64_t* __restrict__ chunk_run) {
   const int64_t E = run_off[nruns];
-  if (E > cap) return;  // chunk_run holds cap / kChunk + 2 entries
-  const int64_t nchunks = (E + kChunk - 1) / kChunk;
-  for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c <= nchunks;
+  if (E > cap) return;  // chunk_run holds cap / kSuper + 2 entries
+  const int64_t nsup = (E + kSuper - 1) / kSuper;
+  for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c <= nsup;
        c += int64_t(gridDim.x) * blockDim.x)
-    chunk_run[c] = c == nchunks ? nruns - 1 : search_run(run_off, 0, nruns - 1, c * int64_t(kChunk));
+    chunk_run[c] = c == nsup ? nruns - 1 : search_run(run_off, 0, nruns - 1, c * int64_t(kSuper));
 }
 
 constexpr int kStageStride = kLaneEvents + 1;  // pad: conflict-free ds_write_b64 / ds_read_b64
+// run pieces at least this long are written wave-cooperatively
+constexpr int64_t kCoopMin = 64;
 
-// run data of a chunk's run window, staged once per chunk in the wave's LDS
+// one run of a wave's 64-run window (lane i holds run jw + i), staged in LDS
 struct WinRun {
   int64_t off;     // run_off[j]
   int64_t anchor;  // run_anchor[j]
@@ -227,19 +225,216 @@ struct WinRun {
   int32_t pad;
 };
 
-// Persistent closed-form writer.  Waves work independently: each takes
-// kChunk-event output chunks grid-stride.  Per chunk it loads the window of
-// (at most 64) runs the chunk touches with one round of coalesced loads into
-// its LDS slice, so a lane entering a run reads LDS instead of chasing
-// dependent global loads.  Lane l then materialises events [8l, 8l+8) of the
-// chunk (seek once, then the branch-free iterator), stages them in LDS, and
-// the wave stores the chunk as coalesced 1 KiB wave-instructions.  Chunks
-// touching more than 64 runs (long stretches of empty or single-fire rules)
-// take a slower per-lane path with direct global loads.
-//
-// ABLATE (diagnostic builds of the same kernel, selected by CG_ABLATE):
-//   0 normal; 1 generate but skip the global stores; 3 locate only.
-template <int ABLATE>
+__device__ __forceinline__ int32_t rl32(int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); }
+__device__ __forceinline__ int64_t rl64(int64_t v, int i) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), i));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v) >> 32)), i));
+  return int64_t((uint64_t(hi) << 32) | lo);
+}
+
+// Lane k of the result holds unit * (position of the k-th set bit of m), for
+// k < popcount(m): each lane pushes its own position to the lane of its rank
+// (set bits to 0..n-1, clear bits to n..63 -- a permutation), ds_permute_b32.
+// All 64 lanes must be active.
+__device__ __forceinline__ int32_t rank_table(uint64_t m, int32_t unit) {
+  const int lane = threadIdx.x & 63;
+  const bool set = (m >> lane) & 1ull;
+  const int32_t below = __popcll(m & ((1ull << lane) - 1ull));
+  const int32_t n = __popcll(m);
+  const int32_t dst = set ? below : n + (lane - below);
+  return __builtin_amdgcn_ds_permute(dst << 2, lane * unit);
+}
+// entry idx of a rank table (ds_bpermute_b32; idx is taken mod 64)
+__device__ __forceinline__ int32_t rank_at(int32_t table, uint32_t idx) {
+  return __builtin_amdgcn_ds_bpermute(int(idx << 2), table);
+}
+// floor(x / n) for x < 2^16, n >= 1, with inv = 1/n (the +0.5 keeps the
+// product at least 0.5/n away from an integer, far above the f32 error)
+__device__ __forceinline__ uint32_t small_div(uint32_t x, float inv) {
+  return uint32_t((float(x) + 0.5f) * inv);
+}
+
+// Fires [p0, p1) of closed-form run w, wave-cooperatively: lane l writes
+// p0 + l + 64u.  A fire's index g = rank(anchor) - 1 + (p - run start) counts
+// (day, hour, minute, second) combinations from the anchor's local day, so it
+// is carried as mixed-radix digits (matching-day rank, hour/minute/second
+// ranks; radices -, nH, nM, nS) and stepped by the constant 64; rank -> seconds
+// comes from per-run lane tables.  Same enumeration as cf_seek/cf_next.
+__device__ void coop_cf(const WinRun& w, const Segment& sg, int64_t p0, int64_t p1,
+                        int64_t* __restrict__ times) {
+  const int lane = threadIdx.x & 63;
+  const CFRule c = cf_rule(w.sp);
+  const uint32_t nS = c.nS, nM = c.nM, nH = c.C / c.nMS;
+  const uint32_t rf = uint32_t(w.anchor - sg.base);
+  const uint32_t jf = rf / 86400u, tf = rf - jf * 86400u;
+  const int32_t ts = rank_table(c.S, 1);
+  const int32_t tm = rank_table(c.M, 60);
+  const int32_t th = rank_table(c.H, 3600);
+  const int32_t td = rank_table(uint64_t(w.dmask >> jf), 86400) + int32_t(jf) * 86400;
+  uint32_t g = cf_rank(c, int32_t(tf)) - 1u + uint32_t(p0 - w.off);
+  uint32_t d = g / c.C;
+  g -= d * c.C;
+  uint32_t h = g / c.nMS;
+  g -= h * c.nMS;
+  uint32_t m = g / nS;
+  uint32_t s = g - m * nS;
+  // + lane
+  const float iS = 1.0f / float(nS), iM = 1.0f / float(nM), iH = 1.0f / float(nH);
+  uint32_t q;
+  s += uint32_t(lane);
+  q = small_div(s, iS);
+  s -= q * nS;
+  m += q;
+  q = small_div(m, iM);
+  m -= q * nM;
+  h += q;
+  q = small_div(h, iH);
+  h -= q * nH;
+  d += q;
+  // digits of 64
+  uint32_t a = 64;
+  const uint32_t a0 = a % nS;
+  a /= nS;
+  const uint32_t a1 = a % nM;
+  a /= nM;
+  const uint32_t a2 = a % nH;
+  const uint32_t a3 = a / nH;
+  const int64_t base = sg.base;
+  auto value = [&]() -> int64_t {
+    return base + int64_t(rank_at(td, d) + rank_at(th, h) + rank_at(tm, m) + rank_at(ts, s));
+  };
+  auto step = [&]() {
+    s += a0;
+    const uint32_t cs = s >= nS;
+    s -= cs ? nS : 0u;
+    m += a1 + cs;
+    const uint32_t cm = m >= nM;
+    m -= cm ? nM : 0u;
+    h += a2 + cm;
+    const uint32_t ch = h >= nH;
+    h -= ch ? nH : 0u;
+    d += a3 + ch;
+  };
+  int64_t* out = times + p0 + lane;
+  const int64_t n = p1 - p0;
+  int64_t b = 0;
+  for (; b + 8 * 64 <= n; b += 8 * 64) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      out[b + 64 * u] = value();
+      step();
+    }
+  }
+  for (; b < n; b += 64) {
+    const int64_t v = value();  // all lanes: the table reads are cross-lane
+    if (b + lane < n) out[b] = v;
+    step();
+  }
+}
+
+// Fires [p0, p1) of @every run w: anchor + (k + 1) * D (constantdelay.go:25-27)
+__device__ void coop_every(const WinRun& w, int64_t p0, int64_t p1, int64_t* __restrict__ times) {
+  const int lane = threadIdx.x & 63;
+  const int64_t D = int64_t(w.sp.sec);
+  int64_t t = w.anchor + (p0 - w.off + lane + 1) * D;
+  const int64_t st = 64 * D;
+  int64_t* out = times + p0 + lane;
+  const int64_t n = p1 - p0;
+  int64_t b = 0;
+  for (; b + 8 * 64 <= n; b += 8 * 64) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      out[b + 64 * u] = t;
+      t += st;
+    }
+  }
+  for (; b < n; b += 64) {
+    if (b + lane < n) out[b] = t;
+    t += st;
+  }
+}
+
+// Fires [pos, rend) spread over many short runs of the window (all inside it):
+// per kChunk piece lane l materialises events [8l, 8l+8) (seek once, then the
+// branch-free iterator), stages them in LDS, and the wave stores the piece
+// with coalesced 512 B wave-instructions.  Walked runs get placeholders that
+// k_write_walk overwrites.
+__device__ void lane_region(const WinRun* win, int64_t woff, const Segment* segs, int64_t pos,
+                            int64_t rend, int64_t* stage, int64_t* __restrict__ times) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t p = pos; p < rend; p += kChunk) {
+    const int64_t i = p + int64_t(lane) * kLaneEvents;
+    // window lane of the run holding event i: the last lane with off <= i
+    int j = 0;
+#pragma unroll
+    for (int st = 32; st > 0; st >>= 1) {
+      const int64_t v = __shfl(woff, (j + st) & 63, 64);
+      if (j + st < 64 && v <= i) j += st;
+    }
+    if (i < rend) {
+      const int32_t qmax = int32_t(rend - i < kLaneEvents ? rend - i : kLaneEvents);
+      int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
+      CFRule cr;
+      CFIter it;
+      const Segment* sg = &segs[0];
+      uint32_t dm = 0;
+      int64_t anchor = 0, D = 0;
+      int32_t k = int32_t(i - win[j].off), n = 0;
+      // enter window run j at its k-th fire
+      auto load_run = [&]() {
+        const WinRun& w = win[j];
+        n = w.count;
+        anchor = w.anchor;
+        dm = w.dmask;
+        sg = &segs[w.seg];
+        if (w.sp.kind == KIND_EVERY) {
+          kind = 1;
+          D = int64_t(w.sp.sec);
+        } else if (run_is_walked(*sg, dm)) {
+          kind = 2;
+        } else {
+          kind = 0;
+          cr = cf_rule(w.sp);
+          it = cf_seek(cr, *sg, dm, anchor, k);
+        }
+      };
+      load_run();
+#pragma unroll 1
+      for (int q = 0; q < qmax; q++) {
+        if (k >= n) {  // next non-empty run, entered at its first fire
+          do {
+            j++;
+            n = win[j].count;
+          } while (n == 0);
+          k = 0;
+          load_run();
+        }
+        const int64_t val =
+            kind == 0 ? cf_value(*sg, it) : (kind == 1 ? anchor + int64_t(k + 1) * D : 0);
+        stage[lane * kStageStride + q] = val;
+        if (kind == 0) cf_next(cr, dm, it);
+        k++;
+      }
+    }
+    __syncwarp();
+    const int64_t lim = rend - p < kChunk ? rend - p : kChunk;
+#pragma unroll
+    for (int u = 0; u < kLaneEvents; u++) {
+      const int t = u * 64 + lane;
+      if (t < lim) times[p + t] = stage[(t / kLaneEvents) * kStageStride + t % kLaneEvents];
+    }
+    __syncwarp();
+  }
+}
+
+// Persistent closed-form writer.  Waves work independently on kSuper-event
+// output slices (grid-stride).  A wave keeps a window of 64 consecutive runs
+// (one coalesced round of loads, staged in its LDS slice) and walks its slice:
+//   * a run piece of >= kCoopMin events is written by the whole wave, 64
+//     consecutive events per store instruction, from mixed-radix digits
+//     (coop_cf) or the @every progression (coop_every);
+//   * a stretch of shorter runs is written lane-parallel (lane_region).
+// Walked runs are left to k_write_walk, which runs after this kernel.
 __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
     const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
@@ -248,11 +443,8 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
   __shared__ int64_t stage_all[kWriteWaves][64 * kStageStride];
   __shared__ WinRun win_all[kWriteWaves][64];
   __shared__ Segment segs[64];
-  extern __shared__ __align__(16) char dyn[];
-  uint32_t* dtab = reinterpret_cast<uint32_t*>(dyn);
   for (int i = threadIdx.x; i < p.G * int(sizeof(Segment) / 8); i += blockDim.x)
     reinterpret_cast<int64_t*>(segs)[i] = reinterpret_cast<const int64_t*>(p.segs)[i];
-  for (int i = threadIdx.x; i < p.nd; i += blockDim.x) dtab[i] = p.dtab[i];
   __syncthreads();
 
   const int G = p.G;
@@ -261,122 +453,73 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
   WinRun* win = win_all[wave];
   const int64_t E = run_off[nruns];
   if (E > cap) return;  // output buffer too small: host grows it and relaunches
-  const int64_t nchunks = (E + kChunk - 1) / kChunk;
+  const int64_t nsup = (E + kSuper - 1) / kSuper;
   const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
-  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nchunks; c += nwaves) {
-    const int64_t base = c * kChunk;
-    const int64_t lo = chunk_run[c], hi = chunk_run[c + 1];
-    int64_t i = base + int64_t(lane) * kLaneEvents;
-    const bool fast = hi - lo < 64;
-    int64_t j;
-    if (fast) {
-      // window: one coalesced round of loads, then LDS
-      const int64_t jl = lo + lane <= hi ? lo + lane : hi;
-      WinRun w;
-      w.off = run_off[jl];
-      w.count = lo + lane <= hi ? run_count[jl] : 0;
-      w.anchor = run_anchor[jl];
-      w.dmask = run_dmask[jl];
+  int64_t woff = INT64_MAX;  // this lane's window run: offset, count
+  int32_t wcnt = 0;
+  auto load_window = [&](int64_t j0) {
+    __syncwarp();  // every lane is done with the previous window
+    const int64_t jl = j0 + lane;
+    WinRun w;
+    if (jl < nruns) {
       const int64_t r = G == 1 ? jl : jl / G;
+      w.off = run_off[jl];
+      w.anchor = run_anchor[jl];
+      w.count = run_count[jl];
+      w.dmask = run_dmask[jl];
       w.seg = int32_t(jl - r * G);
       w.sp = load_spec(specs + r);
-      w.pad = 0;
-      win[lane] = w;
-      // largest j in [lo, hi] with run_off[j] <= i, by shuffles over 64 lanes
-      const int64_t mine = lo + lane <= hi ? w.off : INT64_MAX;
-      int pos = 0;
-#pragma unroll
-      for (int step = 32; step > 0; step >>= 1) {
-        int64_t v = __shfl(mine, (pos + step) & 63, 64);
-        if (pos + step < 64 && v <= i) pos += step;
-      }
-      j = pos;  // window-relative
     } else {
-      j = search_run(run_off, lo, hi, i < E ? i : E - 1);
+      w.off = INT64_MAX;
+      w.anchor = 0;
+      w.count = 0;
+      w.dmask = 0;
+      w.seg = 0;
+      w.sp = DSpec{};
     }
+    w.pad = 0;
+    win[lane] = w;
+    woff = w.off;
+    wcnt = w.count;
     __syncwarp();
-    if (ABLATE == 3 && i < E) stage[lane * kStageStride] = j;
-    if (ABLATE != 3 && i < E) {
-      const int32_t qmax = int32_t(E - i < kLaneEvents ? E - i : kLaneEvents);
-      int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
-      CFRule cr;
-      CFIter it;
-      const Segment* sg = &segs[0];
-      uint32_t dm = 0;
-      int64_t anchor = 0, D = 0;
-      int32_t k, n;
-      // enter run j (window-relative when fast) at its k-th fire
-      auto enter = [&](const DSpec& sp) {
-        if (sp.kind == KIND_EVERY) {
-          kind = 1;
-          D = int64_t(sp.sec);
-        } else if (run_is_walked(*sg, dm)) {
-          kind = 2;
-        } else {
-          kind = 0;
-          cr = cf_rule(sp);
-          it = cf_seek(cr, *sg, dm, anchor, k);
-        }
-      };
-      auto load_run = [&]() {
-        if (fast) {
-          const WinRun& w = win[j];
-          n = w.count;
-          anchor = w.anchor;
-          dm = w.dmask;
-          sg = &segs[w.seg];
-          enter(w.sp);
-        } else {
-          const int64_t r = G == 1 ? j : j / G;
-          n = run_count[j];
-          anchor = run_anchor[j];
-          dm = run_dmask[j];
-          sg = &segs[int(j - r * G)];
-          enter(load_spec(specs + r));
-        }
-      };
-      k = int32_t(i - (fast ? win[j].off : run_off[j]));
-      load_run();
-#pragma unroll 1
-      for (int q = 0; q < qmax; q++) {
-        if (k >= n) {  // next non-empty run, entered at its first fire
-          do {
-            j++;
-            n = fast ? win[j].count : run_count[j];
-          } while (n == 0);
-          k = 0;
-          load_run();
-        }
-        int64_t val = kind == 0 ? cf_value(*sg, it) : (kind == 1 ? anchor + int64_t(k + 1) * D : 0);
-        stage[lane * kStageStride + q] = val;
-        if (kind == 0) cf_next(cr, dm, it);
-        k++;
+  };
+  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
+    int64_t pos = c * kSuper;
+    const int64_t S1 = E - pos < kSuper ? E : pos + kSuper;
+    int64_t jw = chunk_run[c];  // run_off[jw] <= pos
+    load_window(jw);
+    while (pos < S1) {
+      // the run holding pos: the last window lane with off <= pos (lane 0 qualifies)
+      const int i = 63 - __builtin_clzll(__ballot(woff <= pos));
+      if (i == 63 && jw + 64 < nruns) {  // may continue past the window: slide it
+        jw += 63;
+        load_window(jw);
+        continue;
       }
-    }
-    __syncwarp();
-    if (ABLATE == 1 || ABLATE == 3) {
-      // keep the generated values live without storing them
-      if (stage[lane * kStageStride] == INT64_MIN + 7) times[base] = 0;
-    } else {
-      const int64_t lim = E - base;
-#pragma unroll
-      for (int it2 = 0; it2 < kChunk / 128; it2++) {
-        const int e = it2 * 128 + lane * 2;
-        if (e < lim) {
-          const int t = e / kLaneEvents, q = e % kLaneEvents;
-          int64_t a = stage[t * kStageStride + q];
-          if (e + 1 < lim) {
-            longlong2 v;
-            v.x = a;
-            v.y = stage[t * kStageStride + q + 1];
-            *reinterpret_cast<longlong2*>(times + base + e) = v;
-          } else {
-            times[base + e] = a;
-          }
-        }
+      const int64_t roff = rl64(woff, i);
+      const int64_t rend_run = roff + rl32(wcnt, i);
+      const int64_t piece_end = rend_run < S1 ? rend_run : S1;
+      if (piece_end - pos >= kCoopMin) {
+        const WinRun& w = win[i];
+        const Segment& sg = segs[w.seg];
+        if (w.sp.kind == KIND_EVERY) coop_every(w, pos, piece_end, times);
+        else if (!run_is_walked(sg, w.dmask)) coop_cf(w, sg, pos, piece_end, times);
+        pos = piece_end;
+        continue;
       }
+      // a stretch of short runs: up to the next long run of the window
+      const uint64_t big = __ballot(lane > i && wcnt >= kCoopMin);
+      int64_t rend;
+      if (big) {
+        rend = rl64(woff, __builtin_ctzll(big));
+      } else {
+        const int L = 63 - __builtin_clzll(__ballot(woff != INT64_MAX));
+        rend = rl64(woff, L) + rl32(wcnt, L);
+      }
+      if (rend > S1) rend = S1;
+      lane_region(win, woff, segs, pos, rend, stage, times);
+      pos = rend;
     }
-    __syncwarp();
   }
 }
 
@@ -467,8 +610,8 @@ void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStre
 
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
                       hipStream_t st) {
-  int64_t max_chunks = cap / kChunk + 1;
-  hipLaunchKernelGGL(k_chunk_map, dim3(grid_for(max_chunks + 1, 256, 4096)), dim3(256), 0, st,
+  int64_t max_sup = cap / kSuper + 1;
+  hipLaunchKernelGGL(k_chunk_map, dim3(grid_for(max_sup + 1, 256, 4096)), dim3(256), 0, st,
                      run_off, nruns, cap, chunk_run);
 }
 
@@ -476,24 +619,8 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
                      int64_t nruns, const int64_t* chunk_run, int64_t cap, int64_t* times,
                      int n_blocks, hipStream_t st) {
-  static const int ablate = [] {
-    const char* e = getenv("CG_ABLATE");
-    return e ? atoi(e) : 0;
-  }();
-  size_t lds = align_up(size_t(p.nd) * 4, 16);
-  if (ablate == 4) {  // reference: plain fill of the same output bytes
-    (void)hipMemsetAsync(times, 0, size_t(cap) * 8, st);
-    return;
-  }
-#define CG_LAUNCH_WCF(A)                                                                     \
-  hipLaunchKernelGGL(k_write_cf<A>, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p, \
-                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times)
-  switch (ablate) {
-    case 1: CG_LAUNCH_WCF(1); break;
-    case 3: CG_LAUNCH_WCF(3); break;
-    default: CG_LAUNCH_WCF(0); break;
-  }
-#undef CG_LAUNCH_WCF
+  hipLaunchKernelGGL(k_write_cf, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, specs, p,
+                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
 }
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,

@@ -331,7 +331,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     unsigned end_bit = 1;
     while ((1u << end_bit) < unsigned(std::max(N, 2))) end_bit++;
     size_t tmp_bytes = 0;
-    rocprim::radix_sort_pairs(nullptr, tmp_bytes, reinterpret_cast<uint32_t*>(c->rn_nodes.p),
+    (void)rocprim::radix_sort_pairs(nullptr, tmp_bytes, reinterpret_cast<uint32_t*>(c->rn_nodes.p),
                               reinterpret_cast<uint32_t*>(c->pair_node.p), c->pair_rule.p,
                               c->nt_rule.p, size_t(nnz), 0, end_bit, st);
     if ((rc = c->pn_tmp.ensure(tmp_bytes + 16))) return rc;

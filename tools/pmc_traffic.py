@@ -61,10 +61,20 @@ def main():
     ap.add_argument("--kt")
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--sq", help="a pass of SQ_* counters: per-kernel averages per dispatch")
     ap.add_argument("--bench", help="bench.py JSON line of the profiled run")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     res = {"kernels": {}}
+    if a.sq:
+        names = sorted({r["Counter_Name"] for r in _rows(a.sq, "*counter_collection.csv")})
+        for n in names:
+            for k, v in counters(a.sq, n).items():
+                res["kernels"].setdefault(k, {})[n] = sum(v) / len(v)
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+        print(json.dumps(res["kernels"].get("k_write_cf", {})))
+        return
     if a.bench and os.path.exists(a.bench):
         line = [l for l in open(a.bench) if l.startswith("{")][-1]
         b = json.loads(line)
