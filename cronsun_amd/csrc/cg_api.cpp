@@ -395,6 +395,7 @@ int cg_next_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int64_t*
                   int64_t* t_out) {
   if (!c || !s || !z || (s->n && (!t_in || !t_out))) return cg_fail(CG_EINVAL, "cg_next_batch: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
   const int64_t n = int64_t(s->n);
   if (n == 0) return CG_OK;
@@ -531,6 +532,7 @@ int cg_expand_device(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0,
                      int64_t* n_events) {
   if (!c || !s || !z || !n_events) return cg_fail(CG_EINVAL, "cg_expand_device: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   return expand_device_locked(c, s, z, t0, t1, n_events);
 }
 
@@ -538,6 +540,7 @@ int cg_expand(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_
               cg_csr* out) {
   if (!c || !s || !z || !out) return cg_fail(CG_EINVAL, "cg_expand: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int64_t E = 0;
   int rc = expand_device_locked(c, s, z, t0, t1, &E);
   if (rc) return rc;
@@ -564,6 +567,7 @@ int cg_result_copy_times(cg_ctx* c, int64_t first, int64_t count, int64_t* host)
   if (first < 0 || count < 0 || first + count > c->last_E)
     return cg_fail(CG_EINVAL, "range outside the last result");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
   if (count) HIPCHK(hipMemcpy(host, c->times.p + first, count * 8, hipMemcpyDeviceToHost));
   return CG_OK;
@@ -572,6 +576,7 @@ int cg_result_copy_times(cg_ctx* c, int64_t first, int64_t count, int64_t* host)
 int cg_result_copy_offsets(cg_ctx* c, int64_t* host) {
   if (!c || !host) return cg_fail(CG_EINVAL, "cg_result_copy_offsets: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemcpy(host, c->offsets.p, (c->last_R + 1) * 8, hipMemcpyDeviceToHost));
   return CG_OK;

@@ -392,6 +392,7 @@ int cg_rule_nodes(cg_ctx* c, const cg_rules_in* in, int mode, int64_t* rn_off, i
                   int64_t cap, int64_t* nnz) {
   if (!c || !in || !nnz) return cg_fail(CG_EINVAL, "cg_rule_nodes: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
   if ((rc = rule_nodes_locked(c, in, mode, nnz))) return rc;
@@ -414,6 +415,7 @@ int cg_expand_per_node_device(cg_ctx* c, const cg_specs* s, const cg_zone* z, in
   if (!c || !s || !z || !rules || !n_events || !nnz)
     return cg_fail(CG_EINVAL, "cg_expand_per_node_device: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
   return per_node_locked(c, s, z, t0, t1, rules, mode, n_events, nnz);
@@ -423,6 +425,7 @@ int cg_expand_per_node(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
                        const cg_rules_in* rules, int mode, cg_node_csr* out) {
   if (!c || !s || !z || !rules || !out) return cg_fail(CG_EINVAL, "cg_expand_per_node: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
   int64_t En = 0, nnz = 0;
@@ -460,6 +463,7 @@ int cg_node_result_device(cg_ctx* c, const int64_t** d_node_off, const int64_t**
 int cg_node_counts_to_device(cg_ctx* c, int64_t* d_counts) {
   if (!c || !d_counts) return cg_fail(CG_EINVAL, "cg_node_counts_to_device: null");
   std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
   if (c->pn_N > 0)

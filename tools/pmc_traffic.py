@@ -17,6 +17,7 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
 
@@ -29,11 +30,8 @@ def _rows(d, pattern):
 
 
 def _short(name):
-    n = name.split("(")[0]
-    for tok in n.replace("::", " ").replace("<", " ").split():
-        if tok.startswith("k_"):
-            return tok
-    return n
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)", name)
+    return m.group(1) if m else name.split("(")[0]
 
 
 def counters(d, counter):
