@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -220,7 +221,9 @@ int cg_init(int device, cg_ctx** out) {
   HIPCHK(hipSetDevice(device));
   cg_ctx* c = new cg_ctx();
   c->device = device;
-  c->write_blocks = std::max(1, prop.multiProcessorCount) * 4;  // 4 blocks x 4 waves per CU
+  int per_cu = kWriteBlocksPerCU;
+  if (const char* e = getenv("CG_WRITE_BLOCKS_PER_CU")) per_cu = std::max(1, atoi(e));  // diagnostic
+  c->write_blocks = std::max(1, prop.multiProcessorCount) * per_cu;
   if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return cg_fail(CG_EHIP, "hipStreamCreate failed");
@@ -491,7 +494,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   unsigned long long stuck = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(c->times.cap);
-    if ((rc = c->block_run.ensure(cap / kSuper + 2))) return rc;
+    if ((rc = c->block_run.ensure(cap / kSuper + 2 + kTicketWords + 8))) return rc;
     (void)hipEventRecord(c->ev[3], c->st);
     launch_chunk_map(c->run_off.p, nruns, cap, c->block_run.p, c->st);
     (void)hipEventRecord(c->ev[4], c->st);

@@ -22,12 +22,14 @@ struct PlanArgs {
 constexpr int kWriteThreads = 256;
 constexpr int kWritePerThread = 8;
 constexpr int kWriteChunk = kWriteThreads * kWritePerThread;
-// closed-form writer: 4 waves per block; a wave owns kSuper-event output
-// slices, and writes small-run regions in kChunk pieces (8 events per lane)
+// closed-form writer: 4 waves per block; waves take kSuper-event output slices
 constexpr int kWriteWaves = 4;
-constexpr int kLaneEvents = 8;
-constexpr int kChunk = 64 * kLaneEvents;
-constexpr int kSuper = 32 * kChunk;
+constexpr int kWriteBlocksPerCU = 6;  // persistent grid: 6 x 4 waves per CU (LDS ~22 KB/block)
+constexpr int kSuper = 16384;
+// writer slice tickets: one u32 counter per group of blocks, 128 B apart
+constexpr int kTicketGroups = 8;
+constexpr int kTicketStride = 32;                                  // u32 words
+constexpr int kTicketWords = kTicketGroups * kTicketStride / 2;    // int64 words
 
 size_t plan_lds_bytes(const PlanArgs& p);
 
@@ -43,13 +45,14 @@ void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run
 size_t scan_temp_bytes(int64_t n);
 void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st);
 
-// chunk_run needs cap / kChunk + 2 entries; both read E = run_off[nruns] on
-// the device (no host sync) and do nothing when E > cap
+// chunk_run needs cap / kSuper + 2 + kTicketWords + 8 entries (slice map, the
+// writer's slice tickets, 8 diagnostic counters); both read E = run_off[nruns]
+// on the device (no host sync) and do nothing when E > cap
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
                       hipStream_t st);
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
-                     int64_t nruns, const int64_t* chunk_run, int64_t cap, int64_t* times,
+                     int64_t nruns, int64_t* chunk_run, int64_t cap, int64_t* times,
                      int n_blocks, hipStream_t st);
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,

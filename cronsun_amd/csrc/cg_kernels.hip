@@ -15,6 +15,9 @@
 // Integer and HBM-bound throughout: no MFMA.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+
 #include "cg_expand.h"
 #include "cg_kernels.h"
 
@@ -200,30 +203,32 @@ __device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, i
 
 // first run touched by each kSuper-event output slice; E is read on the device
 // so the launch needs no host sync (grid sized by capacity, extra threads exit)
+// (chunk_run holds cap / kSuper + 2 + kTicketWords entries: the map, then the
+// writer's slice ticket counters, reset here)
 __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, int64_t cap,
                             int64_t* __restrict__ chunk_run) {
+  if (blockIdx.x == 0 && threadIdx.x < kTicketWords + 8)
+    chunk_run[cap / kSuper + 2 + threadIdx.x] = 0;
   const int64_t E = run_off[nruns];
-  if (E > cap) return;  // chunk_run holds cap / kSuper + 2 entries
+  if (E > cap) return;
   const int64_t nsup = (E + kSuper - 1) / kSuper;
   for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c <= nsup;
        c += int64_t(gridDim.x) * blockDim.x)
     chunk_run[c] = c == nsup ? nruns - 1 : search_run(run_off, 0, nruns - 1, c * int64_t(kSuper));
 }
 
-constexpr int kStageStride = kLaneEvents + 1;  // pad: conflict-free ds_write_b64 / ds_read_b64
-// run pieces at least this long are written wave-cooperatively
-constexpr int64_t kCoopMin = 64;
 
 // one run of a wave's 64-run window (lane i holds run jw + i), staged in LDS
+// (48 B; the run offset stays in a VGPR of lane i, the plan segment index
+// rides in the spec's kind word: kind | seg << 8)
 struct WinRun {
-  int64_t off;     // run_off[j]
   int64_t anchor;  // run_anchor[j]
   DSpec sp;        // specs[j / G]
   int32_t count;   // run_count[j]
   uint32_t dmask;  // run_dmask[j]
-  int32_t seg;     // j % G
-  int32_t pad;
 };
+__device__ __forceinline__ bool win_every(const WinRun& w) { return (w.sp.kind & 0xFFu) == KIND_EVERY; }
+__device__ __forceinline__ int win_seg(const WinRun& w) { return int(w.sp.kind >> 8); }
 
 __device__ __forceinline__ int32_t rl32(int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); }
 __device__ __forceinline__ int64_t rl64(int64_t v, int i) {
@@ -253,33 +258,101 @@ __device__ __forceinline__ int32_t rank_at(int32_t table, uint32_t idx) {
 __device__ __forceinline__ uint32_t small_div(uint32_t x, float inv) {
   return uint32_t((float(x) + 0.5f) * inv);
 }
+// floor(x / n) for x < 2^24, n >= 1, inv = 1/n: the f32 quotient is off by at
+// most one, fixed by one remainder test each way (cheaper than a u32 divide)
+__device__ __forceinline__ uint32_t fdiv(uint32_t x, uint32_t n, float inv) {
+  uint32_t q = uint32_t(float(x) * inv);
+  const int32_t r = int32_t(x) - int32_t(q * n);
+  q = r < 0 ? q - 1u : (r >= int32_t(n) ? q + 1u : q);
+  return q;
+}
+
+// Output store.  V (diagnostic variants, CG_WRITE_VARIANT; 0 in production):
+// bit 0 = compute only (no store, value kept live), bit 1 = non-temporal store,
+// bit 2 = skip the short runs, bit 3 = skip the long runs, bit 4 = static slice
+// split instead of tickets, bit 5 = per-phase clock stats, bit 6 = plain fill.
+template <int V>
+__device__ __forceinline__ void put(int64_t* p, int64_t v) {
+  if (V & 1) {
+    asm volatile("" ::"v"(v));
+  } else if (V & 2) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
+// cf_seek (cg_expand.h) with the three variable divisions done by fdiv
+// (quotients < 2^24); same result, fewer instructions.
+__device__ __forceinline__ CFIter cf_seek_fast(const CFRule& c, const Segment& sg, uint32_t dmask,
+                                               int64_t uf, int64_t k) {
+  if (k == 0) return cf_decode(sg, uf);
+  const uint32_t rf = uint32_t(uf - sg.base);
+  const uint32_t jf = rf / 86400u, tf = rf - jf * 86400u;
+  uint32_t idx = cf_rank(c, int32_t(tf)) - 1u + uint32_t(k);
+  CFIter it;
+  it.day = int32_t(jf);
+  if (idx >= c.C) {
+    idx -= c.C;
+    const uint32_t dskip = fdiv(idx, c.C, 1.0f / float(c.C));
+    idx -= dskip * c.C;
+    const uint64_t above = uint64_t(dmask) & ~((2ull << jf) - 1ull);
+    it.day = select64(above, dskip);
+  }
+  const uint32_t hi = fdiv(idx, c.nMS, 1.0f / float(c.nMS));
+  const uint32_t rem = idx - hi * c.nMS;
+  const uint32_t mi = fdiv(rem, c.nS, 1.0f / float(c.nS));
+  const uint32_t si = rem - mi * c.nS;
+  it.h = select64(c.H, hi);
+  it.m = select64(c.M, mi);
+  it.s = select64(c.S, si);
+  return it;
+}
+
+// Does mask m (n set bits) hold an arithmetic progression p0 + r*step?
+// (rank r -> position is then linear; n <= 1 counts, with step 0)
+__device__ __forceinline__ bool ap_level(uint64_t m, uint32_t n, int32_t* p0, int32_t* step) {
+  *p0 = m ? __builtin_ctzll(m) : 0;
+  *step = 0;
+  if (n <= 1) return true;
+  const uint64_t rest = m >> *p0;  // bit 0 set
+  const int32_t st = __builtin_ctzll(rest >> 1) + 1;
+  *step = st;
+  // {0, st, 2st, ...} up to the top bit  <=>  ((rest << st) | 1) below the top == rest
+  const int32_t top = 63 - __builtin_clzll(rest);
+  const uint64_t low = top >= 63 ? ~0ull : ((2ull << top) - 1ull);
+  return (((rest << st) | 1ull) & low) == rest;
+}
 
 // Fires [p0, p1) of closed-form run w, wave-cooperatively: lane l writes
 // p0 + l + 64u.  A fire's index g = rank(anchor) - 1 + (p - run start) counts
 // (day, hour, minute, second) combinations from the anchor's local day, so it
 // is carried as mixed-radix digits (matching-day rank, hour/minute/second
-// ranks; radices -, nH, nM, nS) and stepped by the constant 64; rank -> seconds
-// comes from per-run lane tables.  Same enumeration as cf_seek/cf_next.
-__device__ void coop_cf(const WinRun& w, const Segment& sg, int64_t p0, int64_t p1,
+// ranks; radices -, nH, nM, nS) and stepped by the constant 64.  Same
+// enumeration as cf_seek/cf_next.  Rank -> seconds, cheapest form first:
+//   linear   every level an arithmetic progression and the sequence has one
+//            stride (e.g. */10 s with every minute/hour/day): t += 64*stride;
+//   affine   every level an arithmetic progression: t = C0 + sum r_i * w_i;
+//   tables   otherwise: per-level lane tables read with ds_bpermute.
+template <int V>
+__device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_t p0, int64_t p1,
                         int64_t* __restrict__ times) {
   const int lane = threadIdx.x & 63;
   const CFRule c = cf_rule(w.sp);
-  const uint32_t nS = c.nS, nM = c.nM, nH = c.C / c.nMS;
+  const uint32_t nS = c.nS, nM = c.nM, nH = uint32_t(__builtin_popcount(c.H));
   const uint32_t rf = uint32_t(w.anchor - sg.base);
   const uint32_t jf = rf / 86400u, tf = rf - jf * 86400u;
-  const int32_t ts = rank_table(c.S, 1);
-  const int32_t tm = rank_table(c.M, 60);
-  const int32_t th = rank_table(c.H, 3600);
-  const int32_t td = rank_table(uint64_t(w.dmask >> jf), 86400) + int32_t(jf) * 86400;
-  uint32_t g = cf_rank(c, int32_t(tf)) - 1u + uint32_t(p0 - w.off);
-  uint32_t d = g / c.C;
+  const uint32_t dmask = w.dmask >> jf;  // matching days from the anchor's (bit 0)
+  const float iS = 1.0f / float(nS), iM = 1.0f / float(nM), iH = 1.0f / float(nH);
+  // g < 31 * 86400 < 2^24
+  uint32_t g = cf_rank(c, int32_t(tf)) - 1u + uint32_t(p0 - roff);
+  uint32_t d = fdiv(g, c.C, 1.0f / float(c.C));
   g -= d * c.C;
-  uint32_t h = g / c.nMS;
+  uint32_t h = fdiv(g, c.nMS, 1.0f / float(c.nMS));
   g -= h * c.nMS;
-  uint32_t m = g / nS;
+  uint32_t m = fdiv(g, nS, iS);
   uint32_t s = g - m * nS;
   // + lane
-  const float iS = 1.0f / float(nS), iM = 1.0f / float(nM), iH = 1.0f / float(nH);
   uint32_t q;
   s += uint32_t(lane);
   q = small_div(s, iS);
@@ -292,17 +365,13 @@ __device__ void coop_cf(const WinRun& w, const Segment& sg, int64_t p0, int64_t 
   h -= q * nH;
   d += q;
   // digits of 64
-  uint32_t a = 64;
-  const uint32_t a0 = a % nS;
-  a /= nS;
-  const uint32_t a1 = a % nM;
-  a /= nM;
-  const uint32_t a2 = a % nH;
-  const uint32_t a3 = a / nH;
-  const int64_t base = sg.base;
-  auto value = [&]() -> int64_t {
-    return base + int64_t(rank_at(td, d) + rank_at(th, h) + rank_at(tm, m) + rank_at(ts, s));
-  };
+  uint32_t a = small_div(64, iS);
+  const uint32_t a0 = 64 - a * nS;
+  uint32_t a_ = small_div(a, iM);
+  const uint32_t a1 = a - a_ * nM;
+  a = small_div(a_, iH);
+  const uint32_t a2 = a_ - a * nH;
+  const uint32_t a3 = a;
   auto step = [&]() {
     s += a0;
     const uint32_t cs = s >= nS;
@@ -317,26 +386,112 @@ __device__ void coop_cf(const WinRun& w, const Segment& sg, int64_t p0, int64_t 
   };
   int64_t* out = times + p0 + lane;
   const int64_t n = p1 - p0;
-  int64_t b = 0;
-  for (; b + 8 * 64 <= n; b += 8 * 64) {
+  int32_t s0, ss, m0, ms, h0, hs, d0, ds;
+  const uint32_t nD = uint32_t(__builtin_popcount(dmask));
+  const bool apS = ap_level(c.S, nS, &s0, &ss), apM = ap_level(c.M, nM, &m0, &ms);
+  const bool apH = ap_level(c.H, nH, &h0, &hs), apD = ap_level(dmask, nD, &d0, &ds);
+  const bool affine = apS && apM && apH && apD;
+  if (V & 128) {  // diagnostic: the full per-piece setup, then a plain fill of the piece
+    asm volatile("" ::"v"(s), "v"(m), "v"(h), "v"(d), "v"(a0), "v"(a1), "v"(a2), "v"(a3));
+    asm volatile("" ::"v"(int(affine)), "v"(ss + ms + hs + ds + s0 + m0 + h0 + d0));
+    for (int64_t b = 0; b < n; b += 64)
+      if (b + lane < n) put<V>(out + b, b);
+    return;
+  }
+  if (affine) {
+    const int64_t C0 = sg.base + s0 + 60 * m0 + 3600 * h0 + 86400 * int32_t(jf);  // d0 == 0
+    const uint32_t ws = uint32_t(ss), wm = 60u * uint32_t(ms), wh = 3600u * uint32_t(hs),
+                   wd = 86400u * uint32_t(ds);
+    auto value = [&]() -> int64_t {
+      // every product < 2^24 x 2^24 operands: v_mul_u32_u24 (full rate)
+      return C0 + int64_t(__umul24(s, ws) + __umul24(m, wm) + __umul24(h, wh) + __umul24(d, wd));
+    };
+    // one stride: the lowest level with > 1 value wraps evenly into the next
+    // unit, and every level above it takes every value (days: consecutive)
+    const bool days_full = nD <= 1 || ds == 1;
+    int32_t stride = 0;
+    if (nS > 1) {
+      if (uint32_t(ss) * nS == 60 && s0 < ss && nM == 60 && nH == 24 && days_full) stride = ss;
+    } else if (nM > 1) {
+      if (uint32_t(ms) * nM == 60 && m0 < ms && nH == 24 && days_full) stride = 60 * ms;
+    } else if (nH > 1) {
+      if (uint32_t(hs) * nH == 24 && h0 < hs && days_full) stride = 3600 * hs;
+    } else {
+      stride = 86400 * ds;
+    }
+    if (stride > 0 || n <= 64) {
+      int64_t v = value();
+      const int64_t st = 64 * int64_t(stride);
+      int64_t b = 0;
+      for (; b + 8 * 64 <= n; b += 8 * 64) {
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      out[b + 64 * u] = value();
+        for (int u = 0; u < 8; u++) {
+          put<V>(out + b + 64 * u, v);
+          v += st;
+        }
+      }
+      for (; b < n; b += 64) {
+        if (b + lane < n) put<V>(out + b, v);
+        v += st;
+      }
+      return;
+    }
+    int64_t b = 0;
+    for (; b + 8 * 64 <= n; b += 8 * 64) {
+      // all 8 values first, then the 8 stores: a wave whose store is held
+      // back by a full memory pipe has no arithmetic queued behind it
+      int64_t vv[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        vv[u] = value();
+        step();
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) asm volatile("" : "+v"(vv[u]));
+#pragma unroll
+      for (int u = 0; u < 8; u++) put<V>(out + b + 64 * u, vv[u]);
+    }
+    for (; b < n; b += 64) {
+      if (b + lane < n) put<V>(out + b, value());
       step();
     }
+    return;
+  }
+  const int32_t ts = rank_table(c.S, 1);
+  const int32_t tm = rank_table(c.M, 60);
+  const int32_t th = rank_table(c.H, 3600);
+  const int32_t td = rank_table(uint64_t(dmask), 86400) + int32_t(jf) * 86400;
+  const int64_t base = sg.base;
+  auto value = [&]() -> int64_t {
+    return base + int64_t(rank_at(td, d) + rank_at(th, h) + rank_at(tm, m) + rank_at(ts, s));
+  };
+  int64_t b = 0;
+  for (; b + 8 * 64 <= n; b += 8 * 64) {
+    int64_t vv[8];  // values first, then the stores (as in the affine loop)
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      vv[u] = value();
+      step();
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) asm volatile("" : "+v"(vv[u]));
+#pragma unroll
+    for (int u = 0; u < 8; u++) put<V>(out + b + 64 * u, vv[u]);
   }
   for (; b < n; b += 64) {
     const int64_t v = value();  // all lanes: the table reads are cross-lane
-    if (b + lane < n) out[b] = v;
+    if (b + lane < n) put<V>(out + b, v);
     step();
   }
 }
 
 // Fires [p0, p1) of @every run w: anchor + (k + 1) * D (constantdelay.go:25-27)
-__device__ void coop_every(const WinRun& w, int64_t p0, int64_t p1, int64_t* __restrict__ times) {
+template <int V>
+__device__ void coop_every(const WinRun& w, int64_t roff, int64_t p0, int64_t p1,
+                           int64_t* __restrict__ times) {
   const int lane = threadIdx.x & 63;
   const int64_t D = int64_t(w.sp.sec);
-  int64_t t = w.anchor + (p0 - w.off + lane + 1) * D;
+  int64_t t = w.anchor + (p0 - roff + lane + 1) * D;
   const int64_t st = 64 * D;
   int64_t* out = times + p0 + lane;
   const int64_t n = p1 - p0;
@@ -344,12 +499,12 @@ __device__ void coop_every(const WinRun& w, int64_t p0, int64_t p1, int64_t* __r
   for (; b + 8 * 64 <= n; b += 8 * 64) {
 #pragma unroll
     for (int u = 0; u < 8; u++) {
-      out[b + 64 * u] = t;
+      put<V>(out + b + 64 * u, t);
       t += st;
     }
   }
   for (; b < n; b += 64) {
-    if (b + lane < n) out[b] = t;
+    if (b + lane < n) put<V>(out + b, t);
     t += st;
   }
 }
@@ -359,166 +514,236 @@ __device__ void coop_every(const WinRun& w, int64_t p0, int64_t p1, int64_t* __r
 // branch-free iterator), stages them in LDS, and the wave stores the piece
 // with coalesced 512 B wave-instructions.  Walked runs get placeholders that
 // k_write_walk overwrites.
-__device__ void lane_region(const WinRun* win, int64_t woff, const Segment* segs, int64_t pos,
-                            int64_t rend, int64_t* stage, int64_t* __restrict__ times) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t p = pos; p < rend; p += kChunk) {
-    const int64_t i = p + int64_t(lane) * kLaneEvents;
-    // window lane of the run holding event i: the last lane with off <= i
-    int j = 0;
-#pragma unroll
-    for (int st = 32; st > 0; st >>= 1) {
-      const int64_t v = __shfl(woff, (j + st) & 63, 64);
-      if (j + st < 64 && v <= i) j += st;
-    }
-    if (i < rend) {
-      const int32_t qmax = int32_t(rend - i < kLaneEvents ? rend - i : kLaneEvents);
-      int kind = 0;  // 0 closed form, 1 @every, 2 walked (k_write_walk)
-      CFRule cr;
-      CFIter it;
-      const Segment* sg = &segs[0];
-      uint32_t dm = 0;
-      int64_t anchor = 0, D = 0;
-      int32_t k = int32_t(i - win[j].off), n = 0;
-      // enter window run j at its k-th fire
-      auto load_run = [&]() {
-        const WinRun& w = win[j];
-        n = w.count;
-        anchor = w.anchor;
-        dm = w.dmask;
-        sg = &segs[w.seg];
-        if (w.sp.kind == KIND_EVERY) {
-          kind = 1;
-          D = int64_t(w.sp.sec);
-        } else if (run_is_walked(*sg, dm)) {
-          kind = 2;
-        } else {
-          kind = 0;
-          cr = cf_rule(w.sp);
-          it = cf_seek(cr, *sg, dm, anchor, k);
-        }
-      };
-      load_run();
-#pragma unroll 1
-      for (int q = 0; q < qmax; q++) {
-        if (k >= n) {  // next non-empty run, entered at its first fire
-          do {
-            j++;
-            n = win[j].count;
-          } while (n == 0);
-          k = 0;
-          load_run();
-        }
-        const int64_t val =
-            kind == 0 ? cf_value(*sg, it) : (kind == 1 ? anchor + int64_t(k + 1) * D : 0);
-        stage[lane * kStageStride + q] = val;
-        if (kind == 0) cf_next(cr, dm, it);
-        k++;
-      }
-    }
-    __syncwarp();
-    const int64_t lim = rend - p < kChunk ? rend - p : kChunk;
-#pragma unroll
-    for (int u = 0; u < kLaneEvents; u++) {
-      const int t = u * 64 + lane;
-      if (t < lim) times[p + t] = stage[(t / kLaneEvents) * kStageStride + t % kLaneEvents];
-    }
-    __syncwarp();
-  }
-}
-
 // Persistent closed-form writer.  Waves work independently on kSuper-event
-// output slices (grid-stride).  A wave keeps a window of 64 consecutive runs
-// (one coalesced round of loads, staged in its LDS slice) and walks its slice:
-//   * a run piece of >= kCoopMin events is written by the whole wave, 64
-//     consecutive events per store instruction, from mixed-radix digits
-//     (coop_cf) or the @every progression (coop_every);
-//   * a stretch of shorter runs is written lane-parallel (lane_region).
+// output slices, handed out by ticket.  A wave keeps a window of 64
+// consecutive runs (one coalesced round of loads, staged in its LDS slice;
+// only the runs the slice can touch are loaded) and walks its slice in whole,
+// aligned 64-fire blocks, so every store instruction writes one full 512 B
+// block (no partially written cache lines reach HBM):
+//   * blocks inside one run are written wave-cooperatively, 64 consecutive
+//     fires per store, from mixed-radix digits (coop_cf) or the @every
+//     progression (coop_every);
+//   * a block shared by several runs (run boundaries, short runs) is written
+//     lane-parallel: each lane seeks its own fire (cf_seek).
 // Walked runs are left to k_write_walk, which runs after this kernel.
-__global__ __launch_bounds__(kWriteWaves * 64) void k_write_cf(
+template <int V>
+__global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
     const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
-    const int64_t* __restrict__ run_off, int64_t nruns, const int64_t* __restrict__ chunk_run,
+    const int64_t* __restrict__ run_off, int64_t nruns, int64_t* __restrict__ chunk_run,
     int64_t cap, int64_t* __restrict__ times) {
-  __shared__ int64_t stage_all[kWriteWaves][64 * kStageStride];
   __shared__ WinRun win_all[kWriteWaves][64];
-  __shared__ Segment segs[64];
+  extern __shared__ __align__(16) char dyn[];  // the plan's G segments
+  Segment* segs = reinterpret_cast<Segment*>(dyn);
   for (int i = threadIdx.x; i < p.G * int(sizeof(Segment) / 8); i += blockDim.x)
     reinterpret_cast<int64_t*>(segs)[i] = reinterpret_cast<const int64_t*>(p.segs)[i];
   __syncthreads();
 
   const int G = p.G;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int64_t* stage = stage_all[wave];
   WinRun* win = win_all[wave];
   const int64_t E = run_off[nruns];
   if (E > cap) return;  // output buffer too small: host grows it and relaunches
   const int64_t nsup = (E + kSuper - 1) / kSuper;
-  const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
   int64_t woff = INT64_MAX;  // this lane's window run: offset, count
   int32_t wcnt = 0;
+  int64_t jend = nruns;  // runs the current slice can touch: [.., jend)
   auto load_window = [&](int64_t j0) {
     __syncwarp();  // every lane is done with the previous window
     const int64_t jl = j0 + lane;
     WinRun w;
-    if (jl < nruns) {
+    int64_t off = INT64_MAX;
+    if (jl < jend) {  // only the runs this slice needs: no over-fetch into the write stream
       const int64_t r = G == 1 ? jl : jl / G;
-      w.off = run_off[jl];
+      off = run_off[jl];
       w.anchor = run_anchor[jl];
       w.count = run_count[jl];
       w.dmask = run_dmask[jl];
-      w.seg = int32_t(jl - r * G);
       w.sp = load_spec(specs + r);
+      w.sp.kind |= uint32_t(jl - r * G) << 8;
     } else {
-      w.off = INT64_MAX;
       w.anchor = 0;
       w.count = 0;
       w.dmask = 0;
-      w.seg = 0;
       w.sp = DSpec{};
     }
-    w.pad = 0;
     win[lane] = w;
-    woff = w.off;
+    woff = off;
     wcnt = w.count;
     __syncwarp();
   };
-  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
-    int64_t pos = c * kSuper;
+  // Slices are handed out dynamically (the cost per slice varies with the
+  // spec mix; a static split leaves a long tail).  One ticket counter per
+  // XCD-sized group of blocks (blocks go round-robin over the 8 XCDs): group x
+  // owns slices x, x + ng, x + 2 ng, ..., so the counters' atomics spread over
+  // 8 addresses.  Tickets are taken one slice ahead so the atomic's latency
+  // hides under the current slice.
+  const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
+  const int grp = int(blockIdx.x % unsigned(ng));
+  unsigned int* ticket =
+      reinterpret_cast<unsigned int*>(chunk_run + cap / kSuper + 2) + grp * kTicketStride;
+  int64_t static_next = int64_t(blockIdx.x) * kWriteWaves + wave;
+  auto take = [&]() -> int64_t {
+    if (V & 16) {  // diagnostic: static grid-stride split
+      const int64_t t = static_next;
+      static_next += int64_t(gridDim.x) * kWriteWaves;
+      return t;
+    }
+    unsigned int t = 0;
+    if (lane == 0) t = atomicAdd(ticket, 1u);
+    return grp + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
+  };
+  // V & 32 (diagnostic): per-phase shader-clock totals and counts
+  uint64_t st_win = 0, st_long = 0, st_all = 0, n_win = 0, n_long = 0;  // (coop only)
+  auto clk = [&]() -> uint64_t { return (V & 32) ? __builtin_amdgcn_s_memtime() : 0; };
+  const uint64_t k_start = clk();
+  for (int64_t c = take(); c < nsup;) {
+    const int64_t c_next = take();
+    int64_t pos = c * kSuper;  // multiple of 64: every store below is a whole 512 B block
     const int64_t S1 = E - pos < kSuper ? E : pos + kSuper;
+    uint64_t t_a = clk();
+    if (V & 64) {  // diagnostic: plain fill of the slice (with bit 3: + the skeleton's reads)
+      for (int64_t b = pos + lane; b < S1; b += 64) put<V>(times + b, b);
+    }
     int64_t jw = chunk_run[c];  // run_off[jw] <= pos
+    jend = chunk_run[c + 1] + 1;  // the run holding S1 (or the last run)
     load_window(jw);
+    if (V & 32) {
+      st_win += clk() - t_a;
+      n_win++;
+    }
     while (pos < S1) {
       // the run holding pos: the last window lane with off <= pos (lane 0 qualifies)
       const int i = 63 - __builtin_clzll(__ballot(woff <= pos));
-      if (i == 63 && jw + 64 < nruns) {  // may continue past the window: slide it
+      if (i == 63 && jw + 64 < jend) {  // may continue past the window: slide it
         jw += 63;
         load_window(jw);
         continue;
       }
       const int64_t roff = rl64(woff, i);
-      const int64_t rend_run = roff + rl32(wcnt, i);
-      const int64_t piece_end = rend_run < S1 ? rend_run : S1;
-      if (piece_end - pos >= kCoopMin) {
+      const int64_t rend = roff + rl32(wcnt, i);
+      // whole 64-fire blocks of run i from pos on
+      int64_t blk_end = (rend < S1 ? rend : S1) & ~int64_t(63);
+      if (blk_end > pos) {
         const WinRun& w = win[i];
-        const Segment& sg = segs[w.seg];
-        if (w.sp.kind == KIND_EVERY) coop_every(w, pos, piece_end, times);
-        else if (!run_is_walked(sg, w.dmask)) coop_cf(w, sg, pos, piece_end, times);
-        pos = piece_end;
+        const Segment& sg = segs[win_seg(w)];
+        t_a = clk();
+        if (V & 8) {
+        } else if (win_every(w)) {
+          coop_every<V>(w, roff, pos, blk_end, times);
+        } else if (!run_is_walked(sg, w.dmask)) {
+          coop_cf<V>(w, roff, sg, pos, blk_end, times);
+        }  // a walked run's fires come from k_write_walk
+        if (V & 32) {
+          st_long += clk() - t_a;
+          n_long++;
+        }
+        pos = blk_end;
         continue;
       }
-      // a stretch of short runs: up to the next long run of the window
-      const uint64_t big = __ballot(lane > i && wcnt >= kCoopMin);
-      int64_t rend;
-      if (big) {
-        rend = rl64(woff, __builtin_ctzll(big));
-      } else {
+      // A block shared by several runs (run ends, short runs): lane l computes
+      // fire pos + l of whichever run holds it (the per-lane seek), then the
+      // block is stored whole.  Its runs may extend past the window: slide
+      // and finish the remaining lanes.
+      const int64_t e = pos + lane;
+      bool done = e >= S1 || (V & 4);
+      int64_t val = 0;
+      for (;;) {
         const int L = 63 - __builtin_clzll(__ballot(woff != INT64_MAX));
-        rend = rl64(woff, L) + rl32(wcnt, L);
+        const int64_t wend = rl64(woff, L) + rl32(wcnt, L);
+        // window lane of the run holding e: the last lane with off <= e
+        int j = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+          const int64_t v = __shfl(woff, (j + st) & 63, 64);
+          if (j + st < 64 && v <= e) j += st;
+        }
+        const int64_t joff = __shfl(woff, j, 64);  // all lanes active here
+        if (!done && e < wend) {
+          const WinRun& w = win[j];
+          const int32_t k = int32_t(e - joff);
+          const Segment& sg = segs[win_seg(w)];
+          if (win_every(w)) {
+            val = w.anchor + int64_t(k + 1) * int64_t(w.sp.sec);
+          } else if (!run_is_walked(sg, w.dmask)) {
+            const CFRule cr = cf_rule(w.sp);
+            val = cf_value(sg, cf_seek_fast(cr, sg, w.dmask, w.anchor, k));
+          }  // walked: a placeholder k_write_walk overwrites
+          done = true;
+        }
+        if (__ballot(!done) == 0) break;
+        jw += 63;  // the window's last run ends before some lane's fire
+        load_window(jw);
       }
-      if (rend > S1) rend = S1;
-      lane_region(win, woff, segs, pos, rend, stage, times);
-      pos = rend;
+      if (e < S1 && !(V & 4)) put<V>(times + e, val);
+      pos += 64;
+    }
+    c = c_next;
+  }
+  if (V & 32) {
+    st_all = clk() - k_start;
+    unsigned long long* dbg =
+        reinterpret_cast<unsigned long long*>(chunk_run + cap / kSuper + 2 + kTicketWords);
+    if (lane == 0) {
+      atomicAdd(dbg + 0, st_all);
+      atomicAdd(dbg + 1, st_win);
+      atomicAdd(dbg + 2, st_long);
+      atomicAdd(dbg + 3, 0ull);
+      atomicAdd(dbg + 4, n_win);
+      atomicAdd(dbg + 5, n_long);
+      atomicAdd(dbg + 6, 0ull);
+      atomicAdd(dbg + 7, 1ull);
+    }
+  }
+}
+
+// diagnostic store ceiling (CG_WRITE_PROBE): fill the kSuper slices of the
+// output with W*8-byte-per-lane stores, 64 lanes contiguous
+template <int W>
+__global__ __launch_bounds__(kWriteWaves * 64) void k_fill_probe(const int64_t* __restrict__ run_off,
+                                                                 int64_t nruns, int64_t cap,
+                                                                 int64_t* __restrict__ times) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t E = run_off[nruns];
+  if (E > cap) return;
+  if (W == 6 || W == 7) {  // per-wave streams with a pause (s_sleep) after every 24 stores
+    const int64_t nsup = (E + kSuper - 1) / kSuper;
+    const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
+    for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
+      const int64_t p0 = c * kSuper, p1 = E - p0 < kSuper ? E : p0 + kSuper;
+      int k = 0;
+      for (int64_t b = p0 + lane; b < p1; b += 64) {
+        times[b] = b;
+        if (++k == 24) {
+          k = 0;
+          if (W == 6) __builtin_amdgcn_s_sleep(16);
+          else __builtin_amdgcn_s_sleep(64);
+        }
+      }
+    }
+    return;
+  }
+  if (W == 4) {  // block-wide streams: the 4 waves interleave 512 B pieces of one slice
+    const int64_t nsup = (E + kSuper - 1) / kSuper;
+    for (int64_t c = blockIdx.x; c < nsup; c += gridDim.x) {
+      const int64_t p0 = c * kSuper, p1 = E - p0 < kSuper ? E : p0 + kSuper;
+      for (int64_t b = p0 + wave * 64 + lane; b < p1; b += 64 * kWriteWaves) times[b] = b;
+    }
+    return;
+  }
+  const int64_t nsup = (E + kSuper - 1) / kSuper;
+  const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
+  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
+    const int64_t p0 = c * kSuper + (W == 3 ? 8 : 0), p1 = E - c * kSuper < kSuper ? E : c * kSuper + kSuper;
+    for (int64_t b = p0 + lane * (W == 3 ? 1 : W); b < p1; b += 64 * (W == 3 ? 1 : W)) {
+      if (W == 2 && b + 1 < p1) {
+        longlong2 v;
+        v.x = b;
+        v.y = b + 1;
+        *reinterpret_cast<longlong2*>(times + b) = v;
+      } else {
+        times[b] = b;
+      }
     }
   }
 }
@@ -617,10 +842,82 @@ void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_
 
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
-                     int64_t nruns, const int64_t* chunk_run, int64_t cap, int64_t* times,
+                     int64_t nruns, int64_t* chunk_run, int64_t cap, int64_t* times,
                      int n_blocks, hipStream_t st) {
-  hipLaunchKernelGGL(k_write_cf, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, specs, p,
-                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
+  // CG_WRITE_PROBE (diagnostic only, never set in production): replace the
+  // writer by a plain fill of the same E*8 output bytes, same grid and slices,
+  // with 8 B (1) or 16 B (2) per lane per store -- the store ceiling the
+  // writer is compared against.
+  static const int probe = [] {
+    const char* e = getenv("CG_WRITE_PROBE");
+    return e ? atoi(e) : 0;
+  }();
+  if (probe == 1) {
+    hipLaunchKernelGGL(k_fill_probe<1>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
+                       nruns, cap, times);
+    return;
+  }
+  if (probe == 4) {
+    hipLaunchKernelGGL(k_fill_probe<4>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
+                       nruns, cap, times);
+    return;
+  }
+  if (probe == 6) {
+    hipLaunchKernelGGL(k_fill_probe<6>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
+                       nruns, cap, times);
+    return;
+  }
+  if (probe == 7) {
+    hipLaunchKernelGGL(k_fill_probe<7>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
+                       nruns, cap, times);
+    return;
+  }
+  if (probe == 5) {  // hipMemsetAsync of the capacity (>= the E*8 bytes)
+    (void)hipMemsetAsync(times, 0, size_t(cap) * 8, st);
+    return;
+  }
+  if (probe == 3) {  // 8 B per lane, every store instruction 64 B off a 512 B boundary
+    hipLaunchKernelGGL(k_fill_probe<3>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
+                       nruns, cap, times);
+    return;
+  }
+  if (probe == 2) {
+    hipLaunchKernelGGL(k_fill_probe<2>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
+                       nruns, cap, times);
+    return;
+  }
+  static const int variant = [] {
+    const char* e = getenv("CG_WRITE_VARIANT");  // diagnostic only (see put<V>)
+    return e ? atoi(e) : 0;
+  }();
+  const size_t lds = size_t(p.G) * sizeof(Segment);
+#define CG_WCF(V)                                                                                \
+  hipLaunchKernelGGL(k_write_cf<V>, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p, \
+                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times)
+  switch (variant) {
+    case 1: CG_WCF(1); break;
+    case 2: CG_WCF(2); break;
+    case 4: CG_WCF(4); break;
+    case 8: CG_WCF(8); break;
+    case 12: CG_WCF(12); break;
+    case 16: CG_WCF(16); break;
+    case 32: CG_WCF(32); break;
+    case 76: CG_WCF(76); break;
+    case 128: CG_WCF(128); break;
+    default: CG_WCF(0); break;
+  }
+#undef CG_WCF
+  if (variant & 32) {
+    unsigned long long d[8];
+    (void)hipMemcpyAsync(d, chunk_run + cap / kSuper + 2 + kTicketWords, sizeof d,
+                         hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    fprintf(stderr,
+            "[k_write_cf stats] waves=%llu cycles/wave: all=%.0f window=%.0f long=%.0f | "
+            "per wave: windows=%.1f long_pieces=%.1f\n",
+            d[7], double(d[0]) / d[7], double(d[1]) / d[7], double(d[2]) / d[7],
+            double(d[4]) / d[7], double(d[5]) / d[7]);
+  }
 }
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
