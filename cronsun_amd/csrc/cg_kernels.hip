@@ -324,20 +324,88 @@ __device__ __forceinline__ bool ap_level(uint64_t m, uint32_t n, int32_t* p0, in
   return (((rest << st) | 1ull) & low) == rest;
 }
 
-// Fires [p0, p1) of closed-form run w, wave-cooperatively: lane l writes
-// p0 + l + 64u.  A fire's index g = rank(anchor) - 1 + (p - run start) counts
-// (day, hour, minute, second) combinations from the anchor's local day, so it
-// is carried as mixed-radix digits (matching-day rank, hour/minute/second
-// ranks; radices -, nH, nM, nS) and stepped by the constant 64.  Same
-// enumeration as cf_seek/cf_next.  Rank -> seconds, cheapest form first:
+// The aligned 64-fire block holding a run boundary, assembled across runs:
+// each run fills its lanes, and the run that completes the block stores it
+// with one whole 512 B store (no partially written cache line reaches HBM).
+struct Pending {
+  int64_t blk;  // block start, or -1 (wave-uniform)
+  int64_t val;  // this lane's fire in it
+};
+
+// Position offset of this lane's first fire of a piece starting at p0: lane l
+// covers p0 + x, x = (floor64(p0) + l - p0) mod 64 -- lanes before p0 in the
+// head block belong to earlier runs and start one block later.
+__device__ __forceinline__ uint32_t lane_offset(int64_t p0) {
+  const int lane = threadIdx.x & 63;
+  const int32_t x = int32_t((p0 & ~int64_t(63)) + lane - p0);
+  return uint32_t(x < 0 ? x + 64 : x);
+}
+
+// Runs the piece [p0, p1) through the block protocol: value() is this lane's
+// current fire, step() advances it by 64 fires.  Full blocks are stored as
+// computed (8 values first, then 8 stores: a wave held back by a full memory
+// pipe has no arithmetic queued behind the store); the head block merges the
+// pending fires of earlier runs; a partial tail block becomes pending.
+// GAP: a walked run -- its fires come from k_write_walk, so only the shared
+// blocks are written (placeholders there), never its own full blocks.
+template <int V, bool GAP, class Val, class Step>
+__device__ __forceinline__ void drive(Val&& value, Step&& step, int64_t p0, int64_t p1,
+                                      Pending& pd, int64_t* __restrict__ times) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b0 = p0 & ~int64_t(63);
+  const bool mine0 = b0 + lane >= p0;
+  {
+    int64_t v = GAP ? 0 : value();
+    if (!mine0) v = pd.val;
+    if (b0 + 64 > p1) {  // the run ends inside its head block
+      pd.blk = b0;
+      pd.val = v;
+      return;
+    }
+    put<V>(times + b0 + lane, v);
+    pd.blk = -1;
+    if (!GAP && mine0) step();
+  }
+  int64_t b = b0 + 64;
+  if (GAP) {
+    b += (p1 - b) & ~int64_t(63);
+  } else {
+    for (; b + 8 * 64 <= p1; b += 8 * 64) {
+      int64_t vv[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        vv[u] = value();
+        step();
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) asm volatile("" : "+v"(vv[u]));
+#pragma unroll
+      for (int u = 0; u < 8; u++) put<V>(times + b + 64 * u + lane, vv[u]);
+    }
+    for (; b + 64 <= p1; b += 64) {
+      put<V>(times + b + lane, value());
+      step();
+    }
+  }
+  if (b < p1) {
+    pd.blk = b;
+    pd.val = GAP ? 0 : value();
+  }
+}
+
+// Fires [p0, p1) of closed-form run w (run start roff), wave-cooperatively.
+// A fire's index g = rank(anchor) - 1 + (p - roff) counts (day, hour, minute,
+// second) combinations from the anchor's local day, so it is carried as
+// mixed-radix digits (matching-day rank, hour/minute/second ranks; radices -,
+// nH, nM, nS) and stepped by the constant 64.  Same enumeration as
+// cf_seek/cf_next.  Rank -> seconds, cheapest form first:
 //   linear   every level an arithmetic progression and the sequence has one
 //            stride (e.g. */10 s with every minute/hour/day): t += 64*stride;
 //   affine   every level an arithmetic progression: t = C0 + sum r_i * w_i;
 //   tables   otherwise: per-level lane tables read with ds_bpermute.
 template <int V>
 __device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_t p0, int64_t p1,
-                        int64_t* __restrict__ times) {
-  const int lane = threadIdx.x & 63;
+                        Pending& pd, int64_t* __restrict__ times) {
   const CFRule c = cf_rule(w.sp);
   const uint32_t nS = c.nS, nM = c.nM, nH = uint32_t(__builtin_popcount(c.H));
   const uint32_t rf = uint32_t(w.anchor - sg.base);
@@ -352,9 +420,9 @@ __device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_
   g -= h * c.nMS;
   uint32_t m = fdiv(g, nS, iS);
   uint32_t s = g - m * nS;
-  // + lane
+  // + this lane's offset (< 128)
   uint32_t q;
-  s += uint32_t(lane);
+  s += lane_offset(p0);
   q = small_div(s, iS);
   s -= q * nS;
   m += q;
@@ -384,21 +452,11 @@ __device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_
     h -= ch ? nH : 0u;
     d += a3 + ch;
   };
-  int64_t* out = times + p0 + lane;
-  const int64_t n = p1 - p0;
   int32_t s0, ss, m0, ms, h0, hs, d0, ds;
   const uint32_t nD = uint32_t(__builtin_popcount(dmask));
   const bool apS = ap_level(c.S, nS, &s0, &ss), apM = ap_level(c.M, nM, &m0, &ms);
   const bool apH = ap_level(c.H, nH, &h0, &hs), apD = ap_level(dmask, nD, &d0, &ds);
-  const bool affine = apS && apM && apH && apD;
-  if (V & 128) {  // diagnostic: the full per-piece setup, then a plain fill of the piece
-    asm volatile("" ::"v"(s), "v"(m), "v"(h), "v"(d), "v"(a0), "v"(a1), "v"(a2), "v"(a3));
-    asm volatile("" ::"v"(int(affine)), "v"(ss + ms + hs + ds + s0 + m0 + h0 + d0));
-    for (int64_t b = 0; b < n; b += 64)
-      if (b + lane < n) put<V>(out + b, b);
-    return;
-  }
-  if (affine) {
+  if (apS && apM && apH && apD) {
     const int64_t C0 = sg.base + s0 + 60 * m0 + 3600 * h0 + 86400 * int32_t(jf);  // d0 == 0
     const uint32_t ws = uint32_t(ss), wm = 60u * uint32_t(ms), wh = 3600u * uint32_t(hs),
                    wd = 86400u * uint32_t(ds);
@@ -419,41 +477,12 @@ __device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_
     } else {
       stride = 86400 * ds;
     }
-    if (stride > 0 || n <= 64) {
+    if (stride > 0) {
       int64_t v = value();
       const int64_t st = 64 * int64_t(stride);
-      int64_t b = 0;
-      for (; b + 8 * 64 <= n; b += 8 * 64) {
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          put<V>(out + b + 64 * u, v);
-          v += st;
-        }
-      }
-      for (; b < n; b += 64) {
-        if (b + lane < n) put<V>(out + b, v);
-        v += st;
-      }
-      return;
-    }
-    int64_t b = 0;
-    for (; b + 8 * 64 <= n; b += 8 * 64) {
-      // all 8 values first, then the 8 stores: a wave whose store is held
-      // back by a full memory pipe has no arithmetic queued behind it
-      int64_t vv[8];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        vv[u] = value();
-        step();
-      }
-#pragma unroll
-      for (int u = 0; u < 8; u++) asm volatile("" : "+v"(vv[u]));
-#pragma unroll
-      for (int u = 0; u < 8; u++) put<V>(out + b + 64 * u, vv[u]);
-    }
-    for (; b < n; b += 64) {
-      if (b + lane < n) put<V>(out + b, value());
-      step();
+      drive<V, false>([&]() { return v; }, [&]() { v += st; }, p0, p1, pd, times);
+    } else {
+      drive<V, false>(value, step, p0, p1, pd, times);
     }
     return;
   }
@@ -462,70 +491,53 @@ __device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_
   const int32_t th = rank_table(c.H, 3600);
   const int32_t td = rank_table(uint64_t(dmask), 86400) + int32_t(jf) * 86400;
   const int64_t base = sg.base;
-  auto value = [&]() -> int64_t {
+  auto value = [&]() -> int64_t {  // all lanes active: the table reads are cross-lane
     return base + int64_t(rank_at(td, d) + rank_at(th, h) + rank_at(tm, m) + rank_at(ts, s));
   };
-  int64_t b = 0;
-  for (; b + 8 * 64 <= n; b += 8 * 64) {
-    int64_t vv[8];  // values first, then the stores (as in the affine loop)
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      vv[u] = value();
-      step();
+  drive<V, false>(value, step, p0, p1, pd, times);
+}
+
+// Fires [p0, p1) of a short closed-form run: each lane seeks its own fire
+// (the anchor itself, its successor, or cf_seek).
+template <int V>
+__device__ void tiny_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_t p0, int64_t p1,
+                        Pending& pd, int64_t* __restrict__ times) {
+  int32_t k = int32_t(p0 - roff) + int32_t(lane_offset(p0));
+  const CFRule c = cf_rule(w.sp);
+  auto value = [&]() -> int64_t {
+    if (k == 0) return w.anchor;
+    if (int64_t(k) >= p1 - roff) return 0;  // not this run's (a later run's lane)
+    if (k == 1) {
+      CFIter it = cf_decode(sg, w.anchor);
+      cf_next(c, w.dmask, it);
+      return cf_value(sg, it);
     }
-#pragma unroll
-    for (int u = 0; u < 8; u++) asm volatile("" : "+v"(vv[u]));
-#pragma unroll
-    for (int u = 0; u < 8; u++) put<V>(out + b + 64 * u, vv[u]);
-  }
-  for (; b < n; b += 64) {
-    const int64_t v = value();  // all lanes: the table reads are cross-lane
-    if (b + lane < n) put<V>(out + b, v);
-    step();
-  }
+    return cf_value(sg, cf_seek_fast(c, sg, w.dmask, w.anchor, k));
+  };
+  drive<V, false>(value, [&]() { k += 64; }, p0, p1, pd, times);
 }
 
 // Fires [p0, p1) of @every run w: anchor + (k + 1) * D (constantdelay.go:25-27)
 template <int V>
-__device__ void coop_every(const WinRun& w, int64_t roff, int64_t p0, int64_t p1,
+__device__ void coop_every(const WinRun& w, int64_t roff, int64_t p0, int64_t p1, Pending& pd,
                            int64_t* __restrict__ times) {
-  const int lane = threadIdx.x & 63;
   const int64_t D = int64_t(w.sp.sec);
-  int64_t t = w.anchor + (p0 - roff + lane + 1) * D;
+  int64_t t = w.anchor + (p0 - roff + int64_t(lane_offset(p0)) + 1) * D;
   const int64_t st = 64 * D;
-  int64_t* out = times + p0 + lane;
-  const int64_t n = p1 - p0;
-  int64_t b = 0;
-  for (; b + 8 * 64 <= n; b += 8 * 64) {
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      put<V>(out + b + 64 * u, t);
-      t += st;
-    }
-  }
-  for (; b < n; b += 64) {
-    if (b + lane < n) put<V>(out + b, t);
-    t += st;
-  }
+  drive<V, false>([&]() { return t; }, [&]() { t += st; }, p0, p1, pd, times);
 }
 
-// Fires [pos, rend) spread over many short runs of the window (all inside it):
-// per kChunk piece lane l materialises events [8l, 8l+8) (seek once, then the
-// branch-free iterator), stages them in LDS, and the wave stores the piece
-// with coalesced 512 B wave-instructions.  Walked runs get placeholders that
-// k_write_walk overwrites.
 // Persistent closed-form writer.  Waves work independently on kSuper-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
 // consecutive runs (one coalesced round of loads, staged in its LDS slice;
-// only the runs the slice can touch are loaded) and walks its slice in whole,
-// aligned 64-fire blocks, so every store instruction writes one full 512 B
-// block (no partially written cache lines reach HBM):
-//   * blocks inside one run are written wave-cooperatively, 64 consecutive
-//     fires per store, from mixed-radix digits (coop_cf) or the @every
-//     progression (coop_every);
-//   * a block shared by several runs (run boundaries, short runs) is written
-//     lane-parallel: each lane seeks its own fire (cf_seek).
-// Walked runs are left to k_write_walk, which runs after this kernel.
+// only the runs the slice can touch are loaded) and walks its slice run by
+// run, in aligned 64-fire blocks: every store instruction writes one whole
+// 512 B block (a block shared by several runs is assembled across them, see
+// Pending), so no partially written cache line reaches HBM.  Long runs are
+// generated wave-cooperatively from mixed-radix digits (coop_cf) or the
+// @every progression (coop_every); short runs by per-lane seeks (tiny_cf).
+// Walked runs' own blocks are left to k_write_walk, which runs after this
+// kernel.
 template <int V>
 __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
@@ -594,7 +606,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
     return grp + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
   };
   // V & 32 (diagnostic): per-phase shader-clock totals and counts
-  uint64_t st_win = 0, st_long = 0, st_all = 0, n_win = 0, n_long = 0;  // (coop only)
+  uint64_t st_win = 0, st_long = 0, st_all = 0, n_win = 0, n_long = 0, st_mix = 0, n_mix = 0;
   auto clk = [&]() -> uint64_t { return (V & 32) ? __builtin_amdgcn_s_memtime() : 0; };
   const uint64_t k_start = clk();
   for (int64_t c = take(); c < nsup;) {
@@ -612,72 +624,56 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       st_win += clk() - t_a;
       n_win++;
     }
+    Pending pd;
+    pd.blk = -1;
+    pd.val = 0;
+    int i = 63 - __builtin_clzll(__ballot(woff <= pos));  // the run holding pos
     while (pos < S1) {
-      // the run holding pos: the last window lane with off <= pos (lane 0 qualifies)
-      const int i = 63 - __builtin_clzll(__ballot(woff <= pos));
-      if (i == 63 && jw + 64 < jend) {  // may continue past the window: slide it
-        jw += 63;
+      if (i == 64) {  // past the window (the slice's runs continue: jw + 64 < jend)
+        jw += 64;
+        t_a = clk();
         load_window(jw);
+        if (V & 32) {
+          st_win += clk() - t_a;
+          n_win++;
+        }
+        i = 0;
+      }
+      const int32_t cnt = rl32(wcnt, i);
+      if (cnt == 0) {
+        i++;
         continue;
       }
       const int64_t roff = rl64(woff, i);
-      const int64_t rend = roff + rl32(wcnt, i);
-      // whole 64-fire blocks of run i from pos on
-      int64_t blk_end = (rend < S1 ? rend : S1) & ~int64_t(63);
-      if (blk_end > pos) {
-        const WinRun& w = win[i];
-        const Segment& sg = segs[win_seg(w)];
-        t_a = clk();
-        if (V & 8) {
-        } else if (win_every(w)) {
-          coop_every<V>(w, roff, pos, blk_end, times);
-        } else if (!run_is_walked(sg, w.dmask)) {
-          coop_cf<V>(w, roff, sg, pos, blk_end, times);
-        }  // a walked run's fires come from k_write_walk
-        if (V & 32) {
-          st_long += clk() - t_a;
+      const int64_t p1 = roff + cnt < S1 ? roff + cnt : S1;
+      const WinRun& w = win[i];
+      const Segment& sg = segs[win_seg(w)];
+      t_a = clk();
+      if (V & 8) {
+      } else if (win_every(w)) {
+        coop_every<V>(w, roff, pos, p1, pd, times);
+      } else if (run_is_walked(sg, w.dmask)) {
+        drive<V, true>([]() { return int64_t(0); }, []() {}, pos, p1, pd, times);
+      } else if (p1 - pos >= 64) {
+        coop_cf<V>(w, roff, sg, pos, p1, pd, times);
+      } else {
+        tiny_cf<V>(w, roff, sg, pos, p1, pd, times);
+      }
+      if (V & 32) {
+        const uint64_t dt = clk() - t_a;
+        if (p1 - pos >= 64) {
+          st_long += dt;
           n_long++;
+        } else {
+          st_mix += dt;
+          n_mix++;
         }
-        pos = blk_end;
-        continue;
       }
-      // A block shared by several runs (run ends, short runs): lane l computes
-      // fire pos + l of whichever run holds it (the per-lane seek), then the
-      // block is stored whole.  Its runs may extend past the window: slide
-      // and finish the remaining lanes.
-      const int64_t e = pos + lane;
-      bool done = e >= S1 || (V & 4);
-      int64_t val = 0;
-      for (;;) {
-        const int L = 63 - __builtin_clzll(__ballot(woff != INT64_MAX));
-        const int64_t wend = rl64(woff, L) + rl32(wcnt, L);
-        // window lane of the run holding e: the last lane with off <= e
-        int j = 0;
-#pragma unroll
-        for (int st = 32; st > 0; st >>= 1) {
-          const int64_t v = __shfl(woff, (j + st) & 63, 64);
-          if (j + st < 64 && v <= e) j += st;
-        }
-        const int64_t joff = __shfl(woff, j, 64);  // all lanes active here
-        if (!done && e < wend) {
-          const WinRun& w = win[j];
-          const int32_t k = int32_t(e - joff);
-          const Segment& sg = segs[win_seg(w)];
-          if (win_every(w)) {
-            val = w.anchor + int64_t(k + 1) * int64_t(w.sp.sec);
-          } else if (!run_is_walked(sg, w.dmask)) {
-            const CFRule cr = cf_rule(w.sp);
-            val = cf_value(sg, cf_seek_fast(cr, sg, w.dmask, w.anchor, k));
-          }  // walked: a placeholder k_write_walk overwrites
-          done = true;
-        }
-        if (__ballot(!done) == 0) break;
-        jw += 63;  // the window's last run ends before some lane's fire
-        load_window(jw);
-      }
-      if (e < S1 && !(V & 4)) put<V>(times + e, val);
-      pos += 64;
+      pos = p1;
+      i++;
     }
+    // the last slice ends inside a block
+    if (pd.blk >= 0 && pd.blk + lane < S1 && !(V & 8)) put<V>(times + pd.blk + lane, pd.val);
     c = c_next;
   }
   if (V & 32) {
@@ -688,10 +684,10 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       atomicAdd(dbg + 0, st_all);
       atomicAdd(dbg + 1, st_win);
       atomicAdd(dbg + 2, st_long);
-      atomicAdd(dbg + 3, 0ull);
+      atomicAdd(dbg + 3, st_mix);
       atomicAdd(dbg + 4, n_win);
       atomicAdd(dbg + 5, n_long);
-      atomicAdd(dbg + 6, 0ull);
+      atomicAdd(dbg + 6, n_mix);
       atomicAdd(dbg + 7, 1ull);
     }
   }
@@ -913,10 +909,10 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
                          hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     fprintf(stderr,
-            "[k_write_cf stats] waves=%llu cycles/wave: all=%.0f window=%.0f long=%.0f | "
-            "per wave: windows=%.1f long_pieces=%.1f\n",
-            d[7], double(d[0]) / d[7], double(d[1]) / d[7], double(d[2]) / d[7],
-            double(d[4]) / d[7], double(d[5]) / d[7]);
+            "[k_write_cf stats] waves=%llu cycles/wave: all=%.0f window=%.0f coop=%.0f tiny=%.0f | "
+            "per wave: windows=%.1f coop_pieces=%.1f tiny_pieces=%.1f\n",
+            d[7], double(d[0]) / d[7], double(d[1]) / d[7], double(d[2]) / d[7], double(d[3]) / d[7],
+            double(d[4]) / d[7], double(d[5]) / d[7], double(d[6]) / d[7]);
   }
 }
 

@@ -12,6 +12,4 @@ run() {  # name env...
 }
 run base X=0
 run fill8 CG_WRITE_PROBE=1
-run no_mixed CG_WRITE_VARIANT=4
-run bpc4 CG_WRITE_BLOCKS_PER_CU=4
-run base2 X=0
+run stats CG_WRITE_VARIANT=32
