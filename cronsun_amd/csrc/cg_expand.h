@@ -135,6 +135,33 @@ CG_HD int64_t cf_value(const Segment& sg, const CFIter& it) {
   return sg.base + (int64_t)(uint32_t)(it.day * 86400 + it.h * 3600 + it.m * 60 + it.s);
 }
 
+// First matching local time after instant u inside CF segment sg (day mask
+// dmask), or INT64_MAX when none of the segment's days has one.  Within a
+// constant-offset span Go's Next is the fixed-offset walk, which returns
+// exactly this, so a run's first fire needs no walk when the
+// walk from its start would stay inside the span.
+CG_HD int64_t cf_first_after(const CFRule& c, const Segment& sg, uint32_t dmask, int64_t u) {
+  if (c.C == 0) return INT64_MAX;
+  const int64_t rf = u - sg.base;
+  int32_t j = 0, tod = -1;  // u's local day in the segment and second of day
+  if (rf >= 0) {
+    if (rf >= 32 * 86400LL) return INT64_MAX;
+    j = (int32_t)(rf / 86400);
+    tod = (int32_t)(rf - (int64_t)j * 86400);
+  }
+  uint32_t r = 0;  // rank of the first combination after tod
+  if (!((dmask >> j) & 1u) || (r = cf_rank(c, tod)) >= c.C) {
+    const uint32_t above = j >= 31 ? 0u : (dmask & (~0u << (j + 1)));
+    if (!above) return INT64_MAX;
+    j = __builtin_ctz(above);
+    r = 0;
+  }
+  const uint32_t hi = r / c.nMS, rem = r - hi * c.nMS;
+  const uint32_t mi = rem / c.nS, si = rem - mi * c.nS;
+  return sg.base + (int64_t)j * 86400 + (int64_t)select64(c.H, hi) * 3600 +
+         (int64_t)select64(c.M, mi) * 60 + select64(c.S, si);
+}
+
 // Run records of one rule over the plan's G segments (k_count's body).
 // Writes anchor/count/dmask at stride 1 from the given pointers.  Returns
 // false where the reference loop never terminates: Next never returns
@@ -184,7 +211,21 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
     const Segment& sg = segs[s];
     int64_t anchor = 0, cnt = 0;
     uint32_t dm = 0;
-    if (!done) {
+    if (!done && sg.kind == 0 && pending == INT64_MIN) {
+      // Next(pos) in closed form: pos is T0 inside this constant-offset span,
+      // or the last fire of the CF segment just before it (same span), so the
+      // walk from pos never leaves the span before its result
+      const int64_t b = sg.b < t1 ? sg.b : t1;
+      dm = seg_daymask(sp, sg, dtab);
+      const int64_t e = cf_first_after(c, sg, dm, pos > sg.a ? pos : sg.a);
+      if (e <= b) {
+        cnt = 1 + cf_count(c, sg, dm, e, b);
+        anchor = e;
+        pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
+      } else {
+        dm = 0;  // no fire in this segment; the next one searches from its start
+      }
+    } else if (!done) {
       const int64_t b = sg.b < t1 ? sg.b : t1;
       int64_t e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
       pending = INT64_MIN;

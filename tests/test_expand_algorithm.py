@@ -1,0 +1,39 @@
+"""The expansion algorithm the kernels run (cg_expand.h: count_rule with the
+closed-form first fire, closed-form iteration, WALK re-walk), compiled for the
+host and checked fire-by-fire against the oracle's literal Next loop
+(t = Next(t) until > T1) on random specs over zones with DST, midnight and
+30/45-minute transitions (tests/native/expand_host.cpp).  CPU only: the GPU
+tests check the kernels themselves."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "native", "expand_host.cpp")
+BIN = os.path.join(ROOT, "tests", "native", "expand_host")
+
+
+@pytest.fixture(scope="module")
+def expand_host():
+    import oracle_lib as O
+    O.lib()  # builds oracle/liboracle.so if needed
+    srcs = [SRC, os.path.join(ROOT, "cronsun_amd", "csrc", "cg_zone.cpp")]
+    if not os.path.exists(BIN) or any(os.path.getmtime(BIN) < os.path.getmtime(s) for s in srcs + [
+            os.path.join(ROOT, "cronsun_amd", "csrc", "cg_expand.h"),
+            os.path.join(ROOT, "cronsun_amd", "csrc", "cg_time.h")]):
+        subprocess.check_call(["g++", "-O2", "-std=c++17", "-o", BIN] + srcs +
+                              ["-L" + os.path.join(ROOT, "oracle"), "-loracle",
+                               "-Wl,-rpath," + os.path.join(ROOT, "oracle")])
+    return BIN
+
+
+@pytest.mark.parametrize("zone", ["UTC", "America/New_York", "Europe/London", "Australia/Sydney",
+                                  "America/Havana", "Australia/Lord_Howe", "Asia/Kathmandu",
+                                  "Pacific/Chatham", "America/St_Johns", "Africa/Casablanca",
+                                  "Pacific/Apia"])
+def test_host_algorithm_matches_oracle(expand_host, zone):
+    out = subprocess.run([expand_host, zone, "300", "11"], cwd=ROOT, capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert " 0 mismatches" in out.stdout
