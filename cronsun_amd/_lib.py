@@ -8,7 +8,8 @@ import importlib.util
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcronsun_gpu.so")
+# CRONSUN_GPU_LIB: an alternative in-tree build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("CRONSUN_GPU_LIB") or os.path.join(HERE, "libcronsun_gpu.so")
 
 CG_OK = 0
 CG_EINVAL = -1

@@ -24,7 +24,10 @@ constexpr int kWritePerThread = 8;
 constexpr int kWriteChunk = kWriteThreads * kWritePerThread;
 // closed-form writer: 4 waves per block; waves take kSuper-event output slices
 constexpr int kWriteWaves = 4;
-constexpr int kWriteBlocksPerCU = 4;  // persistent grid: 6 x 4 waves per CU (LDS ~22 KB/block)
+#ifndef CG_WRITE_BPC
+#define CG_WRITE_BPC 4
+#endif
+constexpr int kWriteBlocksPerCU = CG_WRITE_BPC;  // persistent grid: blocks of 4 waves per CU
 constexpr int kSuper = 16384;
 // writer slice tickets: one u32 counter per group of blocks, 128 B apart
 constexpr int kTicketGroups = 8;

@@ -19,6 +19,9 @@
 #include <cstdlib>
 
 #include "cg_expand.h"
+#ifndef CG_WRITE_BATCH
+#define CG_WRITE_BATCH 8
+#endif
 #include "cg_kernels.h"
 
 namespace cg {
@@ -341,6 +344,8 @@ __device__ __forceinline__ uint32_t lane_offset(int64_t p0) {
   return uint32_t(x < 0 ? x + 64 : x);
 }
 
+constexpr int kBatch = CG_WRITE_BATCH;  // blocks computed before their stores are issued
+
 // Runs the piece [p0, p1) through the block protocol: value() is this lane's
 // current fire, step() advances it by 64 fires.  Full blocks are stored as
 // computed (8 values first, then 8 stores: a wave held back by a full memory
@@ -370,17 +375,17 @@ __device__ __forceinline__ void drive(Val&& value, Step&& step, int64_t p0, int6
   if (GAP) {
     b += (p1 - b) & ~int64_t(63);
   } else {
-    for (; b + 8 * 64 <= p1; b += 8 * 64) {
-      int64_t vv[8];
+    for (; b + kBatch * 64 <= p1; b += kBatch * 64) {
+      int64_t vv[kBatch];
 #pragma unroll
-      for (int u = 0; u < 8; u++) {
+      for (int u = 0; u < kBatch; u++) {
         vv[u] = value();
         step();
       }
 #pragma unroll
-      for (int u = 0; u < 8; u++) asm volatile("" : "+v"(vv[u]));
+      for (int u = 0; u < kBatch; u++) asm volatile("" : "+v"(vv[u]));
 #pragma unroll
-      for (int u = 0; u < 8; u++) put<V>(times + b + 64 * u + lane, vv[u]);
+      for (int u = 0; u < kBatch; u++) put<V>(times + b + 64 * u + lane, vv[u]);
     }
     for (; b + 64 <= p1; b += 64) {
       put<V>(times + b + lane, value());

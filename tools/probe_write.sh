@@ -10,5 +10,8 @@ run() {  # name env...
   env "$@" timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-sample 0 > gpurun_out/probe/$name.json 2> gpurun_out/probe/$name.err || exit 1
   python3 -c "import json; d=json.load(open('gpurun_out/probe/$name.json')); print('%-14s write_cf_ms=%.4f' % ('$name', d['kernel_ms']['write_cf']))"
 }
-run stats_compute CG_WRITE_VARIANT=33
-run stats CG_WRITE_VARIANT=32
+run base X=0
+run b4 CRONSUN_GPU_LIB=$PWD/cronsun_amd/libcronsun_gpu_b4.so
+run fill8 CG_WRITE_PROBE=1
+run base2 X=0
+run b4_2 CRONSUN_GPU_LIB=$PWD/cronsun_amd/libcronsun_gpu_b4.so
