@@ -2,13 +2,24 @@
 (1M mixed cron rules x 24 h horizon, UTC) per MI355X, weak-scaled over
 job-ID-range shards at N > 1.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W]
   (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
 
-A step = one full expansion of the rank's rule shard over the horizon:
-count -> scan -> block map -> closed-form write -> WALK write -> offsets, with
-the specs resident in HBM and the fire times left in HBM.  At N > 1 each step
-also all-gathers the per-rank event totals (global CSR offsets) over RCCL.
+Workloads (`--workload`, default config2 -- the headline line):
+  config2  a step = one full expansion of the rank's 1M-rule shard over 24 h:
+           count -> scan -> slice map -> closed-form write -> walk write ->
+           offsets, specs resident in HBM, fire times left in HBM.  At N > 1
+           each step also all-gathers the per-rank event totals (global CSR
+           offsets) over RCCL.
+  pernode  config 3 shape: 1M jobs x 10k nodes (500 groups, 0-3 GroupIDs,
+           0-4 NodeIDs, 0-2 ExcludeNodeIDs per rule), the lighter spec mix and
+           a 1 h horizon so the per-node fan-out fits HBM; a step = expansion +
+           rule->node join + transpose + per-node (time, rule) lists, rules
+           resident in HBM (cg_rules_upload).  At N > 1 the per-node counts are
+           all-gathered over RCCL (per-node offsets of every rank's slice).
+  config4  config 4 shape: 10M rules x 7 days over the job-ID-range shards of
+           N GPUs (10M / N rules per rank, lighter spec mix); a step = one
+           expansion per rank.  Fixed total work: `scaling` = "strong".
 
 Prints one JSON line (rank 0).  See DESIGN.md §Measurement for the roofline
 and CPU-baseline definitions.
@@ -23,7 +34,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-SPEC_BYTES = 32          # packed SoA spec per rule in HBM
+SPEC_BYTES = 32          # packed spec per rule in HBM
+METRIC = "fire events materialised/sec (1M rules × 24h) + HBM GB/s at 1/2/4/8 GPU"
 
 
 def log(*a):
@@ -50,8 +62,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--rules", type=int, default=1_000_000, help="rules per GPU")
-    ap.add_argument("--horizon", type=int, default=86400)
+    ap.add_argument("--workload", choices=["config2", "pernode", "config4"], default="config2")
+    ap.add_argument("--rules", type=int, default=0, help="rules per GPU (0 = the workload's)")
+    ap.add_argument("--horizon", type=int, default=0, help="seconds (0 = the workload's)")
     ap.add_argument("--cpu-sample", type=int, default=40_000,
                     help="rules in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -65,21 +78,42 @@ def main():
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
-    import numpy as np
 
-    from cronsun_amd import cron, synth
+    from cronsun_amd import cron, shard, synth
     from cronsun_amd.engine import Engine
 
-    R, H = args.rules, args.horizon
+    wl = args.workload
+    if wl == "config2":
+        R = args.rules or 1_000_000
+        H = args.horizon or 86400
+        mix = synth.MIX_CONFIG2
+        seed = 0x5EED + rank
+    elif wl == "pernode":
+        R = args.rules or 1_000_000
+        H = args.horizon or 3600
+        mix = synth.MIX_LIGHT
+        seed = 0x5EED + 3 + rank
+    else:  # config4: 10M rules in total, job-ID-range shards
+        total = args.rules or 10_000_000
+        lo, hi = shard.shard_range(total, world, rank)
+        R = hi - lo
+        H = args.horizon or 7 * 86400
+        mix = synth.MIX_LIGHT
+        seed = 0x5EED + 4 + lo  # a shard's rules depend on its job-ID range only
     t0 = synth.T0_2026
     t1 = t0 + H
     eng = Engine(local)
-    log(f"[rank {rank}] generating {R} rules (job-ID shard {rank})")
-    specs = synth.spec_mix(R, seed=0x5EED + rank)
+    log(f"[rank {rank}] {wl}: generating {R} rules (job-ID shard {rank})")
+    specs = synth.spec_mix(R, seed=seed, mix=mix)
     arr, status = cron.parse_batch(specs, threads=16)
     assert (status == 0).all()
     sp = eng.upload_c(arr, R)
     utc = cron.UTC()
+    drules = None
+    n_nodes = 10_000
+    if wl == "pernode":
+        rin = synth.rules_for_nodes(R, n_nodes=n_nodes, n_groups=500, seed=0x5EED + 3 + 1000 * rank)
+        drules = eng.upload_rules(rin)
 
     def barrier():
         if world > 1:
@@ -87,8 +121,18 @@ def main():
 
     dev = torch.device("cuda", local)
     tot = torch.zeros(world, dtype=torch.int64, device=dev)
+    node_counts = torch.zeros(n_nodes, dtype=torch.int64, device=dev) if wl == "pernode" else None
+    last = {}
 
     def step():
+        if wl == "pernode":
+            En, nnz = eng.expand_per_node_rules_device(sp, utc, t0, t1, drules)
+            last["nnz"] = nnz
+            if world > 1:
+                # per-node offsets of every rank's slice (RCCL allgather of N int64)
+                eng.node_counts_to_device(node_counts.data_ptr())
+                shard.node_offsets(node_counts, dist)
+            return En
         E = eng.expand_device(sp, utc, t0, t1)
         if world > 1:
             # global CSR offsets of the job-ID-range shards (RCCL allgather)
@@ -102,10 +146,11 @@ def main():
     barrier()
     torch.cuda.synchronize()
     start = time.perf_counter()
-    kts = []
+    kts, nkts = [], []
     for _ in range(args.steps):
         E = step()
         kts.append(eng.kernel_times())
+        nkts.append(eng.node_kernel_times())
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - start
@@ -118,10 +163,9 @@ def main():
     elapsed = float(el.item())
     total_events = int(ev.item())
 
-    kt = np.mean(np.array(kts), axis=0)  # count, scan, map, write_cf, write_walk, offsets (ms)
-    algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
-    write_s = kt[3] / 1e3
-    achieved = algo_bytes / write_s / 1e9 if write_s > 0 else 0.0
+    import numpy as np
+    kt = np.mean(np.array(kts), axis=0)    # count, scan, map, write_cf, write_walk, offsets (ms)
+    nkt = np.mean(np.array(nkts), axis=0)  # join, transpose, node write (ms)
     ms_step = elapsed / args.steps * 1e3
 
     if rank != 0:
@@ -129,13 +173,33 @@ def main():
             dist.destroy_process_group()
         return
 
+    if wl == "pernode":
+        # per-node CSR bytes: R*32 + nnz*4 + (R+1)*8 + E_n*(8+4) + (N+1)*8;
+        # dominant kernel k_node_write
+        nnz = last["nnz"]
+        algo_bytes = R * SPEC_BYTES + nnz * 4 + (R + 1) * 8 + E * 12 + (n_nodes + 1) * 8
+        kname, ksec = "k_node_write", nkt[2] / 1e3
+        metric = "per-node fire events materialised/sec (config 3: 1M jobs × 10k nodes, 1h)"
+        workload = ("config 3: 1M jobs x 10k nodes (500 groups, GroupIDs/NodeIDs/ExcludeNodeIDs), "
+                    "light spec mix, 1h horizon, UTC, per GPU; exclude mode NONE (job.go:591-630)")
+        traffic = None
+    else:
+        algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
+        kname, ksec = "k_write_cf", kt[3] / 1e3
+        metric = METRIC
+        workload = ("config 2: 1M mixed cron rules x 24h horizon, UTC, per GPU (job-ID-range shards)"
+                    if wl == "config2" else
+                    "config 4: 10M rules x 7d horizon, light spec mix, UTC, job-ID-range shards over N GPUs")
+        traffic = pmc_traffic(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"), kname, R, E) \
+            if wl == "config2" else None
+    achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
+
     cpu = None
-    if world == 1 and args.cpu_sample > 0:
+    if world == 1 and args.cpu_sample > 0 and wl == "config2":
         cpu = cpu_baseline(specs[:args.cpu_sample], t0, t1, args.cpu_threads)
 
-    traffic = pmc_traffic(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"), "k_write_cf", R, E)
     out = {
-        "metric": "fire events materialised/sec (1M rules × 24h) + HBM GB/s at 1/2/4/8 GPU",
+        "metric": metric,
         "value": total_events * args.steps / elapsed,
         "unit": "events/s",
         "n_gpus": world,
@@ -143,25 +207,25 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if wl == "config4" else "weak",
         "vs_baseline": None,
         "dtype": "int64",
-        "data": "synthetic (seeded spec mix, SURVEY.md §8d config 2; parsed on host, resident in HBM)",
+        "data": "synthetic (seeded spec mix, SURVEY.md §8d; parsed on host, resident in HBM)",
         "config": {
-            "workload": "config 2: 1M mixed cron rules x 24h horizon, UTC, per GPU (job-ID-range shards)",
+            "workload": workload,
             "rules_per_gpu": R,
             "horizon_s": H,
             "t0": t0,
             "zone": "UTC",
             "events_per_gpu_step": E,
-            "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard event totals)",
+            "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard totals / per-node counts)",
         },
         "hbm_gbps_step": algo_bytes * world / (elapsed / args.steps) / 1e9,
         "kernel_ms": {"count": kt[0], "scan": kt[1], "block_map": kt[2], "write_cf": kt[3],
                       "write_walk": kt[4], "offsets": kt[5]},
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_write_cf",
+            "kernel": kname,
             "achieved": achieved,
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
@@ -171,6 +235,9 @@ def main():
         },
         "cpu_baseline": cpu,
     }
+    if wl == "pernode":
+        out["kernel_ms"].update({"rule_node_join": nkt[0], "transpose": nkt[1], "node_write": nkt[2]})
+        out["config"]["nnz_rule_node_pairs"] = last["nnz"]
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

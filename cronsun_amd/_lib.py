@@ -116,7 +116,12 @@ def _declare(L):
         "cg_expand_per_node": ([vp, vp, vp, i64, i64, P(cg_rules_in), C.c_int, P(cg_node_csr)], C.c_int),
         "cg_expand_per_node_device": ([vp, vp, vp, i64, i64, P(cg_rules_in), C.c_int, P(i64), P(i64)], C.c_int),
         "cg_node_result_device": ([vp, P(vp), P(vp), P(vp), P(i64)], C.c_int),
+        "cg_node_result_copy": ([vp, vp, vp, vp, i64], C.c_int),
         "cg_node_counts_to_device": ([vp, vp], C.c_int),
+        "cg_rules_upload": ([vp, P(cg_rules_in), P(vp)], C.c_int),
+        "cg_rules_free": ([vp], None),
+        "cg_expand_per_node_rules_device": ([vp, vp, vp, i64, i64, vp, C.c_int, P(i64), P(i64)],
+                                            C.c_int),
         "cg_rule_nodes": ([vp, P(cg_rules_in), C.c_int, vp, vp, i64, P(i64)], C.c_int),
         "cg_jobset_new": ([P(vp)], C.c_int),
         "cg_jobset_free": ([vp], None),

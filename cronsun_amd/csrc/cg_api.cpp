@@ -229,6 +229,7 @@ int cg_init(int device, cg_ctx** out) {
     return cg_fail(CG_EHIP, "hipStreamCreate failed");
   }
   for (auto& e : c->ev) (void)hipEventCreate(&e);
+  for (auto& e : c->pev) (void)hipEventCreate(&e);
   *out = c;
   return CG_OK;
 }
@@ -239,6 +240,7 @@ void cg_destroy(cg_ctx* c) {
   (void)hipStreamSynchronize(c->st);
   c->free_all();
   for (auto& e : c->ev) (void)hipEventDestroy(e);
+  for (auto& e : c->pev) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(c->st);
   delete c;
 }
@@ -452,7 +454,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   const int64_t G = pa.G;
   c->last_R = R;
   c->last_G = G;
-  for (float& x : c->kt) x = 0;
+  for (int i = 0; i < 6; i++) c->kt[i] = 0;
   if ((rc = c->offsets.ensure(R + 1))) return rc;
   if (R == 0 || G == 0) {
     HIPCHK(hipMemsetAsync(c->offsets.p, 0, (R + 1) * 8, c->st));

@@ -44,13 +44,30 @@ struct DBuf {
   }
 };
 
+// An integer-interned rule set in device memory (cg_rules_in uploaded).
+struct RulesStore {
+  DBuf<int64_t> nid_off, gid_off, ex_off, group_off;
+  DBuf<int32_t> nids, gids, ex, group_nodes, rule_job;
+  DBuf<uint8_t> group_exists, job_pause;
+  int32_t n_nodes = 0, n_groups = 0, n_rules = 0, n_jobs = 0;
+  void release() {
+    nid_off.release(); gid_off.release(); ex_off.release(); group_off.release();
+    nids.release(); gids.release(); ex.release(); group_nodes.release(); rule_job.release();
+    group_exists.release(); job_pause.release();
+  }
+};
+
 struct cg_ctx {
   int device = 0;
   int write_blocks = 1024;  // persistent k_write_cf grid (set from the CU count)
   hipStream_t st = nullptr;
   hipEvent_t ev[8] = {};
+  hipEvent_t pev[4] = {};  // per-node phases
   std::mutex mu;
-  float kt[6] = {0, 0, 0, 0, 0, 0};
+  // ms: [0..5] expansion phases (count, scan, map, write_cf, write_walk,
+  // offsets), [6..8] per-node phases (rule->node join, transpose + per-node
+  // offsets, k_node_write) of the last per-node call
+  float kt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
   // plan cache
   cg::Plan plan;
@@ -70,11 +87,9 @@ struct cg_ctx {
   int64_t last_E = 0, last_R = 0, last_G = 0;
 
   // per-node buffers
-  DBuf<int64_t> rn_off, rn_cnt64, pair_pos, node_off, node_time, nt_off, d_nid_off, d_gid_off,
-      d_ex_off, d_group_off;
-  DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule, d_nids, d_gids, d_ex,
-      d_group_nodes, d_rule_job, node_cnt32;
-  DBuf<uint8_t> d_group_exists, d_job_pause;
+  DBuf<int64_t> rn_off, rn_cnt64, pair_pos, node_off, node_time, nt_off;
+  DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule;
+  RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   DBuf<char> pn_tmp;
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
 
@@ -84,13 +99,15 @@ struct cg_ctx {
     block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
     run_dmask.release(); scan_tmp.release(); stuck.release();
     rn_off.release(); rn_cnt64.release(); pair_pos.release(); node_off.release();
-    node_time.release(); nt_off.release(); d_nid_off.release(); d_gid_off.release();
-    d_ex_off.release(); d_group_off.release(); rn_cnt.release(); rn_nodes.release();
+    node_time.release(); nt_off.release(); rn_cnt.release(); rn_nodes.release();
     pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();
-    d_nids.release(); d_gids.release(); d_ex.release(); d_group_nodes.release();
-    d_rule_job.release(); node_cnt32.release(); d_group_exists.release();
-    d_job_pause.release(); pn_tmp.release();
+    rules.release(); pn_tmp.release();
   }
+};
+
+struct cg_rules {
+  cg_ctx* ctx = nullptr;
+  RulesStore st;
 };
 
 struct cg_specs {

@@ -18,10 +18,8 @@ struct PlanArgs {
   int64_t t0, t1;
 };
 
-// per-node writer (cg_pernode.hip): 256 threads x 8 events per block
-constexpr int kWriteThreads = 256;
-constexpr int kWritePerThread = 8;
-constexpr int kWriteChunk = kWriteThreads * kWritePerThread;
+// per-node writer (cg_pernode.hip): output tasks of kNodeTask events per wave
+constexpr int kNodeTask = 8192;
 // closed-form writer: 4 waves per block; waves take kSuper-event output slices
 constexpr int kWriteWaves = 4;
 #ifndef CG_WRITE_BPC

@@ -13,14 +13,17 @@
 //   scan                 -> rule->node CSR offsets
 //   k_rule_nodes<true>   same bitmap, ballot/prefix-sum compaction of set bits
 //   radix sort (node)    stable transpose to node -> rules (rocPRIM)
+//   k_node_bounds        per-node pair offsets (lower bound per node)
 //   pair event counts -> scan -> per-node offsets
 //   k_node_write         output-parallel copy of each rule's fire times into
-//                        every node list that contains the rule
+//                        every node list that contains the rule (whole
+//                        64-event blocks, pairs found by shuffle search)
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -127,10 +130,20 @@ __global__ __launch_bounds__(256) void k_rule_nodes(RulesDev d, int mode, int wp
   }
 }
 
-__global__ void k_histogram(const int32_t* __restrict__ keys, int64_t n, int32_t* __restrict__ cnt) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
-       i += int64_t(gridDim.x) * blockDim.x)
-    atomicAdd(&cnt[keys[i]], 1);
+// nt_off[n] = first position of node n in the node-sorted pairs (n <= N):
+// a lower bound per node, no atomics (a histogram of sorted keys would put
+// every lane of a wave on the same counter)
+__global__ void k_node_bounds(const uint32_t* __restrict__ keys, int64_t n, int32_t N,
+                              int64_t* __restrict__ nt_off) {
+  const int64_t v = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (v > N) return;
+  int64_t lo = 0, hi = n;  // first index with keys[i] >= v
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (int64_t(keys[mid]) < v) lo = mid + 1;
+    else hi = mid;
+  }
+  nt_off[v] = lo;
 }
 
 __global__ void k_pair_events(const int32_t* __restrict__ nt_rule, int64_t nnz,
@@ -163,49 +176,114 @@ __device__ __forceinline__ int64_t search_le(const int64_t* __restrict__ off, in
   return lo;
 }
 
-__global__ void k_pair_block_map(const int64_t* __restrict__ pair_pos, int64_t nnz, int64_t nblocks,
-                                 int64_t* __restrict__ block_pair) {
+// first pair touched by each kNodeTask-event output task
+__global__ void k_pair_block_map(const int64_t* __restrict__ pair_pos, int64_t nnz, int64_t ntasks,
+                                 int64_t* __restrict__ task_pair) {
   int64_t b = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (b > nblocks) return;
-  block_pair[b] = b == nblocks ? nnz - 1 : search_le(pair_pos, 0, nnz - 1, b * int64_t(kWriteChunk));
+  if (b > ntasks) return;
+  task_pair[b] = b == ntasks ? nnz - 1 : search_le(pair_pos, 0, nnz - 1, b * int64_t(kNodeTask));
 }
 
-constexpr int kStride = kWritePerThread + 1;
+constexpr int kNodeUnroll = 8;
 
-__global__ __launch_bounds__(kWriteThreads) void k_node_write(
+__device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
+  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), i));
+  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v) >> 32)), i));
+  return int64_t((uint64_t(hi) << 32) | lo);
+}
+
+// Per-node lists: node event e copies fire k of the rule of its (node, rule)
+// pair.  Waves take kNodeTask-event output tasks; a wave keeps 64 consecutive
+// pairs in registers (lane i: pair jw + i, its output start, end, rule and
+// the rule's fire-list start) and fills its task in aligned 64-event blocks:
+// lane l finds the pair of event b + l by a 6-step shuffle search, gathers the
+// fire time (rule lists are re-read once per node of the rule: L2/MALL hits)
+// and the block is stored whole (8-B times, 4-B rule indices).  kNodeUnroll
+// blocks per round keep that many independent searches and gathers in flight.
+// (A wave-uniform walk over the pairs instead of the search measured 1.5x
+// slower: ~10 fires per pair make the per-pair readlane chain the bottleneck.)
+template <int V>
+__global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ pair_pos, const int32_t* __restrict__ nt_rule,
-    const int64_t* __restrict__ block_pair, const int64_t* __restrict__ rule_off,
-    const int64_t* __restrict__ times, int64_t En, int64_t* __restrict__ out_time,
+    const int64_t* __restrict__ task_pair, const int64_t* __restrict__ rule_off,
+    const int64_t* __restrict__ times, int64_t En, int64_t nnz, int64_t* __restrict__ out_time,
     int32_t* __restrict__ out_rule) {
-  __shared__ int64_t st_t[kWriteThreads * kStride];
-  __shared__ int32_t st_r[kWriteThreads * kStride];
-  const int64_t B0 = int64_t(blockIdx.x) * kWriteChunk;
-  int64_t i = B0 + int64_t(threadIdx.x) * kWritePerThread;
-  if (i < En) {
-    int64_t p = search_le(pair_pos, block_pair[blockIdx.x], block_pair[blockIdx.x + 1], i);
-    int64_t k = i - pair_pos[p];
-    int64_t n = pair_pos[p + 1] - pair_pos[p];
-    int32_t r = nt_rule[p];
-    const int64_t* src = times + rule_off[r];
-    for (int q = 0; q < kWritePerThread && i < En; q++, i++, k++) {
-      while (k >= n) {
-        p++;
-        k = 0;
-        n = pair_pos[p + 1] - pair_pos[p];
-        r = nt_rule[p];
-        src = times + rule_off[r];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t ntasks = (En + kNodeTask - 1) / kNodeTask;
+  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x >> 6);
+  for (int64_t t = int64_t(blockIdx.x) * (blockDim.x >> 6) + wave; t < ntasks; t += nwaves) {
+    const int64_t B0 = t * kNodeTask;
+    const int64_t B1 = En - B0 < kNodeTask ? En : B0 + kNodeTask;
+    const int64_t jend = task_pair[t + 1] + 1;  // pairs this task can touch
+    int64_t jw = task_pair[t];
+    int64_t dst = INT64_MAX, dend = INT64_MAX, src = 0;
+    int32_t rr = 0;
+    auto load = [&]() {
+      const int64_t p = jw + lane;
+      if (p < jend) {
+        dst = pair_pos[p];
+        dend = pair_pos[p + 1];
+        rr = nt_rule[p];
+        src = rule_off[rr];
+      } else {
+        dst = INT64_MAX;
+        dend = INT64_MAX;
+        rr = 0;
+        src = 0;
       }
-      st_t[threadIdx.x * kStride + q] = src[k];
-      st_r[threadIdx.x * kStride + q] = r;
+    };
+    load();
+    for (int64_t b = B0; b < B1; b += 64 * kNodeUnroll) {
+      int64_t e[kNodeUnroll], val[kNodeUnroll];
+      int32_t rv[kNodeUnroll];
+      bool done[kNodeUnroll];
+#pragma unroll
+      for (int u = 0; u < kNodeUnroll; u++) {
+        e[u] = b + 64 * u + lane;
+        done[u] = e[u] >= B1;
+        val[u] = 0;
+        rv[u] = 0;
+      }
+      for (;;) {
+        const int L = 63 - __builtin_clzll(__ballot(dst != INT64_MAX));
+        const int64_t wend = rl64n(dend, L);
+        int j[kNodeUnroll];
+#pragma unroll
+        for (int u = 0; u < kNodeUnroll; u++) j[u] = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1) {
+#pragma unroll
+          for (int u = 0; u < kNodeUnroll; u++) {
+            const int64_t v = __shfl(dst, (j[u] + st) & 63, 64);
+            if (j[u] + st < 64 && v <= e[u]) j[u] += st;
+          }
+        }
+        bool pending = false;
+#pragma unroll
+        for (int u = 0; u < kNodeUnroll; u++) {
+          const int64_t jd = __shfl(dst, j[u], 64), js = __shfl(src, j[u], 64);
+          const int32_t jr = __shfl(rr, j[u], 64);
+          if (!done[u] && e[u] < wend) {
+            val[u] = (V & 1) ? js + (e[u] - jd) : times[js + (e[u] - jd)];
+            rv[u] = jr;
+            done[u] = true;
+          }
+          pending |= !done[u];
+        }
+        if (__ballot(pending) == 0) break;
+        jw += 64;  // some lane's event lies past the window's last pair
+        load();
+      }
+#pragma unroll
+      for (int u = 0; u < kNodeUnroll; u++) {
+        if (V & 2) {
+          asm volatile("" ::"v"(val[u]), "v"(rv[u]));
+        } else if (e[u] < B1) {
+          out_time[e[u]] = val[u];
+          out_rule[e[u]] = rv[u];
+        }
+      }
     }
-  }
-  __syncthreads();
-  const int64_t lim = En - B0;
-  for (int e = threadIdx.x; e < kWriteChunk; e += kWriteThreads) {
-    if (e >= lim) break;
-    int t = e / kWritePerThread, q = e % kWritePerThread;
-    out_time[B0 + e] = st_t[t * kStride + q];
-    out_rule[B0 + e] = st_r[t * kStride + q];
   }
 }
 
@@ -261,49 +339,60 @@ int validate_rules(const cg_rules_in* in) {
   return CG_OK;
 }
 
-// builds the rule->node CSR on the device; leaves rn_off/rn_nodes/pair_rule in ctx
-int rule_nodes_locked(cg_ctx* c, const cg_rules_in* in, int mode, int64_t* nnz_out) {
+// validates a host rule set and copies it into a device store
+int upload_rules(const cg_rules_in* in, RulesStore* st, hipStream_t s) {
   int rc = validate_rules(in);
   if (rc) return rc;
-  if (mode < 0 || mode > 2) return cg_fail(CG_EINVAL, "bad exclude mode");
-  const int32_t R = in->n_rules, G = in->n_groups, N = in->n_nodes;
-  const int32_t words = (N + 31) / 32;
-  if (size_t(words) * 4 > 64 * 1024) return cg_fail(CG_ERANGE, "more than 524288 nodes");
-  hipStream_t st = c->st;
+  const int32_t R = in->n_rules, G = in->n_groups;
   const int64_t n_nid = R ? in->nid_off[R] : 0, n_gid = R ? in->gid_off[R] : 0,
                 n_ex = R ? in->ex_off[R] : 0, n_gn = G ? in->group_off[G] : 0;
-  if ((rc = upload(c->d_nid_off, in->nid_off, R ? R + 1 : 0, st))) return rc;
-  if ((rc = upload(c->d_nids, in->nids, n_nid, st))) return rc;
-  if ((rc = upload(c->d_gid_off, in->gid_off, R ? R + 1 : 0, st))) return rc;
-  if ((rc = upload(c->d_gids, in->gids, n_gid, st))) return rc;
-  if ((rc = upload(c->d_ex_off, in->ex_off, R ? R + 1 : 0, st))) return rc;
-  if ((rc = upload(c->d_ex, in->ex, n_ex, st))) return rc;
-  if ((rc = upload(c->d_rule_job, in->rule_job, R, st))) return rc;
-  if ((rc = upload(c->d_job_pause, in->job_pause, in->n_jobs, st))) return rc;
-  if ((rc = upload(c->d_group_off, in->group_off, G ? G + 1 : 0, st))) return rc;
-  if ((rc = upload(c->d_group_nodes, in->group_nodes, n_gn, st))) return rc;
-  if ((rc = upload(c->d_group_exists, in->group_exists, G, st))) return rc;
+  if ((rc = upload(st->nid_off, in->nid_off, R ? R + 1 : 0, s))) return rc;
+  if ((rc = upload(st->nids, in->nids, n_nid, s))) return rc;
+  if ((rc = upload(st->gid_off, in->gid_off, R ? R + 1 : 0, s))) return rc;
+  if ((rc = upload(st->gids, in->gids, n_gid, s))) return rc;
+  if ((rc = upload(st->ex_off, in->ex_off, R ? R + 1 : 0, s))) return rc;
+  if ((rc = upload(st->ex, in->ex, n_ex, s))) return rc;
+  if ((rc = upload(st->rule_job, in->rule_job, R, s))) return rc;
+  if ((rc = upload(st->job_pause, in->job_pause, in->n_jobs, s))) return rc;
+  if ((rc = upload(st->group_off, in->group_off, G ? G + 1 : 0, s))) return rc;
+  if ((rc = upload(st->group_nodes, in->group_nodes, n_gn, s))) return rc;
+  if ((rc = upload(st->group_exists, in->group_exists, G, s))) return rc;
+  st->n_nodes = in->n_nodes;
+  st->n_groups = G;
+  st->n_rules = R;
+  st->n_jobs = in->n_jobs;
+  return cg_hip_check(hipStreamSynchronize(s), "upload rules");  // host arrays may go away
+}
+
+// builds the rule->node CSR on the device; leaves rn_off/rn_nodes/pair_rule in ctx
+int rule_nodes_locked(cg_ctx* c, const RulesStore& st, int mode, int64_t* nnz_out) {
+  if (mode < 0 || mode > 2) return cg_fail(CG_EINVAL, "bad exclude mode");
+  const int32_t R = st.n_rules, G = st.n_groups, N = st.n_nodes;
+  const int32_t words = (N + 31) / 32;
+  if (size_t(words) * 4 > 64 * 1024) return cg_fail(CG_ERANGE, "more than 524288 nodes");
+  hipStream_t s = c->st;
+  int rc;
   if ((rc = c->rn_cnt.ensure(std::max(R, 1)))) return rc;
   if ((rc = c->rn_off.ensure(R + 1))) return rc;
   if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(R))))) return rc;
-  RulesDev d{c->d_nid_off.p, c->d_nids.p, c->d_gid_off.p, c->d_gids.p, c->d_ex_off.p, c->d_ex.p,
-             c->d_rule_job.p, c->d_job_pause.p, c->d_group_off.p, c->d_group_nodes.p,
-             c->d_group_exists.p, R, G, N, std::max(words, 1)};
+  RulesDev d{st.nid_off.p, st.nids.p, st.gid_off.p, st.gids.p, st.ex_off.p, st.ex.p,
+             st.rule_job.p, st.job_pause.p, st.group_off.p, st.group_nodes.p,
+             st.group_exists.p, R, G, N, std::max(words, 1)};
   int wpb = int(std::min<size_t>(4, std::max<size_t>(1, (64 * 1024) / (size_t(d.words) * 4))));
   size_t lds = size_t(wpb) * d.words * 4;
   int grid = gridn(R, wpb, 256 * 16);
   if (R > 0)
-    hipLaunchKernelGGL(k_rule_nodes<false>, dim3(grid), dim3(64 * wpb), lds, st, d, mode, wpb,
+    hipLaunchKernelGGL(k_rule_nodes<false>, dim3(grid), dim3(64 * wpb), lds, s, d, mode, wpb,
                        c->rn_cnt.p, nullptr, nullptr, nullptr);
-  launch_scan(c->rn_cnt.p, c->rn_off.p, R, c->scan_tmp.p, st);
+  launch_scan(c->rn_cnt.p, c->rn_off.p, R, c->scan_tmp.p, s);
   int64_t nnz = 0;
-  if ((rc = cg_hip_check(hipMemcpyAsync(&nnz, c->rn_off.p + R, 8, hipMemcpyDeviceToHost, st), "nnz")))
+  if ((rc = cg_hip_check(hipMemcpyAsync(&nnz, c->rn_off.p + R, 8, hipMemcpyDeviceToHost, s), "nnz")))
     return rc;
-  if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+  if ((rc = cg_hip_check(hipStreamSynchronize(s), "sync"))) return rc;
   if ((rc = c->rn_nodes.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if ((rc = c->pair_rule.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if (R > 0 && nnz > 0)
-    hipLaunchKernelGGL(k_rule_nodes<true>, dim3(grid), dim3(64 * wpb), lds, st, d, mode, wpb,
+    hipLaunchKernelGGL(k_rule_nodes<true>, dim3(grid), dim3(64 * wpb), lds, s, d, mode, wpb,
                        nullptr, c->rn_off.p, c->rn_nodes.p, c->pair_rule.p);
   if ((rc = cg_hip_check(hipGetLastError(), "k_rule_nodes"))) return rc;
   *nnz_out = nnz;
@@ -311,17 +400,18 @@ int rule_nodes_locked(cg_ctx* c, const cg_rules_in* in, int mode, int64_t* nnz_o
 }
 
 int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
-                    const cg_rules_in* in, int mode, int64_t* n_events, int64_t* nnz_out) {
-  if (int64_t(s->n) != in->n_rules)
+                    const RulesStore& in, int mode, int64_t* n_events, int64_t* nnz_out) {
+  if (int64_t(s->n) != in.n_rules)
     return cg_fail(CG_EINVAL, "specs count != rules n_rules");
   int64_t E = 0;
   int rc = expand_device_locked(c, s, z, t0, t1, &E);
   if (rc) return rc;
   int64_t nnz = 0;
+  (void)hipEventRecord(c->pev[0], c->st);
   if ((rc = rule_nodes_locked(c, in, mode, &nnz))) return rc;
-  const int32_t N = in->n_nodes;
+  (void)hipEventRecord(c->pev[1], c->st);
+  const int32_t N = in.n_nodes;
   hipStream_t st = c->st;
-  if ((rc = c->node_cnt32.ensure(std::max(N, 1)))) return rc;
   if ((rc = c->nt_off.ensure(N + 1))) return rc;
   if ((rc = c->nt_rule.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if ((rc = c->pair_node.ensure(std::max<int64_t>(nnz, 1)))) return rc;
@@ -343,13 +433,9 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
              "radix_sort_pairs")))
       return rc;
   }
-  if ((rc = cg_hip_check(hipMemsetAsync(c->node_cnt32.p, 0, size_t(std::max(N, 1)) * 4, st), "memset")))
-    return rc;
-  if (nnz > 0)
-    hipLaunchKernelGGL(k_histogram, dim3(gridn(nnz, 256, 4096)), dim3(256), 0, st, c->pair_node.p,
-                       nnz, c->node_cnt32.p);
+  hipLaunchKernelGGL(k_node_bounds, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t*>(c->pair_node.p), nnz, N, c->nt_off.p);
   if ((rc = c->scan_tmp.ensure(std::max(scan_temp_bytes(N), scan_temp_bytes(nnz))))) return rc;
-  launch_scan(c->node_cnt32.p, c->nt_off.p, N, c->scan_tmp.p, st);
   // per-pair event counts -> positions
   if ((rc = c->rn_cnt.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if ((rc = c->pair_pos.ensure(nnz + 1))) return rc;
@@ -365,17 +451,34 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
   if ((rc = c->node_time.ensure(std::max<int64_t>(En, 1)))) return rc;
   if ((rc = c->node_rule.ensure(std::max<int64_t>(En, 1)))) return rc;
-  const int64_t nblocks = (En + kWriteChunk - 1) / kWriteChunk;
-  if ((rc = c->block_run.ensure(nblocks + 1))) return rc;
+  const int64_t ntasks = (En + kNodeTask - 1) / kNodeTask;
+  if ((rc = c->block_run.ensure(ntasks + 1))) return rc;
+  (void)hipEventRecord(c->pev[2], st);
   if (En > 0) {
-    hipLaunchKernelGGL(k_pair_block_map, dim3(gridn(nblocks + 1, 256, 1 << 30)), dim3(256), 0, st,
-                       c->pair_pos.p, nnz, nblocks, c->block_run.p);
-    hipLaunchKernelGGL(k_node_write, dim3(nblocks), dim3(kWriteThreads), 0, st, c->pair_pos.p,
-                       c->nt_rule.p, c->block_run.p, c->offsets.p, c->times.p, En, c->node_time.p,
-                       c->node_rule.p);
+    hipLaunchKernelGGL(k_pair_block_map, dim3(gridn(ntasks + 1, 256, 1 << 30)), dim3(256), 0, st,
+                       c->pair_pos.p, nnz, ntasks, c->block_run.p);
+    static const int variant = [] {  // diagnostic: 1 no gather, 2 no stores, 3 neither
+      const char* e = getenv("CG_NODE_VARIANT");
+      return e ? atoi(e) : 0;
+    }();
+#define CG_NW(V)                                                                              \
+  hipLaunchKernelGGL(k_node_write<V>, dim3(gridn(ntasks, 4, c->write_blocks)), dim3(256), 0, st, \
+                     c->pair_pos.p, c->nt_rule.p, c->block_run.p, c->offsets.p, c->times.p, En,  \
+                     nnz, c->node_time.p, c->node_rule.p)
+    switch (variant) {
+      case 1: CG_NW(1); break;
+      case 2: CG_NW(2); break;
+      case 3: CG_NW(3); break;
+      default: CG_NW(0); break;
+    }
+#undef CG_NW
   }
+  (void)hipEventRecord(c->pev[3], st);
   if ((rc = cg_hip_check(hipGetLastError(), "per-node kernels"))) return rc;
   if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+  (void)hipEventElapsedTime(&c->kt[6], c->pev[0], c->pev[1]);
+  (void)hipEventElapsedTime(&c->kt[7], c->pev[1], c->pev[2]);
+  (void)hipEventElapsedTime(&c->kt[8], c->pev[2], c->pev[3]);
   c->pn_E = En;
   c->pn_nnz = nnz;
   c->pn_N = N;
@@ -395,7 +498,8 @@ int cg_rule_nodes(cg_ctx* c, const cg_rules_in* in, int mode, int64_t* rn_off, i
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
-  if ((rc = rule_nodes_locked(c, in, mode, nnz))) return rc;
+  if ((rc = upload_rules(in, &c->rules, c->st))) return rc;
+  if ((rc = rule_nodes_locked(c, c->rules, mode, nnz))) return rc;
   if ((rc = cg_hip_check(hipStreamSynchronize(c->st), "sync"))) return rc;
   if (rn_off &&
       (rc = cg_hip_check(hipMemcpy(rn_off, c->rn_off.p, size_t(in->n_rules + 1) * 8, hipMemcpyDeviceToHost),
@@ -418,7 +522,45 @@ int cg_expand_per_node_device(cg_ctx* c, const cg_specs* s, const cg_zone* z, in
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
-  return per_node_locked(c, s, z, t0, t1, rules, mode, n_events, nnz);
+  if ((rc = upload_rules(rules, &c->rules, c->st))) return rc;
+  return per_node_locked(c, s, z, t0, t1, c->rules, mode, n_events, nnz);
+}
+
+int cg_rules_upload(cg_ctx* c, const cg_rules_in* in, cg_rules** out) {
+  if (!c || !in || !out) return cg_fail(CG_EINVAL, "cg_rules_upload: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  cg_rules* r = new cg_rules();
+  r->ctx = c;
+  if ((rc = upload_rules(in, &r->st, c->st))) {
+    r->st.release();
+    delete r;
+    return rc;
+  }
+  *out = r;
+  return CG_OK;
+}
+
+void cg_rules_free(cg_rules* r) {
+  if (!r) return;
+  (void)hipSetDevice(r->ctx->device);
+  r->st.release();
+  delete r;
+}
+
+int cg_expand_per_node_rules_device(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0,
+                                    int64_t t1, const cg_rules* rules, int mode, int64_t* n_events,
+                                    int64_t* nnz) {
+  if (!c || !s || !z || !rules || !n_events || !nnz)
+    return cg_fail(CG_EINVAL, "cg_expand_per_node_rules_device: null");
+  if (rules->ctx != c) return cg_fail(CG_EINVAL, "rule set uploaded on another context");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  return per_node_locked(c, s, z, t0, t1, rules->st, mode, n_events, nnz);
 }
 
 int cg_expand_per_node(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
@@ -429,7 +571,8 @@ int cg_expand_per_node(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
   int64_t En = 0, nnz = 0;
-  if ((rc = per_node_locked(c, s, z, t0, t1, rules, mode, &En, &nnz))) return rc;
+  if ((rc = upload_rules(rules, &c->rules, c->st))) return rc;
+  if ((rc = per_node_locked(c, s, z, t0, t1, c->rules, mode, &En, &nnz))) return rc;
   out->n_events = En;
   out->nnz = nnz;
   if (out->node_off &&
@@ -457,6 +600,29 @@ int cg_node_result_device(cg_ctx* c, const int64_t** d_node_off, const int64_t**
   if (d_time) *d_time = c->node_time.p;
   if (d_rule) *d_rule = c->node_rule.p;
   if (n_events) *n_events = c->pn_E;
+  return CG_OK;
+}
+
+int cg_node_result_copy(cg_ctx* c, int64_t* node_off, int64_t* time, int32_t* rule, int64_t cap) {
+  if (!c) return cg_fail(CG_EINVAL, "cg_node_result_copy: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  if (node_off && (rc = cg_hip_check(hipMemcpy(node_off, c->node_off.p, size_t(c->pn_N + 1) * 8,
+                                               hipMemcpyDeviceToHost), "copy node_off")))
+    return rc;
+  if (time || rule) {
+    if (cap < c->pn_E) return cg_fail(CG_ECAPACITY, "per-node buffers too small; see n_events");
+    if (c->pn_E && time &&
+        (rc = cg_hip_check(hipMemcpy(time, c->node_time.p, size_t(c->pn_E) * 8, hipMemcpyDeviceToHost),
+                           "copy time")))
+      return rc;
+    if (c->pn_E && rule &&
+        (rc = cg_hip_check(hipMemcpy(rule, c->node_rule.p, size_t(c->pn_E) * 4, hipMemcpyDeviceToHost),
+                           "copy rule")))
+      return rc;
+  }
   return CG_OK;
 }
 

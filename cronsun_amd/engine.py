@@ -46,6 +46,26 @@ class Specs:
             pass
 
 
+class DeviceRules:
+    """An uploaded rule set (cg_rules): the interned jobs/groups in HBM."""
+
+    def __init__(self, engine, handle, rules):
+        self.engine = engine
+        self._h = handle
+        self.n_rules, self.n_nodes = rules.n_rules, rules.n_nodes
+
+    def free(self):
+        if self._h:
+            lib().cg_rules_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 def _as_c_schedules(schedules):
     arr = (_lib.cg_schedule * max(len(schedules), 1))()
     for i, s in enumerate(schedules):
@@ -173,9 +193,16 @@ class Engine:
     def kernel_times(self):
         """ms per phase of the last expansion: count, scan, block map,
         write(closed form), write(walk), offsets."""
-        buf = (C.c_float * 6)()
-        k = lib().cg_last_kernel_times(self._h, buf, 6)
-        return list(buf)[:k]
+        buf = (C.c_float * 9)()
+        k = lib().cg_last_kernel_times(self._h, buf, 9)
+        return list(buf)[:min(k, 6)]
+
+    def node_kernel_times(self):
+        """ms per phase of the last per-node call: rule->node join,
+        transpose + per-node offsets, per-node write."""
+        buf = (C.c_float * 9)()
+        lib().cg_last_kernel_times(self._h, buf, 9)
+        return list(buf)[6:9]
 
     def sync(self):
         check(lib().cg_sync(self._h))
@@ -215,6 +242,29 @@ class Engine:
                                               int(t1), C.byref(rin), mode, C.byref(En),
                                               C.byref(nnz)))
         return En.value, nnz.value
+
+    def upload_rules(self, rules):
+        """A rule set resident in HBM (validated once; cg_rules_upload)."""
+        h = C.c_void_p()
+        rin = rules.to_c()
+        check(lib().cg_rules_upload(self._h, C.byref(rin), C.byref(h)))
+        return DeviceRules(self, h, rules)
+
+    def expand_per_node_rules_device(self, specs, loc, t0, t1, drules, mode=_lib.EXCLUDE_NONE):
+        En, nnz = C.c_int64(), C.c_int64()
+        check(lib().cg_expand_per_node_rules_device(self._h, specs._h, self._loc(loc).handle,
+                                                    int(t0), int(t1), drules._h, mode,
+                                                    C.byref(En), C.byref(nnz)))
+        return En.value, nnz.value
+
+    def node_result(self, n_nodes, n_events):
+        """Copy the last per-node result (node_off, time, rule) to host."""
+        node_off = np.empty(n_nodes + 1, dtype=np.int64)
+        time = np.empty(max(n_events, 1), dtype=np.int64)
+        rule = np.empty(max(n_events, 1), dtype=np.int32)
+        check(lib().cg_node_result_copy(self._h, node_off.ctypes.data, time.ctypes.data,
+                                        rule.ctypes.data, n_events))
+        return node_off, time[:n_events], rule[:n_events]
 
     def node_counts_to_device(self, d_ptr):
         check(lib().cg_node_counts_to_device(self._h, C.c_void_p(d_ptr)))

@@ -187,7 +187,9 @@ int cg_result_copy_offsets(cg_ctx* ctx, int64_t* host_offsets /* [R+1] */);
 
 /* Per-kernel device time of the last expansion (ms, HIP events on the ctx
  * stream): [0] count, [1] scan, [2] block map, [3] write (closed form),
- * [4] write (walk), [5] offsets.  n = entries written. */
+ * [4] write (walk), [5] offsets; of the last per-node call: [6] rule->node
+ * join, [7] transpose + per-node offsets, [8] per-node write.  n = entries
+ * written. */
 int cg_last_kernel_times(cg_ctx* ctx, float* ms, int n);
 
 /* --------------------------------------------- rule -> node resolution --- */
@@ -239,9 +241,23 @@ int cg_expand_per_node_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone*
 /* device pointers of the last per-node result */
 int cg_node_result_device(cg_ctx* ctx, const int64_t** d_node_off, const int64_t** d_time,
                           const int32_t** d_rule, int64_t* n_events);
+/* copy the last per-node result to host buffers (node_off [N+1]; time/rule
+ * [n_events], cap = their capacity); any pointer may be NULL */
+int cg_node_result_copy(cg_ctx* ctx, int64_t* node_off, int64_t* time, int32_t* rule, int64_t cap);
 /* per-node event counts of the last per-node result, copied to a DEVICE
  * buffer of N int64 (e.g. a torch tensor for an RCCL allgather) */
 int cg_node_counts_to_device(cg_ctx* ctx, int64_t* d_counts);
+
+/* Device-resident rule sets: a cg_rules_in validated and copied into HBM once
+ * (as specs are by cg_specs_upload), then used by any number of per-node
+ * expansions on the same ctx without re-upload.  Same resolution as
+ * cg_expand_per_node_device (job.go:591-630 / web/job.go:222-257). */
+typedef struct cg_rules cg_rules;
+int cg_rules_upload(cg_ctx* ctx, const cg_rules_in* rules, cg_rules** out);
+void cg_rules_free(cg_rules* rules);
+int cg_expand_per_node_rules_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z,
+                                    int64_t t0, int64_t t1, const cg_rules* rules, int mode,
+                                    int64_t* n_events, int64_t* nnz);
 
 /* rule -> node CSR only (GPU join), host output */
 int cg_rule_nodes(cg_ctx* ctx, const cg_rules_in* rules, int mode, int64_t* rn_off /*[R+1]*/,

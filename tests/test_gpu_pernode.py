@@ -92,3 +92,21 @@ def test_per_node_config3_scale_properties(eng):
     for n in np.random.default_rng(1).choice(rin.n_nodes, 50, replace=False):
         r = rule[node_off[n]:node_off[n + 1]]
         assert (np.diff(r) >= 0).all()
+
+
+def test_device_resident_rules_same_result(eng):
+    """cg_rules_upload + cg_expand_per_node_rules_device == the host-array path."""
+    rin = synth.multi_rule_jobs(200, seed=31)
+    specs = synth.spec_mix(rin.n_rules, seed=8, mix=synth.MIX_LIGHT)
+    arr, status = cron.parse_batch(specs)
+    sp = eng.upload_c(arr, rin.n_rules)
+    t0, t1 = synth.T0_2026, synth.T0_2026 + DAY
+    for mode in (_lib.EXCLUDE_NONE, _lib.EXCLUDE_RULE, _lib.EXCLUDE_CUMULATIVE):
+        node_off, time, rule = eng.expand_per_node(sp, None, t0, t1, rin, mode)
+        drules = eng.upload_rules(rin)
+        for _ in range(2):  # reusable without re-upload
+            En, nnz = eng.expand_per_node_rules_device(sp, None, t0, t1, drules, mode)
+            o2, t2, r2 = eng.node_result(rin.n_nodes, En)
+            assert np.array_equal(o2, node_off) and np.array_equal(t2, time)
+            assert np.array_equal(r2, rule)
+        drules.free()
