@@ -87,7 +87,7 @@ struct cg_ctx {
   int64_t last_E = 0, last_R = 0, last_G = 0;
 
   // per-node buffers
-  DBuf<int64_t> rn_off, rn_cnt64, pair_pos, node_off, node_time, nt_off;
+  DBuf<int64_t> rn_off, rn_cnt64, pair_pos, pair_src, node_off, node_time, nt_off;
   DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule;
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   DBuf<char> pn_tmp;
@@ -98,7 +98,7 @@ struct cg_ctx {
     run_anchor.release(); run_off.release(); offsets.release(); times.release();
     block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
     run_dmask.release(); scan_tmp.release(); stuck.release();
-    rn_off.release(); rn_cnt64.release(); pair_pos.release(); node_off.release();
+    rn_off.release(); rn_cnt64.release(); pair_pos.release(); pair_src.release(); node_off.release();
     node_time.release(); nt_off.release(); rn_cnt.release(); rn_nodes.release();
     pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();
     rules.release(); pn_tmp.release();

@@ -146,12 +146,16 @@ __global__ void k_node_bounds(const uint32_t* __restrict__ keys, int64_t n, int3
   nt_off[v] = lo;
 }
 
+// per (node, rule) pair: its event count and its rule's fire-list start
 __global__ void k_pair_events(const int32_t* __restrict__ nt_rule, int64_t nnz,
-                              const int64_t* __restrict__ rule_off, int32_t* __restrict__ ev) {
+                              const int64_t* __restrict__ rule_off, int32_t* __restrict__ ev,
+                              int64_t* __restrict__ src) {
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < nnz;
        i += int64_t(gridDim.x) * blockDim.x) {
-    int32_t r = nt_rule[i];
-    ev[i] = int32_t(rule_off[r + 1] - rule_off[r]);
+    const int32_t r = nt_rule[i];
+    const int64_t a = rule_off[r];
+    ev[i] = int32_t(rule_off[r + 1] - a);
+    src[i] = a;
   }
 }
 
@@ -184,7 +188,10 @@ __global__ void k_pair_block_map(const int64_t* __restrict__ pair_pos, int64_t n
   task_pair[b] = b == ntasks ? nnz - 1 : search_le(pair_pos, 0, nnz - 1, b * int64_t(kNodeTask));
 }
 
-constexpr int kNodeUnroll = 8;
+#ifndef CG_NODE_UNROLL
+#define CG_NODE_UNROLL 1
+#endif
+constexpr int kNodeUnroll = CG_NODE_UNROLL;
 
 __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
   const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), i));
@@ -205,7 +212,7 @@ __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ pair_pos, const int32_t* __restrict__ nt_rule,
-    const int64_t* __restrict__ task_pair, const int64_t* __restrict__ rule_off,
+    const int64_t* __restrict__ task_pair, const int64_t* __restrict__ pair_src,
     const int64_t* __restrict__ times, int64_t En, int64_t nnz, int64_t* __restrict__ out_time,
     int32_t* __restrict__ out_rule) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -216,22 +223,44 @@ __global__ __launch_bounds__(256) void k_node_write(
     const int64_t B1 = En - B0 < kNodeTask ? En : B0 + kNodeTask;
     const int64_t jend = task_pair[t + 1] + 1;  // pairs this task can touch
     int64_t jw = task_pair[t];
-    int64_t dst = INT64_MAX, dend = INT64_MAX, src = 0;
+    // lane i: pair jw + i as (output start - B0) clamped to int32, and the
+    // fire-list shift delta = rule list start - output start (event e of the
+    // pair reads times[e + delta]): 3 shuffles per event instead of 5, and
+    // 32-bit search steps
+    int32_t dst = INT32_MAX;
+    int64_t delta = 0, dend = INT64_MAX;
     int32_t rr = 0;
-    auto load = [&]() {
-      const int64_t p = jw + lane;
+    // the next window's raw loads are issued one window ahead
+    int64_t n_d = INT64_MAX, n_dend = INT64_MAX, n_src = 0;
+    int32_t n_r = 0;
+    auto fetch = [&](int64_t base) {
+      const int64_t p = base + lane;
       if (p < jend) {
-        dst = pair_pos[p];
-        dend = pair_pos[p + 1];
-        rr = nt_rule[p];
-        src = rule_off[rr];
+        n_d = pair_pos[p];
+        n_dend = pair_pos[p + 1];
+        n_r = nt_rule[p];
+        n_src = pair_src[p];
       } else {
-        dst = INT64_MAX;
-        dend = INT64_MAX;
-        rr = 0;
-        src = 0;
+        n_d = INT64_MAX;
       }
     };
+    auto load = [&]() {  // window jw from the prefetched loads, then prefetch jw + 64
+      if (n_d != INT64_MAX) {
+        dend = n_dend;
+        rr = n_r;
+        delta = n_src - n_d;
+        dst = int32_t(n_d - B0 < int64_t(INT32_MAX)
+                          ? (n_d - B0 > INT32_MIN ? n_d - B0 : INT32_MIN + 1)
+                          : INT32_MAX - 1);
+      } else {
+        dst = INT32_MAX;
+        dend = INT64_MAX;
+        rr = 0;
+        delta = 0;
+      }
+      fetch(jw + 64);
+    };
+    fetch(jw);
     load();
     for (int64_t b = B0; b < B1; b += 64 * kNodeUnroll) {
       int64_t e[kNodeUnroll], val[kNodeUnroll];
@@ -245,7 +274,7 @@ __global__ __launch_bounds__(256) void k_node_write(
         rv[u] = 0;
       }
       for (;;) {
-        const int L = 63 - __builtin_clzll(__ballot(dst != INT64_MAX));
+        const int L = 63 - __builtin_clzll(__ballot(dst != INT32_MAX));
         const int64_t wend = rl64n(dend, L);
         int j[kNodeUnroll];
 #pragma unroll
@@ -254,17 +283,17 @@ __global__ __launch_bounds__(256) void k_node_write(
         for (int st = 32; st > 0; st >>= 1) {
 #pragma unroll
           for (int u = 0; u < kNodeUnroll; u++) {
-            const int64_t v = __shfl(dst, (j[u] + st) & 63, 64);
-            if (j[u] + st < 64 && v <= e[u]) j[u] += st;
+            const int32_t v = __shfl(dst, (j[u] + st) & 63, 64);
+            if (j[u] + st < 64 && int64_t(v) <= e[u] - B0) j[u] += st;
           }
         }
         bool pending = false;
 #pragma unroll
         for (int u = 0; u < kNodeUnroll; u++) {
-          const int64_t jd = __shfl(dst, j[u], 64), js = __shfl(src, j[u], 64);
+          const int64_t jdelta = __shfl(delta, j[u], 64);
           const int32_t jr = __shfl(rr, j[u], 64);
           if (!done[u] && e[u] < wend) {
-            val[u] = (V & 1) ? js + (e[u] - jd) : times[js + (e[u] - jd)];
+            val[u] = (V & 1) ? e[u] + jdelta : times[e[u] + jdelta];
             rv[u] = jr;
             done[u] = true;
           }
@@ -439,9 +468,10 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   // per-pair event counts -> positions
   if ((rc = c->rn_cnt.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if ((rc = c->pair_pos.ensure(nnz + 1))) return rc;
+  if ((rc = c->pair_src.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if (nnz > 0)
     hipLaunchKernelGGL(k_pair_events, dim3(gridn(nnz, 256, 4096)), dim3(256), 0, st, c->nt_rule.p,
-                       nnz, c->offsets.p, c->rn_cnt.p);
+                       nnz, c->offsets.p, c->rn_cnt.p, c->pair_src.p);
   launch_scan(c->rn_cnt.p, c->pair_pos.p, nnz, c->scan_tmp.p, st);
   hipLaunchKernelGGL(k_node_offsets, dim3(gridn(N + 1, 256, 1 << 30)), dim3(256), 0, st,
                      c->nt_off.p, c->pair_pos.p, N, c->node_off.p);
@@ -461,9 +491,14 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
       const char* e = getenv("CG_NODE_VARIANT");
       return e ? atoi(e) : 0;
     }();
+    static const int per_cu = [] {  // persistent grid: blocks of 4 waves per CU
+      const char* e = getenv("CG_NODE_BLOCKS_PER_CU");
+      return e ? std::max(1, atoi(e)) : 8;
+    }();
+    const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
 #define CG_NW(V)                                                                              \
-  hipLaunchKernelGGL(k_node_write<V>, dim3(gridn(ntasks, 4, c->write_blocks)), dim3(256), 0, st, \
-                     c->pair_pos.p, c->nt_rule.p, c->block_run.p, c->offsets.p, c->times.p, En,  \
+  hipLaunchKernelGGL(k_node_write<V>, dim3(gridn(ntasks, 4, nw_blocks)), dim3(256), 0, st,      \
+                     c->pair_pos.p, c->nt_rule.p, c->block_run.p, c->pair_src.p, c->times.p, En, \
                      nnz, c->node_time.p, c->node_rule.p)
     switch (variant) {
       case 1: CG_NW(1); break;
