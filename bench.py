@@ -75,9 +75,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    # RCCL ("nccl") in production; CG_DIST_BACKEND=gloo rehearses the N > 1
+    # path with several ranks sharing fewer GPUs (collectives on host tensors)
+    backend = os.environ.get("CG_DIST_BACKEND", "nccl")
+    ndev = max(torch.cuda.device_count(), 1)
     if world > 1:
+        local = local % ndev
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group(backend)
 
     from cronsun_amd import cron, shard, synth
     from cronsun_amd.engine import Engine
@@ -120,7 +125,8 @@ def main():
             dist.barrier()
 
     dev = torch.device("cuda", local)
-    tot = torch.zeros(world, dtype=torch.int64, device=dev)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # collective tensors
+    tot = torch.zeros(world, dtype=torch.int64, device=cdev)
     node_counts = torch.zeros(n_nodes, dtype=torch.int64, device=dev) if wl == "pernode" else None
     last = {}
 
@@ -131,12 +137,12 @@ def main():
             if world > 1:
                 # per-node offsets of every rank's slice (RCCL allgather of N int64)
                 eng.node_counts_to_device(node_counts.data_ptr())
-                shard.node_offsets(node_counts, dist)
+                shard.node_offsets(node_counts.to(cdev), dist)
             return En
         E = eng.expand_device(sp, utc, t0, t1)
         if world > 1:
             # global CSR offsets of the job-ID-range shards (RCCL allgather)
-            mine = torch.tensor([E], dtype=torch.int64, device=dev)
+            mine = torch.tensor([E], dtype=torch.int64, device=cdev)
             dist.all_gather_into_tensor(tot, mine)
         return E
 
@@ -155,8 +161,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - start
 
-    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    ev = torch.tensor([E], dtype=torch.int64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    ev = torch.tensor([E], dtype=torch.int64, device=cdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(ev, op=dist.ReduceOp.SUM)
