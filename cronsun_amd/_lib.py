@@ -21,6 +21,7 @@ CG_ERANGE = -6
 CG_ENODEV = -7
 CG_EPANIC = -8
 ZERO_TIME = -62135596800
+NO_PROGRESS_TIME = -(1 << 63) + 1
 MAX_HORIZON = 366 * 86400
 
 PARSE_SECOND, PARSE_MINUTE, PARSE_HOUR, PARSE_DOM = 1, 2, 4, 8
@@ -107,6 +108,7 @@ def _declare(L):
         "cg_specs_count": ([vp], sz),
         "cg_specs_free": ([vp], None),
         "cg_next_batch": ([vp, vp, vp, vp, vp], C.c_int),
+        "cg_lock_ttl_batch": ([vp, vp, vp, vp, vp, vp, i64, vp], C.c_int),
         "cg_expand": ([vp, vp, vp, i64, i64, P(cg_csr)], C.c_int),
         "cg_expand_device": ([vp, vp, vp, i64, i64, P(i64)], C.c_int),
         "cg_result_device": ([vp, P(vp), P(vp), P(i64)], C.c_int),

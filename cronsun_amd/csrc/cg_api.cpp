@@ -428,6 +428,46 @@ int cg_next_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int64_t*
   return CG_OK;
 }
 
+// ---------------------------------------------------------- Cmd.lockTtl()
+int cg_lock_ttl_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int64_t* now,
+                      const int32_t* kind, const int64_t* avg_time_ms, int64_t lock_ttl,
+                      int64_t* ttl_out) {
+  if (!c || !s || !z || (s->n && (!now || !kind || !avg_time_ms || !ttl_out)))
+    return cg_fail(CG_EINVAL, "cg_lock_ttl_batch: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  const int64_t n = int64_t(s->n);
+  if (n == 0) return CG_OK;
+  int64_t lo = now[0], hi = now[0];
+  for (int64_t i = 1; i < n; i++) {
+    lo = std::min(lo, now[i]);
+    hi = std::max(hi, now[i]);
+  }
+  if (lo < -(int64_t(1) << 45) || hi > (int64_t(1) << 45))
+    return cg_fail(CG_ERANGE, "input time outside +-1.1M years");
+  const int64_t kDay = 86400;
+  // prev may be the zero time (no fire within five years), and Next(prev) then
+  // walks from year 1; otherwise the two walks end within ~12 years of now.
+  Plan plan;
+  plan.table = build_table(z->rules, std::min(lo, int64_t(CG_ZERO_TIME)) - 64 * kDay,
+                           hi + (12 * 366 + 64) * kDay);
+  PlanArgs pa;
+  int rc = upload_plan(c, plan, 0, 0, &pa);
+  if (rc) return rc;
+  if ((rc = c->nb_in.ensure(n)) || (rc = c->nb_out.ensure(n)) || (rc = c->lt_avg.ensure(n)) ||
+      (rc = c->lt_kind.ensure(n)))
+    return rc;
+  HIPCHK(hipMemcpyAsync(c->nb_in.p, now, n * 8, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipMemcpyAsync(c->lt_kind.p, kind, n * 4, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipMemcpyAsync(c->lt_avg.p, avg_time_ms, n * 8, hipMemcpyHostToDevice, c->st));
+  launch_lock_ttl(s->d, n, pa, c->nb_in.p, c->lt_kind.p, c->lt_avg.p, lock_ttl, c->nb_out.p, c->st);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ttl_out, c->nb_out.p, n * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return CG_OK;
+}
+
 }  // extern "C"
 
 // --------------------------------------------------------------- expansion

@@ -79,8 +79,8 @@ struct cg_ctx {
   DBuf<char> plan_dev;
 
   // expansion buffers
-  DBuf<int64_t> run_anchor, run_off, offsets, times, block_run, nb_in, nb_out;
-  DBuf<int32_t> run_count;
+  DBuf<int64_t> run_anchor, run_off, offsets, times, block_run, nb_in, nb_out, lt_avg;
+  DBuf<int32_t> run_count, lt_kind;
   DBuf<uint32_t> run_dmask;
   DBuf<char> scan_tmp;
   DBuf<unsigned long long> stuck;
@@ -97,6 +97,7 @@ struct cg_ctx {
     plan_dev.release();
     run_anchor.release(); run_off.release(); offsets.release(); times.release();
     block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
+    lt_avg.release(); lt_kind.release();
     run_dmask.release(); scan_tmp.release(); stuck.release();
     rn_off.release(); rn_cnt64.release(); pair_pos.release(); pair_src.release(); node_off.release();
     node_time.release(); nt_off.release(); rn_cnt.release(); rn_nodes.release();

@@ -36,6 +36,9 @@ size_t plan_lds_bytes(const PlanArgs& p);
 
 void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,
                        int64_t* t_out, hipStream_t st);
+void launch_lock_ttl(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* now,
+                     const int32_t* kind, const int64_t* avg_ms, int64_t lock_ttl, int64_t* ttl,
+                     hipStream_t st);
 
 // stuck_rule: atomicMin of the first rule whose reference Next never returns
 void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run_anchor,

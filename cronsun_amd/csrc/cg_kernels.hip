@@ -91,6 +91,30 @@ __global__ __launch_bounds__(256) void k_next_batch(const DSpec* __restrict__ sp
   }
 }
 
+// Cmd.lockTtl (job.go:194-233) per rule: prev = Next(now), Next(prev), then
+// the Kind / AvgTime / LockTtl arithmetic (lock_ttl_of).
+__global__ __launch_bounds__(256) void k_lock_ttl(const DSpec* __restrict__ specs, int64_t n,
+                                                   PlanArgs p, const int64_t* __restrict__ now,
+                                                   const int32_t* __restrict__ kind,
+                                                   const int64_t* __restrict__ avg_ms,
+                                                   int64_t lock_ttl, int64_t* __restrict__ ttl) {
+  extern __shared__ __align__(16) char lds[];
+  PlanView v = stage_plan(p, lds);
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    DSpec sp = load_spec(specs + i);
+    int64_t prev, nxt;
+    if (sp.kind == KIND_EVERY) {  // constantdelay.go:25-27
+      prev = now[i] + int64_t(sp.sec);
+      nxt = prev + int64_t(sp.sec);
+    } else {
+      prev = next_exact(sp, v.z, now[i], INT64_MAX);
+      nxt = prev == CG_NO_PROGRESS ? prev : next_exact(sp, v.z, prev, INT64_MAX);
+    }
+    ttl[i] = lock_ttl_of(prev, nxt, kind[i], avg_ms[i], lock_ttl);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, int64_t R,
                                                 PlanArgs p, int64_t* __restrict__ run_anchor,
                                                 int32_t* __restrict__ run_count,
@@ -807,6 +831,14 @@ void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const i
   if (n <= 0) return;
   hipLaunchKernelGGL(k_next_batch, dim3(grid_for(n, 256, 256 * 16)), dim3(256),
                      plan_lds_bytes(p), st, specs, n, p, t_in, t_out);
+}
+
+void launch_lock_ttl(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* now,
+                     const int32_t* kind, const int64_t* avg_ms, int64_t lock_ttl, int64_t* ttl,
+                     hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_lock_ttl, dim3(grid_for(n, 256, 256 * 16)), dim3(256), plan_lds_bytes(p),
+                     st, specs, n, p, now, kind, avg_ms, lock_ttl, ttl);
 }
 
 void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run_anchor,

@@ -341,4 +341,38 @@ CG_HD int32_t select64(uint64_t m, uint32_t i) {
   return pos;
 }
 
+// ---- Cmd.lockTtl (job.go:194-233) ----
+// Job kinds, job.go:30-34.
+enum { JOB_COMMON = 0, JOB_ALONE = 1, JOB_INTERVAL = 2 };
+// Maximum time.Duration in whole seconds: Sub saturates at +-(2^63-1) ns, and
+// Duration / Second truncates toward zero (time.go Sub, job.go:197).
+#define CG_SUB_SAT_SECS 9223372036LL
+
+// The lease TTL from prev = Next(now) and nxt = Next(prev) (whole seconds),
+// the job's Kind and AvgTime (ms) and conf.Config.LockTtl.  Go's int64
+// arithmetic wraps, so the adds run in uint64.  CG_NO_PROGRESS where either
+// Next never returns (the reference then never returns either).
+CG_HD int64_t lock_ttl_of(int64_t prev, int64_t nxt, int32_t kind, int64_t avg_ms,
+                          int64_t lock_ttl) {
+  if (prev == CG_NO_PROGRESS || nxt == CG_NO_PROGRESS) return CG_NO_PROGRESS;
+  const int64_t d = nxt - prev;  // both within [ZERO_TIME, 2^45]
+  int64_t ttl = d > CG_SUB_SAT_SECS ? CG_SUB_SAT_SECS : (d < -CG_SUB_SAT_SECS ? -CG_SUB_SAT_SECS : d);
+  if (ttl == 0) return 0;
+  if (kind == JOB_INTERVAL) {  // job.go:202-211
+    ttl -= 2;
+    if (ttl > lock_ttl) ttl = lock_ttl;
+    if (ttl < 1) ttl = 1;
+    return ttl;
+  }
+  // job.go:213-216.  Both operands are int64 (1e3 is an untyped constant), so
+  // AvgTime/1e3 - cost*1e3 is cost - 1000*cost: the round-up fires only for a
+  // negative cost.
+  int64_t cost = avg_ms / 1000;
+  if (int64_t(uint64_t(cost) - uint64_t(cost) * 1000u) > 0) cost = int64_t(uint64_t(cost) + 1u);
+  if (ttl >= cost) ttl = int64_t(uint64_t(ttl) - uint64_t(cost));  // job.go:219-221
+  if (ttl > lock_ttl) ttl = lock_ttl;
+  if (ttl < 2) ttl = 2;  // job.go:227-230
+  return ttl;
+}
+
 }  // namespace cg

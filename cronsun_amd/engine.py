@@ -3,6 +3,8 @@ seen from Python.  Wraps a cg_ctx (one HIP device + stream + HBM buffers).
 
   Engine.upload(schedules)                  -> Specs (SoA packed in HBM)
   Engine.next_batch(specs, loc, t)          Schedule.Next for every rule
+  Engine.lock_ttl_batch(specs, loc, now, kind, avg_time_ms, lock_ttl)
+                                            Cmd.lockTtl for every rule
   Engine.expand(specs, loc, t0, t1)         rule-major CSR of fire times
   Engine.expand_device(specs, loc, t0, t1)  same, left in HBM (bench)
   Engine.expand_per_node(specs, loc, t0, t1, rules, mode)
@@ -160,6 +162,21 @@ class Engine:
         out = np.empty_like(t)
         check(lib().cg_next_batch(self._h, sp._h, self._loc(loc).handle, t.ctypes.data,
                                   out.ctypes.data))
+        return out
+
+    def lock_ttl_batch(self, specs, loc, now, kind, avg_time_ms, lock_ttl=300):
+        """Cmd.lockTtl (job.go:194-233) per rule at time now[i] (scalar or
+        per rule): the lease TTL in seconds, 0 for a rule that never fires.
+        kind = Job.Kind, avg_time_ms = Job.AvgTime, lock_ttl = conf LockTtl."""
+        sp = self._specs(specs)
+        n = sp.n
+        t = np.ascontiguousarray(np.broadcast_to(np.asarray(now, dtype=np.int64), (n,)))
+        k = np.ascontiguousarray(np.broadcast_to(np.asarray(kind, dtype=np.int32), (n,)))
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(avg_time_ms, dtype=np.int64), (n,)))
+        out = np.empty(n, dtype=np.int64)
+        check(lib().cg_lock_ttl_batch(self._h, sp._h, self._loc(loc).handle, t.ctypes.data,
+                                      k.ctypes.data, a.ctypes.data, int(lock_ttl),
+                                      out.ctypes.data))
         return out
 
     # -------------------------------------------------------- expansion

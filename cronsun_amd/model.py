@@ -6,6 +6,7 @@ libcronsun_gpu.so (cg_jobset_*).
   Job.Cmds(nid, groups)            job.go:591-614  (ExcludeNodeIDs is a no-op there)
   Job.IsRunOn(nid, groups)         job.go:616-630
   Job.GetJobNodes(groups)          web/job.go:222-257 (cumulative excludes)
+  JobSet.lock_ttls(now, loc)       Cmd.lockTtl (job.go:194-233) for every rule
   JobSet(jobs, groups)             all jobs interned at once -> RulesIn for the
                                    GPU per-node expansion (node/node.go:121-158
                                    for every node at once)
@@ -77,6 +78,7 @@ class Job:
     Retry: int = 0
     Interval: int = 0
     Kind: int = KindCommon
+    AvgTime: int = 0  # ms, job.go:62 (updated by Job.avgTime, job.go:579-589)
 
     def ValidRules(self):  # job.go:683-690
         for r in self.Rules:
@@ -177,6 +179,16 @@ class JobSet:
         out = np.zeros(cap, dtype=np.int32)
         k = check(lib().cg_jobset_job_nodes(self._h, job, out.ctypes.data, cap))
         return [self.node_id(int(x)) for x in out[:min(k, cap)]]
+
+    def lock_ttls(self, now, loc=None, lock_ttl=300, engine=None):
+        """Cmd.lockTtl for every (job, rule) Cmd at time `now` (unix seconds):
+        the etcd lease TTL newLock would take (job.go:235-241), 0 for a rule
+        that never fires.  lock_ttl = conf.Config.LockTtl."""
+        from .engine import default_engine
+        eng = engine or default_engine()
+        kind = np.array([self.jobs[j].Kind for j in self.rule_job], dtype=np.int32)
+        avg = np.array([self.jobs[j].AvgTime for j in self.rule_job], dtype=np.int64)
+        return eng.lock_ttl_batch(self.schedules(), loc, now, kind, avg, lock_ttl)
 
     def schedules(self):
         """Parsed schedules in rule order (JobRule.Valid on each)."""

@@ -151,10 +151,31 @@ void cg_specs_free(cg_specs* specs);
 /* --------------------------------------------------------- Next() ------ */
 /* out[i] = Schedule.Next(t_in[i]) for rule i, evaluated in zone z
  * (spec.go:55-145, constantdelay.go:25-27).  Host arrays of n = rule count.
- * Never-firing specs give CG_ZERO_TIME.  Replaces per-entry calls in
+ * Never-firing specs give CG_ZERO_TIME; a rule whose Next never returns
+ * (AddDate stuck on a skipped local day) gives CG_NO_PROGRESS_TIME.  Replaces per-entry calls in
  * Cron.run (cron.go:212-215, 242-243) and Cmd.lockTtl (job.go:196-197). */
 int cg_next_batch(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, const int64_t* t_in,
                   int64_t* t_out);
+
+/* ---------------------------------------------------- Cmd.lockTtl() ---- */
+/* ttl_out[i] = Cmd.lockTtl() (job.go:194-233) for rule i at time now[i]:
+ *   prev = Next(now); ttl = Next(prev).Sub(prev) / Second (saturating);
+ *   ttl == 0 -> 0 (lock() treats the rule as invalid, job.go:246-248);
+ *   kind[i] == CG_JOB_INTERVAL -> clamp(ttl - 2, 1, lock_ttl);
+ *   otherwise ttl -= cost when ttl >= cost, cost = avg_time_ms[i] / 1e3 in
+ *   Go int64 arithmetic (so the ceiling at job.go:214 only fires for a
+ *   negative AvgTime), then clamp to [2, lock_ttl].
+ * kind = Job.Kind (job.go:30-34), avg_time_ms = Job.AvgTime,
+ * lock_ttl = conf.Config.LockTtl (conf.go:136-138 defaults it to 300).
+ * A rule whose Next never returns gets CG_NO_PROGRESS_TIME.  Host arrays of
+ * n = rule count.  Replaces the per-Cmd call in newLock (job.go:235-241). */
+#define CG_JOB_COMMON 0
+#define CG_JOB_ALONE 1
+#define CG_JOB_INTERVAL 2
+#define CG_NO_PROGRESS_TIME (INT64_MIN + 1)
+int cg_lock_ttl_batch(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, const int64_t* now,
+                      const int32_t* kind, const int64_t* avg_time_ms, int64_t lock_ttl,
+                      int64_t* ttl_out);
 
 /* --------------------------------------------------------- expansion --- */
 /* Fire times of every rule over (t0, t1]: for each rule,

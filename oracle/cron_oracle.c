@@ -1290,3 +1290,47 @@ int32_t or_job_nodes(const or_jobset *js, int32_t job, int32_t *out, int32_t cap
     free(ex.v);
     return cnt;
 }
+
+/* ------------------------------------------------------------------------ */
+/* job.go:194-233  Cmd.lockTtl                                              */
+/* ------------------------------------------------------------------------ */
+
+/* t.Sub(u) for whole-second instants (Next results carry nsec 0): Go forms
+ * d = (t.sec-u.sec)*Second + (t.nsec-u.nsec) in wrapping int64 and keeps it
+ * when u.Add(d) == t, else saturates to minDuration / maxDuration. */
+static int64_t go_sub(int64_t t, int32_t tn, int64_t u, int32_t un) {
+    uint64_t d = (uint64_t)(t - u) * (uint64_t)NS_PER_SEC + (uint64_t)(int64_t)(tn - un);
+    int64_t di = (int64_t)d;
+    /* u.Add(di): seconds and nanoseconds of u + di, compared with t */
+    int64_t s = u + floordiv(di, NS_PER_SEC);
+    int64_t ns = (int64_t)un + (di - floordiv(di, NS_PER_SEC) * NS_PER_SEC);
+    if (ns >= NS_PER_SEC) { s++; ns -= NS_PER_SEC; }
+    if (s == t && ns == tn) return di;
+    return (t < u || (t == u && tn < un)) ? INT64_MIN : INT64_MAX;
+}
+
+int64_t or_lock_ttl(const or_sched *s, int64_t now, int32_t now_nsec,
+                    const or_loc *l, int kind, int64_t avg_time,
+                    int64_t lock_ttl) {
+    int64_t prev = or_sched_next(s, now, now_nsec, l);
+    if (prev == OR_NO_PROGRESS) return OR_NO_PROGRESS;
+    int64_t nxt = or_sched_next(s, prev, 0, l);
+    if (nxt == OR_NO_PROGRESS) return OR_NO_PROGRESS;
+    int64_t ttl = go_sub(nxt, 0, prev, 0) / NS_PER_SEC; /* truncates toward 0 */
+    if (ttl == 0) return 0;
+    if (kind == OR_KIND_INTERVAL) {
+        ttl -= 2;
+        if (ttl > lock_ttl) ttl = lock_ttl;
+        if (ttl < 1) ttl = 1;
+        return ttl;
+    }
+    /* cost := c.Job.AvgTime / 1e3 ; if c.Job.AvgTime/1e3-cost*1e3 > 0 { cost += 1 }
+     * -- int64 operands throughout, wrapping like Go */
+    int64_t cost = avg_time / 1000;
+    int64_t lhs = (int64_t)((uint64_t)(avg_time / 1000) - (uint64_t)cost * 1000u);
+    if (lhs > 0) cost = (int64_t)((uint64_t)cost + 1u);
+    if (ttl >= cost) ttl = (int64_t)((uint64_t)ttl - (uint64_t)cost);
+    if (ttl > lock_ttl) ttl = lock_ttl;
+    if (ttl < 2) ttl = 2;
+    return ttl;
+}

@@ -158,6 +158,16 @@ int or_job_is_run_on(const or_jobset *js, int32_t job, int32_t n);
 int32_t or_job_nodes(const or_jobset *js, int32_t job, int32_t *out,
                      int32_t cap);
 
+/* Cmd.lockTtl() (job.go:194-233) with time.Now() = (now, now_nsec), the
+ * rule's schedule in loc, Job.Kind, Job.AvgTime (ms) and conf LockTtl.
+ * OR_NO_PROGRESS where a Next call never returns. */
+#define OR_KIND_COMMON 0
+#define OR_KIND_ALONE 1
+#define OR_KIND_INTERVAL 2
+int64_t or_lock_ttl(const or_sched *s, int64_t now, int32_t now_nsec,
+                    const or_loc *l, int kind, int64_t avg_time,
+                    int64_t lock_ttl);
+
 #ifdef __cplusplus
 }
 #endif

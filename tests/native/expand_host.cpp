@@ -2,28 +2,12 @@
 // closed-form iteration + WALK re-walk, exactly what k_count/k_write_cf/
 // k_write_walk run) against the oracle's literal Next loop.  Test
 // infrastructure; the GPU tests check the kernels themselves.
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
 #include <random>
-#include <string>
-#include <vector>
 
 #include "../../cronsun_amd/csrc/cg_expand.h"
-#include "../../oracle/cron_oracle.h"
+#include "host_common.h"
 
 using namespace cg;
-
-static std::vector<uint8_t> slurp(const char* p) {
-  FILE* f = fopen(p, "rb");
-  if (!f) { perror(p); exit(2); }
-  std::vector<uint8_t> d;
-  uint8_t b[4096];
-  size_t n;
-  while ((n = fread(b, 1, sizeof b, f)) > 0) d.insert(d.end(), b, b + n);
-  fclose(f);
-  return d;
-}
 
 static const char* atoms[6][16] = {
     {"*/7", "0", "5", "*/20", "15/35", "10-40/3", "7,30,45", "59", "0/15", "3-3", "0", "58-59", "0", "0", "30", "*/30"},
@@ -33,30 +17,12 @@ static const char* atoms[6][16] = {
     {"*", "?", "1", "2", "Feb", "Jan,Jul", "Apr-Oct", "*/3", "Mar", "Nov", "Dec", "*", "*", "*", "Oct", "Sep-Dec"},
     {"*", "?", "0", "1-5", "Mon", "Sun", "mon/2", "Sat,Sun", "*/2", "3", "fri-sat", "*", "*", "0", "6", "?"}};
 
-static DSpec pack(const or_sched& s) {
-  DSpec d{};
-  if (s.kind == 1) { d.kind = KIND_EVERY; d.sec = uint64_t(s.delay_ns / 1000000000LL); return d; }
-  d.sec = s.spec.second & 0x0FFFFFFFFFFFFFFFull;
-  d.min = s.spec.minute & 0x0FFFFFFFFFFFFFFFull;
-  d.hour = uint32_t(s.spec.hour & 0xFFFFFF);
-  d.dom = uint32_t(s.spec.dom & 0xFFFFFFFEu) | uint32_t(s.spec.dom >> 63);
-  d.mondow = uint32_t(s.spec.month & 0x1FFE) | (uint32_t(s.spec.dow & 0x7F) << 16) |
-             (uint32_t(s.spec.dow >> 63) << 23);
-  return d;
-}
-
 int main(int argc, char** argv) {
   const char* zone = argc > 1 ? argv[1] : "UTC";
   int nspec = argc > 2 ? atoi(argv[2]) : 400;
   ZoneRules zr;
   or_loc* ol = nullptr;
-  if (!strcmp(zone, "UTC")) { zr = zone_utc(); or_loc_utc(&ol); }
-  else {
-    auto d = slurp((std::string("tests/golden/zoneinfo/") + zone).c_str());
-    std::string e;
-    zone_from_tzif(d.data(), d.size(), &zr, &e);
-    or_loc_from_tzif(d.data(), d.size(), &ol);
-  }
+  load_zone(zone, &zr, &ol);
   std::mt19937_64 rng(argc > 3 ? strtoull(argv[3], nullptr, 10) : 777);
   std::vector<or_sched> scheds;
   std::vector<std::string> names;

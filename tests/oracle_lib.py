@@ -79,6 +79,8 @@ def lib():
     L.or_job_is_run_on.argtypes = [C.POINTER(OrJobset), i32, i32]
     L.or_job_nodes.argtypes = [C.POINTER(OrJobset), i32, C.POINTER(i32), i32]
     L.or_job_nodes.restype = i32
+    L.or_lock_ttl.argtypes = [C.POINTER(OrSched), i64, i32, vp, C.c_int, i64, i64]
+    L.or_lock_ttl.restype = i64
     _lib = L
     return L
 
@@ -131,6 +133,11 @@ def parse(spec, options=OPT_DEFAULT):
 
 def sched_next(s, t, loc, nsec=0):
     return lib().or_sched_next(C.byref(s), t, nsec, loc.h)
+
+
+def lock_ttl(s, now, loc, kind, avg_time, lock_ttl_conf, nsec=0):
+    """Cmd.lockTtl (job.go:194-233)."""
+    return lib().or_lock_ttl(C.byref(s), now, nsec, loc.h, kind, avg_time, lock_ttl_conf)
 
 
 def expand(s, t0, t1, loc):
