@@ -109,6 +109,16 @@ def _declare(L):
         "cg_specs_free": ([vp], None),
         "cg_next_batch": ([vp, vp, vp, vp, vp], C.c_int),
         "cg_lock_ttl_batch": ([vp, vp, vp, vp, vp, vp, i64, vp], C.c_int),
+        "cg_dispatcher_new": ([vp, vp, vp, i64, P(vp)], C.c_int),
+        "cg_dispatcher_free": ([vp], None),
+        "cg_dispatcher_count": ([vp], i64),
+        "cg_dispatcher_effective": ([vp, P(i64)], C.c_int),
+        "cg_dispatcher_fire": ([vp, i64, P(i64), P(i64)], C.c_int),
+        "cg_dispatcher_due": ([vp, i64, i64, vp], C.c_int),
+        "cg_dispatcher_due_device": ([vp, P(vp), P(i64)], C.c_int),
+        "cg_dispatcher_set": ([vp, vp, vp, sz, i64], C.c_int),
+        "cg_dispatcher_remove": ([vp, vp, sz], C.c_int),
+        "cg_dispatcher_snapshot": ([vp, vp, vp, vp], C.c_int),
         "cg_expand": ([vp, vp, vp, i64, i64, P(cg_csr)], C.c_int),
         "cg_expand_device": ([vp, vp, vp, i64, i64, P(i64)], C.c_int),
         "cg_result_device": ([vp, P(vp), P(vp), P(i64)], C.c_int),

@@ -33,16 +33,7 @@ int cg_hip_check(hipError_t e, const char* what) {
                  std::string(what) + ": " + hipGetErrorString(e));
 }
 
-#define HIPCHK(x)                                   \
-  do {                                              \
-    int _rc = cg_hip_check((x), #x);                \
-    if (_rc != CG_OK) return _rc;                   \
-  } while (0)
 
-struct cg_zone {
-  ZoneRules rules;
-  uint64_t serial;
-};
 
 static uint64_t next_serial() {
   static std::mutex m;
@@ -253,7 +244,9 @@ int cg_sync(cg_ctx* c) {
 }
 
 // ------------------------------------------------------------------ specs
-static int pack_spec(const cg_schedule& s, DSpec* d) {
+}  // extern "C"
+
+int pack_spec(const cg_schedule& s, DSpec* d) {
   std::memset(d, 0, sizeof *d);
   if (s.kind == 1) {
     if (s.delay_ns <= 0 || s.delay_ns % 1000000000LL != 0)
@@ -274,6 +267,8 @@ static int pack_spec(const cg_schedule& s, DSpec* d) {
               (uint32_t((s.dow >> 63) & 1u) << 23);
   return CG_OK;
 }
+
+extern "C" {
 
 static int upload_packed(cg_ctx* c, const std::vector<DSpec>& h, cg_specs** out) {
   HIPCHK(hipSetDevice(c->device));
@@ -362,6 +357,9 @@ int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* p
   const int32_t G = int32_t(plan.segs.size());
   const int32_t nd = int32_t(plan.dtab.size());
   if (G > 64) return cg_fail(CG_ERANGE, "plan has more than 64 segments (horizon too long)");
+  // plan_dev is shared by every entry point: whatever it held is gone, so the
+  // expansion's plan cache must not be trusted after this (expand re-validates)
+  c->plan_valid = false;
   // one packed upload: when | off | segs | dtab
   size_t o_when = 0, o_off = o_when + size_t(zn) * 8;
   size_t o_seg = (o_off + size_t(zn) * 4 + 15) / 16 * 16;

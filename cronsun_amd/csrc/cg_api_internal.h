@@ -13,6 +13,12 @@
 int cg_fail(int code, const std::string& msg);
 int cg_hip_check(hipError_t e, const char* what);
 
+#define HIPCHK(x)                    \
+  do {                               \
+    int _rc = cg_hip_check((x), #x); \
+    if (_rc != CG_OK) return _rc;    \
+  } while (0)
+
 // Grow-only device buffer (grows by 1.25x so repeated calls settle).
 template <class T>
 struct DBuf {
@@ -111,6 +117,11 @@ struct cg_rules {
   RulesStore st;
 };
 
+struct cg_zone {
+  cg::ZoneRules rules;
+  uint64_t serial;
+};
+
 struct cg_specs {
   cg_ctx* ctx = nullptr;
   cg::DSpec* d = nullptr;
@@ -118,6 +129,8 @@ struct cg_specs {
   bool owner = false;
 };
 
+// cg_schedule -> packed 32-byte device spec (validates @every delays)
+int pack_spec(const cg_schedule& s, cg::DSpec* d);
 int upload_plan(cg_ctx* c, const cg::Plan& plan, int64_t t0, int64_t t1, cg::PlanArgs* pa);
 int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
                          int64_t* n_events);

@@ -36,6 +36,25 @@ size_t plan_lds_bytes(const PlanArgs& p);
 
 void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,
                        int64_t* t_out, hipStream_t st);
+// GPU-resident dispatcher (cg_dispatch.cpp): one block per kDispatchTile entries
+constexpr int kDispatchTile = 4096;
+struct DispatchState {
+  unsigned long long min_key;  // byTime minimum of Next (sign-flipped; ~0 = none)
+  unsigned long long n_due;    // entries fired by the last wake
+  unsigned long long stuck;    // first entry whose Next never returns (~0 = none)
+  unsigned long long pad;
+};
+void launch_dispatch_fire(const DSpec* specs, int64_t n, const PlanArgs& p, int64_t effective,
+                          int64_t now, int64_t* next, int64_t* prev, unsigned long long* due_bits,
+                          uint32_t* tile_cnt, DispatchState* st, hipStream_t s);
+void launch_dispatch_compact(const unsigned long long* due_bits, const uint32_t* tile_cnt, int64_t n,
+                             int32_t* due, hipStream_t s);
+void launch_dispatch_place(DSpec* specs, const int64_t* idx, const DSpec* src, int64_t first,
+                           int64_t k, const PlanArgs& p, int64_t now, int64_t* next, int64_t* prev,
+                           DispatchState* st, hipStream_t s);
+void launch_dispatch_clear(const int64_t* idx, int64_t first, int64_t k, int64_t* next, int64_t* prev,
+                           hipStream_t s);
+void launch_dispatch_min(const int64_t* next, int64_t n, DispatchState* st, hipStream_t s);
 void launch_lock_ttl(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* now,
                      const int32_t* kind, const int64_t* avg_ms, int64_t lock_ttl, int64_t* ttl,
                      hipStream_t st);

@@ -115,6 +115,161 @@ __global__ __launch_bounds__(256) void k_lock_ttl(const DSpec* __restrict__ spec
   }
 }
 
+// ---- GPU-resident dispatcher (Cron.run, node/cron/cron.go:210-275) ----
+// Order key of an entry's Next under byTime (cron.go:64-79): the zero time
+// sorts after every other time; "never returns" never fires either.
+__device__ __forceinline__ unsigned long long next_key(int64_t t) {
+  return (t == CG_ZERO_TIME || t == CG_NO_PROGRESS) ? ~0ull
+                                                    : (uint64_t(t) ^ (uint64_t(1) << 63));
+}
+
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) {
+    unsigned long long u = __shfl_xor(v, o, 64);
+    v = u < v ? u : v;
+  }
+  return v;
+}
+
+// One wake of the run loop (cron.go:234-244): every entry whose Next equals
+// `effective` is due: Prev = Next, Next = Schedule.Next(now).  Fused with the
+// next wake's byTime minimum (cron.go:220-230) over the updated Nexts.  One
+// block per kDispatchTile entries; a due bitmap word per 64 entries and a due
+// count per tile feed the ordered compaction.
+__global__ __launch_bounds__(256) void k_dispatch_fire(
+    const DSpec* __restrict__ specs, int64_t n, PlanArgs p, int64_t effective, int64_t now,
+    int64_t* __restrict__ next, int64_t* __restrict__ prev, unsigned long long* __restrict__ due_bits,
+    uint32_t* __restrict__ tile_cnt, DispatchState* __restrict__ st) {
+  extern __shared__ __align__(16) char lds[];
+  __shared__ unsigned long long s_min[4];
+  __shared__ uint32_t s_cnt[4];
+  PlanView v = stage_plan(p, lds);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t base = int64_t(blockIdx.x) * kDispatchTile;
+  unsigned long long kmin = ~0ull;
+  uint32_t cnt = 0;
+  for (int j = 0; j < kDispatchTile / 256; j++) {
+    const int64_t w0 = base + j * 256 + wv * 64;  // first entry of this wave's word
+    const int64_t i = w0 + lane;
+    bool due = false;
+    if (i < n) {
+      int64_t t = next[i];
+      if (t == effective) {
+        due = true;
+        const DSpec sp = load_spec(specs + i);
+        prev[i] = t;
+        t = sp.kind == KIND_EVERY ? now + int64_t(sp.sec) : next_exact(sp, v.z, now, INT64_MAX);
+        if (t == CG_NO_PROGRESS) atomicMin(&st->stuck, (unsigned long long)i);
+        next[i] = t;
+      }
+      const unsigned long long k = next_key(t);
+      kmin = k < kmin ? k : kmin;
+    }
+    const unsigned long long b = __ballot(due);
+    if (lane == 0 && w0 < n) due_bits[w0 >> 6] = b;
+    cnt += __popcll(b);
+  }
+  kmin = wave_min_u64(kmin);
+  if (lane == 0) {
+    s_min[wv] = kmin;
+    s_cnt[wv] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = s_min[0];
+    uint32_t c = s_cnt[0];
+    for (int w = 1; w < 4; w++) {
+      m = s_min[w] < m ? s_min[w] : m;
+      c += s_cnt[w];
+    }
+    tile_cnt[blockIdx.x] = c;
+    if (m != ~0ull) atomicMin(&st->min_key, m);
+    if (c) atomicAdd(&st->n_due, (unsigned long long)c);
+  }
+}
+
+// Due entry indices in ascending order: tile base = sum of the earlier tiles'
+// counts, then wave 0 expands the tile's 64 bitmap words in order.
+__global__ __launch_bounds__(256) void k_dispatch_compact(
+    const unsigned long long* __restrict__ due_bits, const uint32_t* __restrict__ tile_cnt,
+    int64_t n, int32_t* __restrict__ due) {
+  __shared__ unsigned long long s_sum[4];
+  const int64_t b = blockIdx.x;
+  if (tile_cnt[b] == 0) return;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long s = 0;
+  for (int64_t k = threadIdx.x; k < b; k += 256) s += tile_cnt[k];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) s_sum[wv] = s;
+  __syncthreads();
+  if (wv != 0) return;
+  const int64_t tile_base = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+  const int64_t w = b * (kDispatchTile / 64) + lane;
+  unsigned long long bits = w * 64 < n ? due_bits[w] : 0ull;
+  const uint32_t pc = __popcll(bits);
+  uint32_t incl = pc;
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t u = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += u;
+  }
+  int64_t o = tile_base + (incl - pc);
+  while (bits) {
+    due[o++] = int32_t(w * 64 + __builtin_ctzll(bits));
+    bits &= bits - 1;
+  }
+}
+
+// Entries (re)placed at time now (run start, cron.go:212-215; add, cron.go:246-252):
+// Next = Schedule.Next(now), Prev = zero.  idx == nullptr: entries [first, first+k).
+__global__ __launch_bounds__(256) void k_dispatch_place(
+    DSpec* __restrict__ specs, const int64_t* __restrict__ idx, const DSpec* __restrict__ src,
+    int64_t first, int64_t k, PlanArgs p, int64_t now, int64_t* __restrict__ next,
+    int64_t* __restrict__ prev, DispatchState* __restrict__ st) {
+  extern __shared__ __align__(16) char lds[];
+  PlanView v = stage_plan(p, lds);
+  for (int64_t j = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; j < k;
+       j += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = idx ? idx[j] : first + j;
+    DSpec sp;
+    if (src) {
+      sp = load_spec(src + j);
+      specs[i] = sp;
+    } else {
+      sp = load_spec(specs + i);
+    }
+    const int64_t t =
+        sp.kind == KIND_EVERY ? now + int64_t(sp.sec) : next_exact(sp, v.z, now, INT64_MAX);
+    if (t == CG_NO_PROGRESS) atomicMin(&st->stuck, (unsigned long long)i);
+    next[i] = t;
+    prev[i] = CG_ZERO_TIME;
+  }
+}
+
+// Entries removed (cron.go:254-262) or slots never filled: Next = Prev = zero,
+// which byTime sorts last and no wake ever matches.
+__global__ void k_dispatch_clear(const int64_t* __restrict__ idx, int64_t first, int64_t k,
+                                 int64_t* __restrict__ next, int64_t* __restrict__ prev) {
+  for (int64_t j = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; j < k;
+       j += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = idx ? idx[j] : first + j;
+    next[i] = CG_ZERO_TIME;
+    prev[i] = CG_ZERO_TIME;
+  }
+}
+
+// byTime minimum over all entries (after adds / removes).
+__global__ __launch_bounds__(256) void k_dispatch_min(const int64_t* __restrict__ next, int64_t n,
+                                                       DispatchState* __restrict__ st) {
+  unsigned long long m = ~0ull;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const unsigned long long k = next_key(next[i]);
+    m = k < m ? k : m;
+  }
+  m = wave_min_u64(m);
+  if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(&st->min_key, m);
+}
+
 __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, int64_t R,
                                                 PlanArgs p, int64_t* __restrict__ run_anchor,
                                                 int32_t* __restrict__ run_count,
@@ -839,6 +994,43 @@ void launch_lock_ttl(const DSpec* specs, int64_t n, const PlanArgs& p, const int
   if (n <= 0) return;
   hipLaunchKernelGGL(k_lock_ttl, dim3(grid_for(n, 256, 256 * 16)), dim3(256), plan_lds_bytes(p),
                      st, specs, n, p, now, kind, avg_ms, lock_ttl, ttl);
+}
+
+void launch_dispatch_fire(const DSpec* specs, int64_t n, const PlanArgs& p, int64_t effective,
+                          int64_t now, int64_t* next, int64_t* prev, unsigned long long* due_bits,
+                          uint32_t* tile_cnt, DispatchState* st, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t tiles = (n + kDispatchTile - 1) / kDispatchTile;
+  hipLaunchKernelGGL(k_dispatch_fire, dim3(unsigned(tiles)), dim3(256), plan_lds_bytes(p), s, specs,
+                     n, p, effective, now, next, prev, due_bits, tile_cnt, st);
+}
+
+void launch_dispatch_compact(const unsigned long long* due_bits, const uint32_t* tile_cnt, int64_t n,
+                             int32_t* due, hipStream_t s) {
+  if (n <= 0) return;
+  const int64_t tiles = (n + kDispatchTile - 1) / kDispatchTile;
+  hipLaunchKernelGGL(k_dispatch_compact, dim3(unsigned(tiles)), dim3(256), 0, s, due_bits, tile_cnt,
+                     n, due);
+}
+
+void launch_dispatch_place(DSpec* specs, const int64_t* idx, const DSpec* src, int64_t first,
+                           int64_t k, const PlanArgs& p, int64_t now, int64_t* next, int64_t* prev,
+                           DispatchState* st, hipStream_t s) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(k_dispatch_place, dim3(grid_for(k, 256, 256 * 16)), dim3(256), plan_lds_bytes(p),
+                     s, specs, idx, src, first, k, p, now, next, prev, st);
+}
+
+void launch_dispatch_clear(const int64_t* idx, int64_t first, int64_t k, int64_t* next, int64_t* prev,
+                           hipStream_t s) {
+  if (k <= 0) return;
+  hipLaunchKernelGGL(k_dispatch_clear, dim3(grid_for(k, 256, 4096)), dim3(256), 0, s, idx, first, k,
+                     next, prev);
+}
+
+void launch_dispatch_min(const int64_t* next, int64_t n, DispatchState* st, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_dispatch_min, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, next, n, st);
 }
 
 void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run_anchor,

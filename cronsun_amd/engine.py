@@ -5,6 +5,7 @@ seen from Python.  Wraps a cg_ctx (one HIP device + stream + HBM buffers).
   Engine.next_batch(specs, loc, t)          Schedule.Next for every rule
   Engine.lock_ttl_batch(specs, loc, now, kind, avg_time_ms, lock_ttl)
                                             Cmd.lockTtl for every rule
+  Engine.dispatcher(specs, loc, now)        Cron.run's entry state in HBM
   Engine.expand(specs, loc, t0, t1)         rule-major CSR of fire times
   Engine.expand_device(specs, loc, t0, t1)  same, left in HBM (bench)
   Engine.expand_per_node(specs, loc, t0, t1, rules, mode)
@@ -59,6 +60,71 @@ class DeviceRules:
     def free(self):
         if self._h:
             lib().cg_rules_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Dispatcher:
+    """Cron.run's entries (node/cron/cron.go:210-275) resident in HBM
+    (cg_dispatcher_*): slots with a schedule, Next and Prev."""
+
+    def __init__(self, engine, handle):
+        self.engine = engine
+        self._h = handle
+
+    def __len__(self):
+        return int(lib().cg_dispatcher_count(self._h))
+
+    @property
+    def effective(self):
+        """The earliest non-zero Next (ZERO_TIME: nothing can fire)."""
+        e = C.c_int64()
+        check(lib().cg_dispatcher_effective(self._h, C.byref(e)))
+        return e.value
+
+    def fire(self, now):
+        """One wake at `now` >= effective: the due slots (ascending) and the
+        next effective time."""
+        n, e = C.c_int64(), C.c_int64()
+        check(lib().cg_dispatcher_fire(self._h, int(now), C.byref(n), C.byref(e)))
+        due = np.empty(max(n.value, 1), dtype=np.int32)
+        check(lib().cg_dispatcher_due(self._h, 0, n.value, due.ctypes.data))
+        return due[:n.value], e.value
+
+    def fire_count(self, now):
+        """One wake, leaving the due list in HBM: (n_due, next effective)."""
+        n, e = C.c_int64(), C.c_int64()
+        check(lib().cg_dispatcher_fire(self._h, int(now), C.byref(n), C.byref(e)))
+        return n.value, e.value
+
+    def set(self, idx, schedules, now):
+        """Add or replace entries: slot idx[j] <- schedules[j], Next = Next(now)."""
+        ix = np.ascontiguousarray(np.atleast_1d(idx), dtype=np.int64)
+        arr = _as_c_schedules(schedules)
+        check(lib().cg_dispatcher_set(self._h, ix.ctypes.data, C.cast(arr, C.c_void_p), len(ix),
+                                      int(now)))
+
+    def remove(self, idx):
+        ix = np.ascontiguousarray(np.atleast_1d(idx), dtype=np.int64)
+        check(lib().cg_dispatcher_remove(self._h, ix.ctypes.data, len(ix)))
+
+    def snapshot(self):
+        """(next, prev, live) per slot."""
+        n = len(self)
+        nx = np.empty(max(n, 1), dtype=np.int64)
+        pv = np.empty(max(n, 1), dtype=np.int64)
+        lv = np.empty(max(n, 1), dtype=np.uint8)
+        check(lib().cg_dispatcher_snapshot(self._h, nx.ctypes.data, pv.ctypes.data, lv.ctypes.data))
+        return nx[:n], pv[:n], lv[:n].astype(bool)
+
+    def free(self):
+        if self._h:
+            lib().cg_dispatcher_free(self._h)
             self._h = None
 
     def __del__(self):
@@ -178,6 +244,13 @@ class Engine:
                                       k.ctypes.data, a.ctypes.data, int(lock_ttl),
                                       out.ctypes.data))
         return out
+
+    def dispatcher(self, specs, loc, now):
+        """Cron.run start (cron.go:212-215) over `specs` at `now`."""
+        sp = self._specs(specs)
+        h = C.c_void_p()
+        check(lib().cg_dispatcher_new(self._h, sp._h, self._loc(loc).handle, int(now), C.byref(h)))
+        return Dispatcher(self, h)
 
     # -------------------------------------------------------- expansion
     def expand(self, specs, loc, t0, t1):
@@ -303,4 +376,4 @@ def device_count():
     return lib().cg_device_count()
 
 
-__all__ = ["Engine", "Specs", "RulesIn", "default_engine", "device_count", "CgError"]
+__all__ = ["Engine", "Specs", "Dispatcher", "RulesIn", "default_engine", "device_count", "CgError"]

@@ -177,6 +177,52 @@ int cg_lock_ttl_batch(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, cons
                       const int32_t* kind, const int64_t* avg_time_ms, int64_t lock_ttl,
                       int64_t* ttl_out);
 
+/* ------------------------------------------------------- dispatcher ---- */
+/* The state of Cron.run (node/cron/cron.go:210-275) resident in HBM.  Entries
+ * are slots 0..count-1 (the caller maps Entry IDs, cron.go:17-27 `indexes`,
+ * to slots).  Each slot holds a schedule, Next and Prev (unix seconds;
+ * CG_ZERO_TIME = zero time).
+ *
+ *   cg_dispatcher_new        run() start: Next = Schedule.Next(now) for every
+ *                            entry of specs (cron.go:212-215); Prev = zero.
+ *   cg_dispatcher_effective  entries[0].Next after sort.Sort(byTime)
+ *                            (cron.go:220-230): the earliest non-zero Next, or
+ *                            CG_ZERO_TIME when none (the loop then sleeps
+ *                            ten years).
+ *   cg_dispatcher_fire       the timer fired at `now` >= effective
+ *                            (cron.go:234-244): every entry whose Next ==
+ *                            effective is due; its Prev = Next and
+ *                            Next = Schedule.Next(now).  Returns the due count
+ *                            and the next effective time.
+ *   cg_dispatcher_due        the last wake's due slots, ascending (the
+ *                            reference runs them in byTime order, which is
+ *                            unordered among equal Next values).
+ *   cg_dispatcher_set        add or replace entries (cron.go:246-252,
+ *                            125-142): slot idx[j] gets schedule s[j],
+ *                            Next = Schedule.Next(now), Prev = zero.  Slots
+ *                            past the current count extend it; skipped slots
+ *                            stay empty.
+ *   cg_dispatcher_remove     DelJob (cron.go:149-164, 254-262): the slot is
+ *                            emptied and never fires.
+ *   cg_dispatcher_snapshot   Entries() (cron.go:166-174, 296-308): Next, Prev
+ *                            and liveness per slot (any pointer may be NULL).
+ * A schedule whose Next never returns (the reference loop then blocks
+ * forever) makes the call fail with CG_ERANGE naming the slot. */
+typedef struct cg_dispatcher cg_dispatcher;
+int cg_dispatcher_new(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t now,
+                      cg_dispatcher** out);
+void cg_dispatcher_free(cg_dispatcher* d);
+int64_t cg_dispatcher_count(const cg_dispatcher* d);
+int cg_dispatcher_effective(const cg_dispatcher* d, int64_t* effective);
+int cg_dispatcher_fire(cg_dispatcher* d, int64_t now, int64_t* n_due, int64_t* effective);
+int cg_dispatcher_due(const cg_dispatcher* d, int64_t first, int64_t count, int32_t* out);
+/* the due list in HBM (valid until the next call on d) */
+int cg_dispatcher_due_device(const cg_dispatcher* d, const int32_t** due, int64_t* n_due);
+int cg_dispatcher_set(cg_dispatcher* d, const int64_t* idx, const cg_schedule* s, size_t k,
+                      int64_t now);
+int cg_dispatcher_remove(cg_dispatcher* d, const int64_t* idx, size_t k);
+int cg_dispatcher_snapshot(const cg_dispatcher* d, int64_t* next, int64_t* prev, uint8_t* live);
+
 /* --------------------------------------------------------- expansion --- */
 /* Fire times of every rule over (t0, t1]: for each rule,
  *   t = t0; loop { t = Next(t); if t.IsZero() || t > t1 break; emit t }

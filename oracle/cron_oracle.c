@@ -1334,3 +1334,43 @@ int64_t or_lock_ttl(const or_sched *s, int64_t now, int32_t now_nsec,
     if (ttl < 2) ttl = 2;
     return ttl;
 }
+
+/* ------------------------------------------------------------------------ */
+/* node/cron/cron.go:210-275  Cron.run                                      */
+/* ------------------------------------------------------------------------ */
+
+void or_cron_start(or_entry *e, size_t n, int64_t now, const or_loc *l) {
+    for (size_t i = 0; i < n; i++) e[i].next = or_sched_next(e[i].s, now, 0, l);
+}
+
+/* byTime.Less: zero sorts after everything; two zeros are not less */
+static int by_time_cmp(const void *a, const void *b) {
+    const or_entry *x = (const or_entry *)a, *y = (const or_entry *)b;
+    int xl, yl;
+    if (x->next == OR_ZERO_TIME) xl = 0;
+    else if (y->next == OR_ZERO_TIME) xl = 1;
+    else xl = x->next < y->next;
+    if (y->next == OR_ZERO_TIME) yl = 0;
+    else if (x->next == OR_ZERO_TIME) yl = 1;
+    else yl = y->next < x->next;
+    return xl ? -1 : (yl ? 1 : 0);
+}
+
+int64_t or_cron_effective(or_entry *e, size_t n) {
+    if (n) qsort(e, n, sizeof *e, by_time_cmp);
+    if (n == 0 || e[0].next == OR_ZERO_TIME) return OR_ZERO_TIME;
+    return e[0].next;
+}
+
+int64_t or_cron_fire(or_entry *e, size_t n, int64_t effective, int64_t now,
+                     const or_loc *l, int32_t *due_ids) {
+    int64_t k = 0;
+    for (size_t i = 0; i < n; i++) {
+        if (e[i].next != effective) break;
+        if (due_ids) due_ids[k] = e[i].id;
+        k++;
+        e[i].prev = e[i].next;
+        e[i].next = or_sched_next(e[i].s, now, 0, l);
+    }
+    return k;
+}

@@ -12,6 +12,8 @@
  *   job.go:274-288, 591-630          JobRule.included, Job.Cmds, Job.IsRunOn
  *   group.go:111-119                 Group.Included
  *   web/job.go:222-257               Job.GetJobNodes (cumulative excludes)
+ *   job.go:194-233                   Cmd.lockTtl
+ *   node/cron/cron.go:64-79,210-244  byTime + the Cron.run wake loop
  * plus the Go standard library `time` semantics the reference relies on but
  * which are not under /root/reference (third-party boundary, Go >= 1.15
  * semantics with TZif footer support): Location.lookup, tzset (POSIX TZ
@@ -157,6 +159,24 @@ int or_job_is_run_on(const or_jobset *js, int32_t job, int32_t n);
  * Returns the count; writes at most cap node ids. */
 int32_t or_job_nodes(const or_jobset *js, int32_t job, int32_t *out,
                      int32_t cap);
+
+/* Cron.run (node/cron/cron.go:210-275), one wake at a time.  An entry is a
+ * schedule + Next + Prev + id (the caller's handle). */
+typedef struct {
+    const or_sched *s;
+    int64_t next, prev;
+    int32_t id;
+} or_entry;
+/* run() start: entry.Next = entry.Schedule.Next(now) (cron.go:212-215) */
+void or_cron_start(or_entry *e, size_t n, int64_t now, const or_loc *l);
+/* sort.Sort(byTime) (cron.go:64-79, 220) in place; returns entries[0].Next,
+ * or OR_ZERO_TIME when there are no entries or it is zero (cron.go:223-230) */
+int64_t or_cron_effective(or_entry *e, size_t n);
+/* the timer fired at `now` (cron.go:234-244): walk the sorted entries while
+ * Next == effective, Prev = Next, Next = Schedule.Next(now); writes the ids
+ * run, returns how many */
+int64_t or_cron_fire(or_entry *e, size_t n, int64_t effective, int64_t now,
+                     const or_loc *l, int32_t *due_ids);
 
 /* Cmd.lockTtl() (job.go:194-233) with time.Now() = (now, now_nsec), the
  * rule's schedule in loc, Job.Kind, Job.AvgTime (ms) and conf LockTtl.

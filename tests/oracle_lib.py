@@ -26,6 +26,11 @@ class OrSched(C.Structure):
     _fields_ = [("kind", C.c_int), ("spec", OrSpec), ("delay_ns", C.c_int64)]
 
 
+class OrEntry(C.Structure):
+    _fields_ = [("s", C.POINTER(OrSched)), ("next", C.c_int64), ("prev", C.c_int64),
+                ("id", C.c_int32)]
+
+
 class OrJobset(C.Structure):
     _fields_ = [("n_nodes", C.c_int32), ("n_groups", C.c_int32), ("n_rules", C.c_int32),
                 ("n_jobs", C.c_int32),
@@ -79,6 +84,12 @@ def lib():
     L.or_job_is_run_on.argtypes = [C.POINTER(OrJobset), i32, i32]
     L.or_job_nodes.argtypes = [C.POINTER(OrJobset), i32, C.POINTER(i32), i32]
     L.or_job_nodes.restype = i32
+    L.or_cron_start.argtypes = [C.POINTER(OrEntry), C.c_size_t, i64, vp]
+    L.or_cron_start.restype = None
+    L.or_cron_effective.argtypes = [C.POINTER(OrEntry), C.c_size_t]
+    L.or_cron_effective.restype = i64
+    L.or_cron_fire.argtypes = [C.POINTER(OrEntry), C.c_size_t, i64, i64, vp, C.POINTER(i32)]
+    L.or_cron_fire.restype = i64
     L.or_lock_ttl.argtypes = [C.POINTER(OrSched), i64, i32, vp, C.c_int, i64, i64]
     L.or_lock_ttl.restype = i64
     _lib = L
@@ -133,6 +144,60 @@ def parse(spec, options=OPT_DEFAULT):
 
 def sched_next(s, t, loc, nsec=0):
     return lib().or_sched_next(C.byref(s), t, nsec, loc.h)
+
+
+class OracleCron:
+    """Cron.run's entries driven one wake at a time (or_cron_*, cron.go:210-275).
+    Entry ids are the caller's slot numbers."""
+
+    def __init__(self, scheds, loc):
+        self.loc = loc
+        self.keep = {}
+        self.rows = []  # [sched, next, prev, id]
+        for i, sc in enumerate(scheds):
+            self.keep[i] = sc
+            self.rows.append([sc, ZERO_TIME, ZERO_TIME, i])
+
+    def _arr(self):
+        a = (OrEntry * max(len(self.rows), 1))()
+        for k, (sc, nx, pv, i) in enumerate(self.rows):
+            a[k].s = C.pointer(sc)
+            a[k].next, a[k].prev, a[k].id = nx, pv, i
+        return a
+
+    def _back(self, a):
+        self.rows = [[self.keep[a[k].id], a[k].next, a[k].prev, a[k].id]
+                     for k in range(len(self.rows))]
+
+    def start(self, now):
+        a = self._arr()
+        lib().or_cron_start(a, len(self.rows), now, self.loc.h)
+        self._back(a)
+
+    def effective(self):
+        a = self._arr()
+        e = lib().or_cron_effective(a, len(self.rows))
+        self._back(a)
+        return e
+
+    def fire(self, effective, now):
+        a = self._arr()
+        ids = (C.c_int32 * max(len(self.rows), 1))()
+        k = lib().or_cron_fire(a, len(self.rows), effective, now, self.loc.h, ids)
+        self._back(a)
+        return sorted(ids[i] for i in range(k))
+
+    def set(self, i, sc, now):
+        """add/replace (cron.go:246-252): Next = Next(now), Prev = zero"""
+        self.keep[i] = sc
+        nx = lib().or_sched_next(C.byref(sc), now, 0, self.loc.h)
+        self.rows = [r for r in self.rows if r[3] != i] + [[sc, nx, ZERO_TIME, i]]
+
+    def remove(self, i):
+        self.rows = [r for r in self.rows if r[3] != i]
+
+    def snapshot(self):
+        return {r[3]: (r[1], r[2]) for r in self.rows}
 
 
 def lock_ttl(s, now, loc, kind, avg_time, lock_ttl_conf, nsec=0):

@@ -150,3 +150,19 @@ def test_config2_scale_properties(eng):
         got = times[off[i]:off[i + 1]]
         exp = et[eo[k]:eo[k + 1]]
         assert np.array_equal(got, exp), specs[i]
+
+
+def test_plan_cache_survives_other_entry_points(eng):
+    """Next/lockTtl upload their own zone tables into the context's plan
+    buffer: a repeated expansion over the same (zone, T0, T1) must rebuild its
+    plan rather than reuse the cached one."""
+    rng = np.random.default_rng(11)
+    scheds = [cron.Parse(random_spec(rng)) for _ in range(400)]
+    ny = product_zone("America/New_York")
+    t0 = 1772900000
+    sp = eng.upload(scheds)
+    first = eng.expand(sp, ny, t0, t0 + 3 * DAY)
+    eng.next_batch(sp, product_zone("Australia/Lord_Howe"), np.full(len(scheds), t0, dtype=np.int64))
+    eng.lock_ttl_batch(sp, product_zone("Pacific/Apia"), t0, 0, 0)
+    again = eng.expand(sp, ny, t0, t0 + 3 * DAY)
+    assert np.array_equal(first[0], again[0]) and np.array_equal(first[1], again[1])
