@@ -20,6 +20,10 @@ Workloads (`--workload`, default config2 -- the headline line):
   config4  config 4 shape: 10M rules x 7 days over the job-ID-range shards of
            N GPUs (10M / N rules per rank, lighter spec mix); a step = one
            expansion per rank.  Fixed total work: `scaling` = "strong".
+  dispatch SURVEY.md §8(f)-1: Cron.run's entry table resident in HBM, 10M
+           entries of the config-2 mix per GPU; a step = one on-time wake
+           (fire every entry whose Next is the earliest, Next(now) for them,
+           next minimum, ordered due list left in HBM).
 
 Prints one JSON line (rank 0).  See DESIGN.md §Measurement for the roofline
 and CPU-baseline definitions.
@@ -62,11 +66,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["config2", "pernode", "config4"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "pernode", "config4", "dispatch"], default="config2")
     ap.add_argument("--rules", type=int, default=0, help="rules per GPU (0 = the workload's)")
     ap.add_argument("--horizon", type=int, default=0, help="seconds (0 = the workload's)")
-    ap.add_argument("--cpu-sample", type=int, default=40_000,
-                    help="rules in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=None,
+                    help="rules in the CPU-baseline sample (0 = skip; default 40k, 1M for dispatch)")
     ap.add_argument("--cpu-threads", type=int, default=0)
     args = ap.parse_args()
 
@@ -88,11 +92,18 @@ def main():
     from cronsun_amd.engine import Engine
 
     wl = args.workload
+    if args.cpu_sample is None:
+        args.cpu_sample = 1_000_000 if wl == "dispatch" else 40_000
     if wl == "config2":
         R = args.rules or 1_000_000
         H = args.horizon or 86400
         mix = synth.MIX_CONFIG2
         seed = 0x5EED + rank
+    elif wl == "dispatch":
+        R = args.rules or 10_000_000
+        H = 0
+        mix = synth.MIX_CONFIG2
+        seed = 0x5EED + 5 + rank
     elif wl == "pernode":
         R = args.rules or 1_000_000
         H = args.horizon or 3600
@@ -109,7 +120,13 @@ def main():
     t1 = t0 + H
     eng = Engine(local)
     log(f"[rank {rank}] {wl}: generating {R} rules (job-ID shard {rank})")
-    specs = synth.spec_mix(R, seed=seed, mix=mix)
+    if wl == "dispatch" and R > 1_000_000:
+        # the 1M-rule config-2 set tiled (Python generation of 10M strings
+        # takes minutes; entries are independent, so repeats change nothing)
+        base = synth.spec_mix(1_000_000, seed=seed, mix=mix)
+        specs = (base * (R // len(base) + 1))[:R]
+    else:
+        specs = synth.spec_mix(R, seed=seed, mix=mix)
     arr, status = cron.parse_batch(specs, threads=16)
     assert (status == 0).all()
     sp = eng.upload_c(arr, R)
@@ -130,7 +147,17 @@ def main():
     node_counts = torch.zeros(n_nodes, dtype=torch.int64, device=dev) if wl == "pernode" else None
     last = {}
 
+    disp = eng.dispatcher(sp, utc, t0) if wl == "dispatch" else None
+    wake = {"due": 0, "wakes": 0}
+
     def step():
+        if wl == "dispatch":
+            tw = time.perf_counter()
+            n_due, _ = disp.fire_count(disp.effective)  # an on-time wake
+            wake.setdefault("wall", []).append(time.perf_counter() - tw)
+            wake["due"] += n_due
+            wake["wakes"] += 1
+            return n_due
         if wl == "pernode":
             En, nnz = eng.expand_per_node_rules_device(sp, utc, t0, t1, drules)
             last["nnz"] = nnz
@@ -153,13 +180,17 @@ def main():
     torch.cuda.synchronize()
     start = time.perf_counter()
     kts, nkts = [], []
+    wake["due"] = wake["wakes"] = 0
+    wake["wall"] = []
     for _ in range(args.steps):
         E = step()
         kts.append(eng.kernel_times())
-        nkts.append(eng.node_kernel_times())
+        nkts.append(eng.dispatch_kernel_times() if wl == "dispatch" else eng.node_kernel_times())
+    t_loop = time.perf_counter() - start
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - start
+    wake["loop_s"], wake["tail_s"] = t_loop, elapsed - t_loop
 
     el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     ev = torch.tensor([E], dtype=torch.int64, device=cdev)
@@ -175,6 +206,14 @@ def main():
     ms_step = elapsed / args.steps * 1e3
 
     if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    if wl == "dispatch":
+        print(json.dumps(dispatch_line(args, R, world, elapsed, wake, nkt,
+                                       cpu_dispatch(specs[:args.cpu_sample], t0)
+                                       if world == 1 and args.cpu_sample > 0 else None)), flush=True)
         if world > 1:
             dist.destroy_process_group()
         return
@@ -247,6 +286,72 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def dispatch_line(args, R, world, elapsed, wake, nkt, cpu):
+    import numpy as np
+    wall = np.array(wake["wall"] or [0.0])
+    due = wake["due"] / max(wake["wakes"], 1)
+    # k_dispatch_scan per launch: read Next of every entry (8 B) and write the
+    # due bitmap (1 bit); the advance pass then reads the due entries' spec
+    # (32 B) and Next (8 B) and writes Prev/Next (16 B)
+    algo = R * 8 + R / 8
+    fire_s = nkt[0] / 1e3
+    achieved = algo / fire_s / 1e9 if fire_s > 0 else 0.0
+    return {
+        "metric": "dispatcher entries scanned/sec (Cron.run wake over 10M entries)",
+        "value": R * world * args.steps / elapsed,
+        "unit": "entries/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (config-2 spec mix, seeded; parsed on host, resident in HBM)",
+        "config": {"workload": "dispatch: Cron.run entry table of 10M config-2 rules per GPU "
+                               "(the 1M-rule set tiled), on-time wakes from 2026-01-01 UTC",
+                   "entries_per_gpu": R, "zone": "UTC", "mean_due_per_wake": due,
+                   "parallelism": f"dp{world} (independent entry tables)"},
+        "wakes_per_s": args.steps / elapsed,
+        "timed_split_s": {"loop": wake["loop_s"], "final_sync_barrier": wake["tail_s"],
+                          "fire_calls": float(wall.sum())},
+        "wake_wall_us": {q: float(np.percentile(wall, p)) * 1e6 for q, p in
+                         (("p50", 50), ("p90", 90), ("p99", 99), ("max", 100))},
+        "kernel_ms": {"scan": nkt[0], "compact": nkt[1], "advance": nkt[2],
+                      "wake_total": float(sum(nkt))},
+        "roofline": {"bound": "hbm", "kernel": "k_dispatch_scan", "achieved": achieved,
+                     "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                     "traffic": None, "algo_bytes_per_launch": algo},
+        "cpu_baseline": cpu,
+    }
+
+
+def cpu_dispatch(specs, t0):
+    """The reference's wake (sort.Sort(byTime) + Next for the due prefix,
+    cron.go:220-244) as the oracle's C port, on a bounded sample: the time of
+    one steady-state wake (after the start wake has sorted the table)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+    import oracle_lib as O
+    scheds = [O.parse(s)[0] for s in specs]
+    arr = (O.OrEntry * len(scheds))()
+    for i, sc in enumerate(scheds):
+        arr[i].s = C.pointer(sc)
+        arr[i].id = i
+    loc = O.Loc("UTC")
+    L = O.lib()
+    L.or_cron_start(arr, len(scheds), t0, loc.h)
+    ids = (C.c_int32 * len(scheds))()
+    e = L.or_cron_effective(arr, len(scheds))
+    L.or_cron_fire(arr, len(scheds), e, e, loc.h, ids)
+    ts = time.perf_counter()
+    wakes = 0
+    while time.perf_counter() - ts < 5.0 and wakes < 50:
+        e = L.or_cron_effective(arr, len(scheds))
+        L.or_cron_fire(arr, len(scheds), e, e, loc.h, ids)
+        wakes += 1
+    dt = (time.perf_counter() - ts) / wakes
+    return {"value": len(scheds) / dt, "unit": "entries/s", "cores": 1, "kind": "port",
+            "sample": f"{len(scheds)} entries of the same mix, {wakes} steady-state wakes "
+                      f"({dt * 1e3:.1f} ms per wake: qsort by Next + Next for the due prefix)"}
 
 
 def cpu_baseline(specs, t0, t1, threads):

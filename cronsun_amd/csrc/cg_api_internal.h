@@ -72,8 +72,9 @@ struct cg_ctx {
   std::mutex mu;
   // ms: [0..5] expansion phases (count, scan, map, write_cf, write_walk,
   // offsets), [6..8] per-node phases (rule->node join, transpose + per-node
-  // offsets, k_node_write) of the last per-node call
-  float kt[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // offsets, k_node_write) of the last per-node call, [9..11] dispatcher
+  // wake (scan, due compaction, advance) of the last cg_dispatcher_fire
+  float kt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 
   // plan cache
   cg::Plan plan;

@@ -5,11 +5,11 @@
 // (sort.Sort(byTime), cron.go:220) and calls Schedule.Next for each entry that
 // fired.  Here every entry is a slot (its Entry ID maps to a slot index on the
 // host side) with three HBM arrays: the packed spec (32 B), Next and Prev
-// (int64 unix seconds).  A wake is one fused kernel (k_dispatch_fire) that
-// fires the entries whose Next equals the current minimum, advances them with
-// Next(now) and reduces the next minimum in the same pass, followed by an
-// ordered compaction of the due slots.  No sort: the run loop only ever needs
-// the minimum and the entries equal to it.
+// (int64 unix seconds).  A wake is a streaming scan (due bitmap + the minimum
+// over the entries that stay), an ordered compaction of the due slots, and a
+// dense pass that advances the due entries with Next(now) and folds them into
+// the minimum.  No sort: the run loop only ever needs the minimum and the
+// entries equal to it.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -60,6 +60,7 @@ struct cg_dispatcher {
   // wake scratch
   unsigned long long* due_bits = nullptr;
   uint32_t* tile_cnt = nullptr;
+  unsigned long long* tile_min = nullptr;
   int32_t* due = nullptr;
   DispatchState* st = nullptr;
   int64_t n_due = 0;
@@ -75,12 +76,13 @@ struct cg_dispatcher {
 
   void release() {
     for (void* p : {(void*)specs, (void*)next, (void*)prev, (void*)due_bits, (void*)tile_cnt,
-                    (void*)due, (void*)st})
+                    (void*)tile_min, (void*)due, (void*)st})
       if (p) (void)hipFree(p);
     specs = nullptr;
     next = prev = nullptr;
     due_bits = nullptr;
     tile_cnt = nullptr;
+    tile_min = nullptr;
     due = nullptr;
     st = nullptr;
     tab_dev.release();
@@ -124,7 +126,8 @@ struct cg_dispatcher {
         (rc = grow_keep(&next, size_t(n), nc, ctx->st)) ||
         (rc = grow_keep(&prev, size_t(n), nc, ctx->st)) ||
         (rc = grow_keep(&due_bits, 0, tiles * (kDispatchTile / 64), ctx->st)) ||
-        (rc = grow_keep(&tile_cnt, 0, tiles, ctx->st)) || (rc = grow_keep(&due, 0, nc, ctx->st)))
+        (rc = grow_keep(&tile_cnt, 0, tiles, ctx->st)) ||
+        (rc = grow_keep(&tile_min, 0, tiles, ctx->st)) || (rc = grow_keep(&due, 0, nc, ctx->st)))
       return rc;
     if (!st) HIPCHK(hipMalloc(&st, sizeof(DispatchState)));
     cap = nc;
@@ -229,13 +232,20 @@ int cg_dispatcher_fire(cg_dispatcher* d, int64_t now, int64_t* n_due, int64_t* e
                               "(the run loop's timer fires at or after it)");
   int rc = d->ensure_table(now);
   if (rc) return rc;
-  if ((rc = d->reset_state())) return rc;
-  launch_dispatch_fire(d->specs, d->n, d->pa, d->effective, now, d->next, d->prev, d->due_bits,
-                       d->tile_cnt, d->st, c->st);
-  launch_dispatch_compact(d->due_bits, d->tile_cnt, d->n, d->due, c->st);
+  // (k_dispatch_compact writes the whole DispatchState: no reset)
+  (void)hipEventRecord(c->pev[0], c->st);
+  launch_dispatch_scan(d->next, d->n, d->effective, d->due_bits, d->tile_cnt, d->tile_min, c->st);
+  (void)hipEventRecord(c->pev[1], c->st);
+  launch_dispatch_compact(d->due_bits, d->tile_cnt, d->tile_min, d->n, d->due, d->st, c->st);
+  (void)hipEventRecord(c->pev[2], c->st);
+  launch_dispatch_advance(d->specs, d->due, d->n, d->pa, now, d->next, d->prev, d->st, c->st);
+  (void)hipEventRecord(c->pev[3], c->st);
   HIPCHK(hipGetLastError());
   DispatchState h;
   rc = d->read_state(&h);
+  (void)hipEventElapsedTime(&c->kt[9], c->pev[0], c->pev[1]);
+  (void)hipEventElapsedTime(&c->kt[10], c->pev[1], c->pev[2]);
+  (void)hipEventElapsedTime(&c->kt[11], c->pev[2], c->pev[3]);
   d->n_due = int64_t(h.n_due);
   *n_due = d->n_due;
   *effective = d->effective;

@@ -44,11 +44,15 @@ struct DispatchState {
   unsigned long long stuck;    // first entry whose Next never returns (~0 = none)
   unsigned long long pad;
 };
-void launch_dispatch_fire(const DSpec* specs, int64_t n, const PlanArgs& p, int64_t effective,
-                          int64_t now, int64_t* next, int64_t* prev, unsigned long long* due_bits,
-                          uint32_t* tile_cnt, DispatchState* st, hipStream_t s);
-void launch_dispatch_compact(const unsigned long long* due_bits, const uint32_t* tile_cnt, int64_t n,
-                             int32_t* due, hipStream_t s);
+void launch_dispatch_scan(const int64_t* next, int64_t n, int64_t effective,
+                          unsigned long long* due_bits, uint32_t* tile_cnt,
+                          unsigned long long* tile_min, hipStream_t s);
+void launch_dispatch_advance(const DSpec* specs, const int32_t* due, int64_t n, const PlanArgs& p,
+                             int64_t now, int64_t* next, int64_t* prev, DispatchState* st,
+                             hipStream_t s);
+void launch_dispatch_compact(const unsigned long long* due_bits, const uint32_t* tile_cnt,
+                             const unsigned long long* tile_min, int64_t n, int32_t* due,
+                             DispatchState* st, hipStream_t s);
 void launch_dispatch_place(DSpec* specs, const int64_t* idx, const DSpec* src, int64_t first,
                            int64_t k, const PlanArgs& p, int64_t now, int64_t* next, int64_t* prev,
                            DispatchState* st, hipStream_t s);

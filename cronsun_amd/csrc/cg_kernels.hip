@@ -131,40 +131,39 @@ __device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v)
   return v;
 }
 
-// One wake of the run loop (cron.go:234-244): every entry whose Next equals
-// `effective` is due: Prev = Next, Next = Schedule.Next(now).  Fused with the
-// next wake's byTime minimum (cron.go:220-230) over the updated Nexts.  One
-// block per kDispatchTile entries; a due bitmap word per 64 entries and a due
-// count per tile feed the ordered compaction.
-__global__ __launch_bounds__(256) void k_dispatch_fire(
-    const DSpec* __restrict__ specs, int64_t n, PlanArgs p, int64_t effective, int64_t now,
-    int64_t* __restrict__ next, int64_t* __restrict__ prev, unsigned long long* __restrict__ due_bits,
-    uint32_t* __restrict__ tile_cnt, DispatchState* __restrict__ st) {
-  extern __shared__ __align__(16) char lds[];
+// One wake of the run loop (cron.go:234-244), in three launches:
+//   k_dispatch_scan     every entry whose Next equals `effective` is due: a
+//                       bitmap word per 64 entries, a due count per tile, and
+//                       the byTime minimum over the entries that stay;
+//   k_dispatch_compact  the due slots in ascending order;
+//   k_dispatch_advance  dense over the due list: Prev = Next, Next =
+//                       Schedule.Next(now), folded into the minimum.
+// The scan is a pure 8 B/entry stream; the Next walks run on full waves of
+// due entries instead of on the few due lanes of every scanned wave.
+__global__ __launch_bounds__(256) void k_dispatch_scan(
+    const int64_t* __restrict__ next, int64_t n, int64_t effective,
+    unsigned long long* __restrict__ due_bits, uint32_t* __restrict__ tile_cnt,
+    unsigned long long* __restrict__ tile_min) {
   __shared__ unsigned long long s_min[4];
   __shared__ uint32_t s_cnt[4];
-  PlanView v = stage_plan(p, lds);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t base = int64_t(blockIdx.x) * kDispatchTile;
+  constexpr int kIter = kDispatchTile / 256;
+  // all loads first: 16 outstanding 512 B wave loads per wave
+  int64_t t[kIter];
+#pragma unroll
+  for (int j = 0; j < kIter; j++) {
+    const int64_t i = base + j * 256 + wv * 64 + lane;
+    t[j] = i < n ? __builtin_nontemporal_load(next + i) : CG_ZERO_TIME;
+  }
   unsigned long long kmin = ~0ull;
   uint32_t cnt = 0;
-  for (int j = 0; j < kDispatchTile / 256; j++) {
+#pragma unroll
+  for (int j = 0; j < kIter; j++) {
     const int64_t w0 = base + j * 256 + wv * 64;  // first entry of this wave's word
-    const int64_t i = w0 + lane;
-    bool due = false;
-    if (i < n) {
-      int64_t t = next[i];
-      if (t == effective) {
-        due = true;
-        const DSpec sp = load_spec(specs + i);
-        prev[i] = t;
-        t = sp.kind == KIND_EVERY ? now + int64_t(sp.sec) : next_exact(sp, v.z, now, INT64_MAX);
-        if (t == CG_NO_PROGRESS) atomicMin(&st->stuck, (unsigned long long)i);
-        next[i] = t;
-      }
-      const unsigned long long k = next_key(t);
-      kmin = k < kmin ? k : kmin;
-    }
+    const bool due = t[j] == effective;           // (padding lanes hold the zero time)
+    const unsigned long long k = due ? ~0ull : next_key(t[j]);
+    kmin = k < kmin ? k : kmin;
     const unsigned long long b = __ballot(due);
     if (lane == 0 && w0 < n) due_bits[w0 >> 6] = b;
     cnt += __popcll(b);
@@ -182,9 +181,39 @@ __global__ __launch_bounds__(256) void k_dispatch_fire(
       m = s_min[w] < m ? s_min[w] : m;
       c += s_cnt[w];
     }
-    tile_cnt[blockIdx.x] = c;
-    if (m != ~0ull) atomicMin(&st->min_key, m);
-    if (c) atomicAdd(&st->n_due, (unsigned long long)c);
+    tile_cnt[blockIdx.x] = c;  // per-tile results: thousands of same-address
+    tile_min[blockIdx.x] = m;  // atomics would serialise at one L2 channel
+  }
+}
+
+__global__ __launch_bounds__(256) void k_dispatch_advance(
+    const DSpec* __restrict__ specs, const int32_t* __restrict__ due, PlanArgs p, int64_t now,
+    int64_t* __restrict__ next, int64_t* __restrict__ prev, DispatchState* __restrict__ st) {
+  extern __shared__ __align__(16) char lds[];
+  const int64_t m = int64_t(*(volatile unsigned long long*)&st->n_due);
+  if (int64_t(blockIdx.x) * blockDim.x >= m) return;  // uniform: before any barrier
+  PlanView v = stage_plan(p, lds);
+  unsigned long long kmin = ~0ull;
+  for (int64_t j = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; j < m;
+       j += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t i = due[j];
+    const DSpec sp = load_spec(specs + i);
+    prev[i] = next[i];
+    const int64_t t =
+        sp.kind == KIND_EVERY ? now + int64_t(sp.sec) : next_exact(sp, v.z, now, INT64_MAX);
+    if (t == CG_NO_PROGRESS) atomicMin(&st->stuck, (unsigned long long)i);
+    next[i] = t;
+    const unsigned long long k = next_key(t);
+    kmin = k < kmin ? k : kmin;
+  }
+  __shared__ unsigned long long s_min[4];
+  kmin = wave_min_u64(kmin);
+  if ((threadIdx.x & 63) == 0) s_min[threadIdx.x >> 6] = kmin;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m2 = s_min[0];
+    for (int w = 1; w < 4; w++) m2 = s_min[w] < m2 ? s_min[w] : m2;
+    if (m2 != ~0ull) atomicMin(&st->min_key, m2);
   }
 }
 
@@ -192,11 +221,34 @@ __global__ __launch_bounds__(256) void k_dispatch_fire(
 // counts, then wave 0 expands the tile's 64 bitmap words in order.
 __global__ __launch_bounds__(256) void k_dispatch_compact(
     const unsigned long long* __restrict__ due_bits, const uint32_t* __restrict__ tile_cnt,
-    int64_t n, int32_t* __restrict__ due) {
-  __shared__ unsigned long long s_sum[4];
+    const unsigned long long* __restrict__ tile_min, int64_t n, int32_t* __restrict__ due,
+    DispatchState* __restrict__ st) {
+  __shared__ unsigned long long s_sum[4], s_min[4];
   const int64_t b = blockIdx.x;
-  if (tile_cnt[b] == 0) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (b == int64_t(gridDim.x) - 1) {  // the wake's totals: due count, minimum of the rest
+    unsigned long long c = 0, m = ~0ull;
+    for (int64_t k = threadIdx.x; k < gridDim.x; k += 256) {
+      c += tile_cnt[k];
+      m = tile_min[k] < m ? tile_min[k] : m;
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+    m = wave_min_u64(m);
+    if (lane == 0) {
+      s_sum[wv] = c;
+      s_min[wv] = m;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the whole wake state: no host-side reset needed
+      st->stuck = ~0ull;
+      st->n_due = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+      unsigned long long mm = s_min[0];
+      for (int w = 1; w < 4; w++) mm = s_min[w] < mm ? s_min[w] : mm;
+      st->min_key = mm;
+    }
+    __syncthreads();
+  }
+  if (tile_cnt[b] == 0) return;
   unsigned long long s = 0;
   for (int64_t k = threadIdx.x; k < b; k += 256) s += tile_cnt[k];
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -266,8 +318,15 @@ __global__ __launch_bounds__(256) void k_dispatch_min(const int64_t* __restrict_
     const unsigned long long k = next_key(next[i]);
     m = k < m ? k : m;
   }
+  __shared__ unsigned long long s_min[4];
   m = wave_min_u64(m);
-  if ((threadIdx.x & 63) == 0 && m != ~0ull) atomicMin(&st->min_key, m);
+  if ((threadIdx.x & 63) == 0) s_min[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; w++) m = s_min[w] < m ? s_min[w] : m;
+    m = s_min[0] < m ? s_min[0] : m;
+    if (m != ~0ull) atomicMin(&st->min_key, m);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, int64_t R,
@@ -996,21 +1055,32 @@ void launch_lock_ttl(const DSpec* specs, int64_t n, const PlanArgs& p, const int
                      st, specs, n, p, now, kind, avg_ms, lock_ttl, ttl);
 }
 
-void launch_dispatch_fire(const DSpec* specs, int64_t n, const PlanArgs& p, int64_t effective,
-                          int64_t now, int64_t* next, int64_t* prev, unsigned long long* due_bits,
-                          uint32_t* tile_cnt, DispatchState* st, hipStream_t s) {
+void launch_dispatch_scan(const int64_t* next, int64_t n, int64_t effective,
+                          unsigned long long* due_bits, uint32_t* tile_cnt,
+                          unsigned long long* tile_min, hipStream_t s) {
   if (n <= 0) return;
   const int64_t tiles = (n + kDispatchTile - 1) / kDispatchTile;
-  hipLaunchKernelGGL(k_dispatch_fire, dim3(unsigned(tiles)), dim3(256), plan_lds_bytes(p), s, specs,
-                     n, p, effective, now, next, prev, due_bits, tile_cnt, st);
+  hipLaunchKernelGGL(k_dispatch_scan, dim3(unsigned(tiles)), dim3(256), 0, s, next, n, effective,
+                     due_bits, tile_cnt, tile_min);
 }
 
-void launch_dispatch_compact(const unsigned long long* due_bits, const uint32_t* tile_cnt, int64_t n,
-                             int32_t* due, hipStream_t s) {
+void launch_dispatch_advance(const DSpec* specs, const int32_t* due, int64_t n, const PlanArgs& p,
+                             int64_t now, int64_t* next, int64_t* prev, DispatchState* st,
+                             hipStream_t s) {
+  if (n <= 0) return;
+  // sized for the largest possible due list; blocks past the device-side
+  // count exit before staging the zone table
+  hipLaunchKernelGGL(k_dispatch_advance, dim3(grid_for(n, 256, 4096)), dim3(256),
+                     plan_lds_bytes(p), s, specs, due, p, now, next, prev, st);
+}
+
+void launch_dispatch_compact(const unsigned long long* due_bits, const uint32_t* tile_cnt,
+                             const unsigned long long* tile_min, int64_t n, int32_t* due,
+                             DispatchState* st, hipStream_t s) {
   if (n <= 0) return;
   const int64_t tiles = (n + kDispatchTile - 1) / kDispatchTile;
   hipLaunchKernelGGL(k_dispatch_compact, dim3(unsigned(tiles)), dim3(256), 0, s, due_bits, tile_cnt,
-                     n, due);
+                     tile_min, n, due, st);
 }
 
 void launch_dispatch_place(DSpec* specs, const int64_t* idx, const DSpec* src, int64_t first,
@@ -1030,7 +1100,7 @@ void launch_dispatch_clear(const int64_t* idx, int64_t first, int64_t k, int64_t
 
 void launch_dispatch_min(const int64_t* next, int64_t n, DispatchState* st, hipStream_t s) {
   if (n <= 0) return;
-  hipLaunchKernelGGL(k_dispatch_min, dim3(grid_for(n, 256, 2048)), dim3(256), 0, s, next, n, st);
+  hipLaunchKernelGGL(k_dispatch_min, dim3(grid_for(n, 256 * 8, 1024)), dim3(256), 0, s, next, n, st);
 }
 
 void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run_anchor,

@@ -283,16 +283,22 @@ class Engine:
     def kernel_times(self):
         """ms per phase of the last expansion: count, scan, block map,
         write(closed form), write(walk), offsets."""
-        buf = (C.c_float * 9)()
-        k = lib().cg_last_kernel_times(self._h, buf, 9)
+        buf = (C.c_float * 12)()
+        k = lib().cg_last_kernel_times(self._h, buf, 12)
         return list(buf)[:min(k, 6)]
 
     def node_kernel_times(self):
         """ms per phase of the last per-node call: rule->node join,
         transpose + per-node offsets, per-node write."""
-        buf = (C.c_float * 9)()
-        lib().cg_last_kernel_times(self._h, buf, 9)
+        buf = (C.c_float * 12)()
+        lib().cg_last_kernel_times(self._h, buf, 12)
         return list(buf)[6:9]
+
+    def dispatch_kernel_times(self):
+        """ms of the last dispatcher wake: scan, due compaction, advance."""
+        buf = (C.c_float * 12)()
+        lib().cg_last_kernel_times(self._h, buf, 12)
+        return list(buf)[9:12]
 
     def sync(self):
         check(lib().cg_sync(self._h))
