@@ -30,6 +30,7 @@ PARSE_DEFAULT = 1 | 2 | 4 | 8 | 16 | 64 | 128
 PARSE_STANDARD = 2 | 4 | 8 | 16 | 32 | 128
 
 EXCLUDE_NONE, EXCLUDE_RULE, EXCLUDE_CUMULATIVE = 0, 1, 2
+INGEST_OK, INGEST_UNMARSHAL, INGEST_INVALID, INGEST_PANIC, INGEST_REPLACED, INGEST_UNSUPPORTED = range(6)
 
 
 class CgError(RuntimeError):
@@ -146,6 +147,13 @@ def _declare(L):
         "cg_jobset_cmds": ([vp, i32, C.c_char_p, vp, i32], i32),
         "cg_jobset_is_run_on": ([vp, i32, C.c_char_p], C.c_int),
         "cg_jobset_job_nodes": ([vp, i32, vp, i32], i32),
+        "cg_jobset_ingest_groups": ([vp, vp, vp, sz, C.c_int, vp], C.c_int),
+        "cg_jobset_ingest_jobs": ([vp, vp, vp, sz, C.c_int, vp], C.c_int),
+        "cg_jobset_schedules": ([vp, vp, sz], C.c_int),
+        "cg_jobset_job_meta": ([vp, vp, vp, vp, sz], C.c_int),
+        "cg_jobset_job_id": ([vp, i32], C.c_char_p),
+        "cg_jobset_group_id": ([vp, i32], C.c_char_p),
+        "cg_jobset_rule_id": ([vp, i32], C.c_char_p),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)

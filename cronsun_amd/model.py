@@ -103,7 +103,42 @@ def _cstr_array(strs):
     return arr, len(enc), enc
 
 
-class JobSet:
+class _Interned:
+    """Host-side queries over an interned cg_jobset handle (self._h)."""
+
+    def rules_in(self) -> RulesIn:
+        """Copy the interned arrays into a RulesIn (numpy-owned)."""
+        return rules_in_of(self._h)
+
+    def node_index(self, nid):
+        return lib().cg_jobset_node_index(self._h, nid.encode())
+
+    def node_id(self, idx):
+        v = lib().cg_jobset_node_id(self._h, idx)
+        return None if v is None else v.decode()
+
+    def cmds(self, job, nid):
+        out = np.zeros(max(self.n_rules, 1), dtype=np.int32)
+        k = check(lib().cg_jobset_cmds(self._h, job, nid.encode(), out.ctypes.data, len(out)))
+        return [int(x) for x in out[:k]]
+
+    def is_run_on(self, job, nid):
+        return bool(check(lib().cg_jobset_is_run_on(self._h, job, nid.encode())))
+
+    def job_nodes(self, job):
+        cap = 1 << 16
+        out = np.zeros(cap, dtype=np.int32)
+        k = check(lib().cg_jobset_job_nodes(self._h, job, out.ctypes.data, cap))
+        return [self.node_id(int(x)) for x in out[:min(k, cap)]]
+
+    def __del__(self):
+        try:
+            lib().cg_jobset_free(self._h)
+        except Exception:
+            pass
+
+
+class JobSet(_Interned):
     """All jobs + groups interned by the C++ host layer (cg_jobset)."""
 
     def __init__(self, jobs, groups: GroupMap):
@@ -128,57 +163,9 @@ class JobSet:
                 self.rules.append(r)
                 self.rule_job.append(ji)
 
-    def __del__(self):
-        try:
-            lib().cg_jobset_free(self._h)
-        except Exception:
-            pass
-
-    def rules_in(self) -> RulesIn:
-        """Copy the interned arrays into a RulesIn (numpy-owned)."""
-        c = _lib.cg_rules_in()
-        check(lib().cg_jobset_rules(self._h, C.byref(c)))
-
-        def arr(ptr, n, dt):
-            if n == 0:
-                return np.zeros(0, dtype=dt)
-            ct = {np.int64: C.c_int64, np.int32: C.c_int32, np.uint8: C.c_uint8}[dt]
-            return np.ctypeslib.as_array((ct * n).from_address(ptr)).copy()
-
-        R, G, J = c.n_rules, c.n_groups, c.n_jobs
-        nid_off = arr(c.nid_off, R + 1, np.int64)
-        gid_off = arr(c.gid_off, R + 1, np.int64)
-        ex_off = arr(c.ex_off, R + 1, np.int64)
-        group_off = arr(c.group_off, G + 1, np.int64)
-        return RulesIn(
-            c.n_nodes, G, R, J,
-            group_off=group_off, group_nodes=arr(c.group_nodes, int(group_off[-1]), np.int32),
-            group_exists=arr(c.group_exists, G, np.uint8), rule_job=arr(c.rule_job, R, np.int32),
-            nid_off=nid_off, nids=arr(c.nids, int(nid_off[-1]), np.int32),
-            gid_off=gid_off, gids=arr(c.gids, int(gid_off[-1]), np.int32),
-            ex_off=ex_off, ex=arr(c.ex, int(ex_off[-1]), np.int32),
-            job_pause=arr(c.job_pause, J, np.uint8))
-
-    def node_index(self, nid):
-        return lib().cg_jobset_node_index(self._h, nid.encode())
-
-    def node_id(self, idx):
-        v = lib().cg_jobset_node_id(self._h, idx)
-        return None if v is None else v.decode()
-
-    def cmds(self, job, nid):
-        out = np.zeros(max(len(self.rules), 1), dtype=np.int32)
-        k = check(lib().cg_jobset_cmds(self._h, job, nid.encode(), out.ctypes.data, len(out)))
-        return [int(x) for x in out[:k]]
-
-    def is_run_on(self, job, nid):
-        return bool(check(lib().cg_jobset_is_run_on(self._h, job, nid.encode())))
-
-    def job_nodes(self, job):
-        cap = 1 << 16
-        out = np.zeros(cap, dtype=np.int32)
-        k = check(lib().cg_jobset_job_nodes(self._h, job, out.ctypes.data, cap))
-        return [self.node_id(int(x)) for x in out[:min(k, cap)]]
+    @property
+    def n_rules(self):
+        return len(self.rules)
 
     def lock_ttls(self, now, loc=None, lock_ttl=300, engine=None):
         """Cmd.lockTtl for every (job, rule) Cmd at time `now` (unix seconds):
@@ -195,3 +182,29 @@ class JobSet:
         for r in self.rules:
             r.Valid()
         return [r.Schedule for r in self.rules]
+
+
+def rules_in_of(h) -> RulesIn:
+    """cg_jobset_rules of a handle, copied into a numpy-owned RulesIn."""
+    c = _lib.cg_rules_in()
+    check(lib().cg_jobset_rules(h, C.byref(c)))
+
+    def arr(ptr, n, dt):
+        if n == 0:
+            return np.zeros(0, dtype=dt)
+        ct = {np.int64: C.c_int64, np.int32: C.c_int32, np.uint8: C.c_uint8}[dt]
+        return np.ctypeslib.as_array((ct * n).from_address(ptr)).copy()
+
+    R, G, J = c.n_rules, c.n_groups, c.n_jobs
+    nid_off = arr(c.nid_off, R + 1, np.int64)
+    gid_off = arr(c.gid_off, R + 1, np.int64)
+    ex_off = arr(c.ex_off, R + 1, np.int64)
+    group_off = arr(c.group_off, G + 1, np.int64)
+    return RulesIn(
+        c.n_nodes, G, R, J,
+        group_off=group_off, group_nodes=arr(c.group_nodes, int(group_off[-1]), np.int32),
+        group_exists=arr(c.group_exists, G, np.uint8), rule_job=arr(c.rule_job, R, np.int32),
+        nid_off=nid_off, nids=arr(c.nids, int(nid_off[-1]), np.int32),
+        gid_off=gid_off, gids=arr(c.gids, int(gid_off[-1]), np.int32),
+        ex_off=ex_off, ex=arr(c.ex, int(ex_off[-1]), np.int32),
+        job_pause=arr(c.job_pause, J, np.uint8))

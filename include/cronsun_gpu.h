@@ -357,6 +357,35 @@ int cg_jobset_is_run_on(const cg_jobset* js, int32_t job, const char* nid);
 /* Job.GetJobNodes (web/job.go:222-257): node indices in first-seen order */
 int32_t cg_jobset_job_nodes(const cg_jobset* js, int32_t job, int32_t* nodes_out, int32_t cap);
 
+/* ------------------------------------------ bulk ingestion (etcd JSON) --- */
+/* GetGroups("") / GetJobs() (group.go:39-63, job.go:339-365) over the raw
+ * etcd values: docs[i] is the JSON value of one key under /cronsun/group/
+ * (groups) or /cronsun/cmd/ (jobs), in key order.  Each value goes through
+ * json.Unmarshal into Group / Job (Go 1.7-1.8 encoding/json semantics, see
+ * cg_ingest.cpp), Job.Valid (every rule's Timer through cron.Parse) and
+ * alone(); the last valid value of an ID wins.  Decoding runs on nthreads
+ * host threads.  status[i] (optional) gets one of: */
+#define CG_INGEST_OK 0          /* added to the jobset */
+#define CG_INGEST_UNMARSHAL 1   /* json.Unmarshal error: skipped (job.go:353-356) */
+#define CG_INGEST_INVALID 2     /* Job.Valid error (ErrNilRule, parse error): skipped */
+#define CG_INGEST_PANIC 3       /* a null rule: the reference panics in JobRule.Valid */
+#define CG_INGEST_REPLACED 4    /* a later value with the same ID replaced it */
+#define CG_INGEST_UNSUPPORTED 5 /* an ID containing NUL (not representable here) */
+int cg_jobset_ingest_groups(cg_jobset* js, const char* const* docs, const size_t* lens, size_t n,
+                            int nthreads, int32_t* status);
+int cg_jobset_ingest_jobs(cg_jobset* js, const char* const* docs, const size_t* lens, size_t n,
+                          int nthreads, int32_t* status);
+/* JobRule.Schedule per rule (rule order of cg_jobset_rules); returns the rule
+ * count (writes at most cap).  CG_EINVAL if a rule was added without a timer. */
+int cg_jobset_schedules(const cg_jobset* js, cg_schedule* out, size_t cap);
+/* Job.Kind, Job.AvgTime (ms) and Job.Parallels (after alone()) per job;
+ * returns the job count (writes at most cap; any pointer may be NULL) */
+int cg_jobset_job_meta(const cg_jobset* js, int32_t* kind, int64_t* avg_time_ms,
+                       int64_t* parallels, size_t cap);
+const char* cg_jobset_job_id(const cg_jobset* js, int32_t job);
+const char* cg_jobset_group_id(const cg_jobset* js, int32_t group);
+const char* cg_jobset_rule_id(const cg_jobset* js, int32_t rule);
+
 #ifdef __cplusplus
 }
 #endif
