@@ -20,6 +20,12 @@ Workloads (`--workload`, default config2 -- the headline line):
   config4  config 4 shape: 10M rules x 7 days over the job-ID-range shards of
            N GPUs (10M / N rules per rank, lighter spec mix); a step = one
            expansion per rank.  Fixed total work: `scaling` = "strong".
+  config3  config 3 as specified: 1M jobs x 10k nodes, the config-2 spec mix,
+           24 h -> per-node lists, streamed in 1 h windows (`--window`; the
+           whole day's 62 G node events would not fit one GPU's HBM): a step
+           = 24 windows of expansion + join + transpose + per-node write, each
+           window's per-node counts all-gathered at N > 1.  `--exclude-mode`
+           none (the scheduling path) | rule | cumulative (web/job.go).
   dispatch SURVEY.md §8(f)-1: Cron.run's entry table resident in HBM, 10M
            entries of the config-2 mix per GPU; a step = one on-time wake
            (fire every entry whose Next is the earliest, Next(now) for them,
@@ -66,9 +72,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["config2", "pernode", "config4", "dispatch"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "pernode", "config3", "config4", "dispatch"], default="config2")
     ap.add_argument("--rules", type=int, default=0, help="rules per GPU (0 = the workload's)")
     ap.add_argument("--horizon", type=int, default=0, help="seconds (0 = the workload's)")
+    ap.add_argument("--window", type=int, default=0,
+                    help="per-node output window in seconds (0 = the workload's; config3: 3600)")
+    ap.add_argument("--exclude-mode", choices=["none", "rule", "cumulative"], default="none")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="rules in the CPU-baseline sample (0 = skip; default 40k, 1M for dispatch)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -77,6 +86,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
     import torch
     import torch.distributed as dist
     # RCCL ("nccl") in production; CG_DIST_BACKEND=gloo rehearses the N > 1
@@ -109,6 +119,11 @@ def main():
         H = args.horizon or 3600
         mix = synth.MIX_LIGHT
         seed = 0x5EED + 3 + rank
+    elif wl == "config3":
+        R = args.rules or 1_000_000
+        H = args.horizon or 86400
+        mix = synth.MIX_CONFIG2
+        seed = 0x5EED + 3 + rank
     else:  # config4: 10M rules in total, job-ID-range shards
         total = args.rules or 10_000_000
         lo, hi = shard.shard_range(total, world, rank)
@@ -118,6 +133,9 @@ def main():
         seed = 0x5EED + 4 + lo  # a shard's rules depend on its job-ID range only
     t0 = synth.T0_2026
     t1 = t0 + H
+    pn = wl in ("pernode", "config3")
+    W = args.window or (3600 if wl == "config3" else H)
+    xmode = {"none": 0, "rule": 1, "cumulative": 2}[args.exclude_mode]
     eng = Engine(local)
     log(f"[rank {rank}] {wl}: generating {R} rules (job-ID shard {rank})")
     if wl == "dispatch" and R > 1_000_000:
@@ -133,7 +151,7 @@ def main():
     utc = cron.UTC()
     drules = None
     n_nodes = 10_000
-    if wl == "pernode":
+    if pn:
         rin = synth.rules_for_nodes(R, n_nodes=n_nodes, n_groups=500, seed=0x5EED + 3 + 1000 * rank)
         drules = eng.upload_rules(rin)
 
@@ -144,7 +162,7 @@ def main():
     dev = torch.device("cuda", local)
     cdev = dev if backend == "nccl" else torch.device("cpu")  # collective tensors
     tot = torch.zeros(world, dtype=torch.int64, device=cdev)
-    node_counts = torch.zeros(n_nodes, dtype=torch.int64, device=dev) if wl == "pernode" else None
+    node_counts = torch.zeros(n_nodes, dtype=torch.int64, device=dev) if pn else None
     last = {}
 
     disp = eng.dispatcher(sp, utc, t0) if wl == "dispatch" else None
@@ -158,13 +176,22 @@ def main():
             wake["due"] += n_due
             wake["wakes"] += 1
             return n_due
-        if wl == "pernode":
-            En, nnz = eng.expand_per_node_rules_device(sp, utc, t0, t1, drules)
-            last["nnz"] = nnz
-            if world > 1:
-                # per-node offsets of every rank's slice (RCCL allgather of N int64)
-                eng.node_counts_to_device(node_counts.data_ptr())
-                shard.node_offsets(node_counts.to(cdev), dist)
+        if pn:
+            En = 0
+            kt_sum = np.zeros(6)
+            nkt_sum = np.zeros(3)
+            for a in range(t0, t1, W):  # per-node lists window by window
+                En_w, nnz = eng.expand_per_node_rules_device(sp, utc, a, min(a + W, t1), drules,
+                                                             xmode)
+                En += En_w
+                kt_sum += np.array(eng.kernel_times())
+                nkt_sum += np.array(eng.node_kernel_times())
+                last.setdefault("first_nkt", eng.node_kernel_times())  # the uncached join
+                if world > 1:
+                    # per-node offsets of every rank's slice (RCCL allgather of N int64)
+                    eng.node_counts_to_device(node_counts.data_ptr())
+                    shard.node_offsets(node_counts.to(cdev), dist)
+            last.update(nnz=nnz, kt=kt_sum, nkt=nkt_sum, windows=len(range(t0, t1, W)))
             return En
         E = eng.expand_device(sp, utc, t0, t1)
         if world > 1:
@@ -184,8 +211,12 @@ def main():
     wake["wall"] = []
     for _ in range(args.steps):
         E = step()
-        kts.append(eng.kernel_times())
-        nkts.append(eng.dispatch_kernel_times() if wl == "dispatch" else eng.node_kernel_times())
+        if pn:
+            kts.append(last["kt"])
+            nkts.append(last["nkt"])
+        else:
+            kts.append(eng.kernel_times())
+            nkts.append(eng.dispatch_kernel_times() if wl == "dispatch" else eng.node_kernel_times())
     t_loop = time.perf_counter() - start
     torch.cuda.synchronize()
     barrier()
@@ -200,7 +231,6 @@ def main():
     elapsed = float(el.item())
     total_events = int(ev.item())
 
-    import numpy as np
     kt = np.mean(np.array(kts), axis=0)    # count, scan, map, write_cf, write_walk, offsets (ms)
     nkt = np.mean(np.array(nkts), axis=0)  # join, transpose, node write (ms)
     ms_step = elapsed / args.steps * 1e3
@@ -218,15 +248,18 @@ def main():
             dist.destroy_process_group()
         return
 
-    if wl == "pernode":
-        # per-node CSR bytes: R*32 + nnz*4 + (R+1)*8 + E_n*(8+4) + (N+1)*8;
-        # dominant kernel k_node_write
-        nnz = last["nnz"]
-        algo_bytes = R * SPEC_BYTES + nnz * 4 + (R + 1) * 8 + E * 12 + (n_nodes + 1) * 8
+    if pn:
+        # per-node CSR bytes: R*32 + nnz*4 + (R+1)*8 + E_n*(8+4) + (N+1)*8
+        # per window; dominant kernel k_node_write (its time summed over the windows)
+        nnz, nw = last["nnz"], last["windows"]
+        algo_bytes = nw * (R * SPEC_BYTES + nnz * 4 + (R + 1) * 8 + (n_nodes + 1) * 8) + E * 12
         kname, ksec = "k_node_write", nkt[2] / 1e3
-        metric = "per-node fire events materialised/sec (config 3: 1M jobs × 10k nodes, 1h)"
-        workload = ("config 3: 1M jobs x 10k nodes (500 groups, GroupIDs/NodeIDs/ExcludeNodeIDs), "
-                    "light spec mix, 1h horizon, UTC, per GPU; exclude mode NONE (job.go:591-630)")
+        hz = f"{H // 3600}h" if H % 3600 == 0 else f"{H}s"
+        metric = f"per-node fire events materialised/sec (config 3: 1M jobs × 10k nodes, {hz})"
+        workload = (f"config 3: 1M jobs x 10k nodes (500 groups, GroupIDs/NodeIDs/ExcludeNodeIDs), "
+                    f"{'config-2' if wl == 'config3' else 'light'} spec mix, {hz} horizon in "
+                    f"{nw} window(s) of {W}s, UTC, per GPU; exclude mode {args.exclude_mode}"
+                    + (" (job.go:591-630)" if xmode == 0 else ""))
         traffic = None
     else:
         algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
@@ -280,9 +313,14 @@ def main():
         },
         "cpu_baseline": cpu,
     }
-    if wl == "pernode":
+    if pn:
         out["kernel_ms"].update({"rule_node_join": nkt[0], "transpose": nkt[1], "node_write": nkt[2]})
         out["config"]["nnz_rule_node_pairs"] = last["nnz"]
+        out["config"]["windows"] = last["windows"]
+        # the rule->node join + transpose depend only on the uploaded rule set and
+        # exclude mode: computed on the first call (warmup), reused afterwards
+        out["join_transpose_once_ms"] = {"rule_node_join": last["first_nkt"][0],
+                                         "transpose": last["first_nkt"][1]}
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

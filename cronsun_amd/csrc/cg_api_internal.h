@@ -56,6 +56,7 @@ struct RulesStore {
   DBuf<int32_t> nids, gids, ex, group_nodes, rule_job;
   DBuf<uint8_t> group_exists, job_pause;
   int32_t n_nodes = 0, n_groups = 0, n_rules = 0, n_jobs = 0;
+  uint64_t serial = 0;  // unique per upload: keys the per-node transpose cache
   void release() {
     nid_off.release(); gid_off.release(); ex_off.release(); group_off.release();
     nids.release(); gids.release(); ex.release(); group_nodes.release(); rule_job.release();
@@ -99,6 +100,10 @@ struct cg_ctx {
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   DBuf<char> pn_tmp;
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
+  // the rule->node join + transpose depend only on (rule set, exclude mode):
+  // kept across per-node calls on the same uploaded rule set (time windows)
+  uint64_t pn_cache_serial = 0;
+  int pn_cache_mode = -1;
 
   void free_all() {
     plan_dev.release();

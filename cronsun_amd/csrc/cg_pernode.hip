@@ -23,6 +23,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -390,6 +391,8 @@ int upload_rules(const cg_rules_in* in, RulesStore* st, hipStream_t s) {
   st->n_groups = G;
   st->n_rules = R;
   st->n_jobs = in->n_jobs;
+  static std::atomic<uint64_t> next_serial{1};
+  st->serial = next_serial.fetch_add(1);
   return cg_hip_check(hipStreamSynchronize(s), "upload rules");  // host arrays may go away
 }
 
@@ -436,17 +439,23 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   int rc = expand_device_locked(c, s, z, t0, t1, &E);
   if (rc) return rc;
   int64_t nnz = 0;
-  (void)hipEventRecord(c->pev[0], c->st);
-  if ((rc = rule_nodes_locked(c, in, mode, &nnz))) return rc;
-  (void)hipEventRecord(c->pev[1], c->st);
   const int32_t N = in.n_nodes;
   hipStream_t st = c->st;
+  const bool cached = in.serial != 0 && in.serial == c->pn_cache_serial && mode == c->pn_cache_mode;
+  (void)hipEventRecord(c->pev[0], c->st);
+  if (cached) {
+    nnz = c->pn_nnz;
+  } else {
+    c->pn_cache_serial = 0;  // the transpose buffers are about to change
+    if ((rc = rule_nodes_locked(c, in, mode, &nnz))) return rc;
+  }
+  (void)hipEventRecord(c->pev[1], c->st);
   if ((rc = c->nt_off.ensure(N + 1))) return rc;
   if ((rc = c->nt_rule.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if ((rc = c->pair_node.ensure(std::max<int64_t>(nnz, 1)))) return rc;
   if ((rc = c->node_off.ensure(N + 1))) return rc;
   // transpose: stable radix sort of (node, rule) pairs by node
-  if (nnz > 0) {
+  if (nnz > 0 && !cached) {
     unsigned end_bit = 1;
     while ((1u << end_bit) < unsigned(std::max(N, 2))) end_bit++;
     size_t tmp_bytes = 0;
@@ -462,8 +471,9 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
              "radix_sort_pairs")))
       return rc;
   }
-  hipLaunchKernelGGL(k_node_bounds, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
-                     reinterpret_cast<const uint32_t*>(c->pair_node.p), nnz, N, c->nt_off.p);
+  if (!cached)
+    hipLaunchKernelGGL(k_node_bounds, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
+                       reinterpret_cast<const uint32_t*>(c->pair_node.p), nnz, N, c->nt_off.p);
   if ((rc = c->scan_tmp.ensure(std::max(scan_temp_bytes(N), scan_temp_bytes(nnz))))) return rc;
   // per-pair event counts -> positions
   if ((rc = c->rn_cnt.ensure(std::max<int64_t>(nnz, 1)))) return rc;
@@ -517,6 +527,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_E = En;
   c->pn_nnz = nnz;
   c->pn_N = N;
+  c->pn_cache_serial = in.serial;
+  c->pn_cache_mode = mode;
   *n_events = En;
   *nnz_out = nnz;
   return CG_OK;

@@ -110,3 +110,34 @@ def test_device_resident_rules_same_result(eng):
             assert np.array_equal(o2, node_off) and np.array_equal(t2, time)
             assert np.array_equal(r2, rule)
         drules.free()
+
+
+def test_transpose_cache_keyed_by_rule_set_and_mode(eng):
+    """The rule->node join + transpose is reused across calls on the same
+    uploaded rule set and mode (time windows); switching rule set or mode, or
+    interleaving the host-array path, must never reuse a stale transpose."""
+    ra = synth.multi_rule_jobs(150, seed=41)
+    rb = synth.multi_rule_jobs(150, seed=42)
+    t0 = synth.T0_2026
+    fresh = {}
+    sps = {}
+    for name, rin in (("a", ra), ("b", rb)):
+        specs = synth.spec_mix(rin.n_rules, seed=9, mix=synth.MIX_LIGHT)
+        arr, _ = cron.parse_batch(specs)
+        sps[name] = eng.upload_c(arr, rin.n_rules)
+        for mode in (_lib.EXCLUDE_NONE, _lib.EXCLUDE_CUMULATIVE):
+            for w in range(2):
+                a = t0 + w * 3600
+                fresh[name, mode, w] = eng.expand_per_node(sps[name], None, a, a + 3600, rin, mode)
+    da, db = eng.upload_rules(ra), eng.upload_rules(rb)
+    order = [("a", 0, 0), ("a", 0, 1), ("b", 0, 0), ("a", 2, 1), ("a", 2, 0), ("a", 0, 1),
+             ("b", 2, 1), ("b", 2, 0)]
+    for name, mode, w in order:
+        rin, d = (ra, da) if name == "a" else (rb, db)
+        a = t0 + w * 3600
+        En, _ = eng.expand_per_node_rules_device(sps[name], None, a, a + 3600, d, mode)
+        got = eng.node_result(rin.n_nodes, En)
+        exp = fresh[name, mode, w]
+        assert all(np.array_equal(x, y) for x, y in zip(got, exp)), (name, mode, w)
+        if w == 1:  # the host-array path in between re-uploads its own rule set
+            eng.expand_per_node(sps[name], None, a, a + 3600, rin, mode)
