@@ -100,6 +100,7 @@ def main():
 
     from cronsun_amd import cron, shard, synth
     from cronsun_amd.engine import Engine
+    cdev_early = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
 
     wl = args.workload
     if args.cpu_sample is None:
@@ -124,31 +125,57 @@ def main():
         H = args.horizon or 86400
         mix = synth.MIX_CONFIG2
         seed = 0x5EED + 3 + rank
-    else:  # config4: 10M rules in total, job-ID-range shards
+    else:  # config4: 10M rules in total, job-ID-range shards balanced by events
         total = args.rules or 10_000_000
-        lo, hi = shard.shard_range(total, world, rank)
-        R = hi - lo
+        R = total
         H = args.horizon or 7 * 86400
         mix = synth.MIX_LIGHT
-        seed = 0x5EED + 4 + lo  # a shard's rules depend on its job-ID range only
+        seed = 0x5EED + 4
     t0 = synth.T0_2026
     t1 = t0 + H
     pn = wl in ("pernode", "config3")
     W = args.window or (3600 if wl == "config3" else H)
     xmode = {"none": 0, "rule": 1, "cumulative": 2}[args.exclude_mode]
     eng = Engine(local)
-    log(f"[rank {rank}] {wl}: generating {R} rules (job-ID shard {rank})")
-    if wl == "dispatch" and R > 1_000_000:
-        # the 1M-rule config-2 set tiled (Python generation of 10M strings
-        # takes minutes; entries are independent, so repeats change nothing)
-        base = synth.spec_mix(1_000_000, seed=seed, mix=mix)
-        specs = (base * (R // len(base) + 1))[:R]
-    else:
-        specs = synth.spec_mix(R, seed=seed, mix=mix)
-    arr, status = cron.parse_batch(specs, threads=16)
-    assert (status == 0).all()
-    sp = eng.upload_c(arr, R)
     utc = cron.UTC()
+    log(f"[rank {rank}] {wl}: generating {R} rules")
+    shard_info = None
+    if wl == "config4":
+        # the global 10M-rule set is the 1M-rule light-mix block tiled in
+        # job-ID order (rule i = block[i % 1M]), so any rank can build any range
+        base_n = min(total, 1_000_000)
+        base_arr, status = cron.parse_batch(synth.spec_mix(base_n, seed=seed, mix=mix), threads=16)
+        assert (status == 0).all()
+        base_np = np.ctypeslib.as_array(base_arr)
+
+        def upload_range(lo, hi):
+            a = np.ascontiguousarray(base_np[np.arange(lo, hi) % base_n])
+            return eng.upload_c((base_arr._type_ * (hi - lo)).from_buffer(a), hi - lo)
+
+        if world > 1:
+            # §8e: a cheap count pass over a provisional equal slice, one
+            # all-gather of per-block event sums, cuts of equal estimated events
+            tc = time.perf_counter()
+            lo, hi, _ = shard.event_balanced_range(
+                total, lambda a, b: eng.count(upload_range(a, b), utc, t0, t1), dist,
+                block=65536, device=cdev_early)
+            shard_info = {"lo": lo, "hi": hi, "count_pass_s": time.perf_counter() - tc}
+        else:
+            lo, hi = 0, total
+        R = hi - lo
+        sp = upload_range(lo, hi)
+        specs = None
+    else:
+        if wl == "dispatch" and R > 1_000_000:
+            # the 1M-rule config-2 set tiled (Python generation of 10M strings
+            # takes minutes; entries are independent, so repeats change nothing)
+            base = synth.spec_mix(1_000_000, seed=seed, mix=mix)
+            specs = (base * (R // len(base) + 1))[:R]
+        else:
+            specs = synth.spec_mix(R, seed=seed, mix=mix)
+        arr, status = cron.parse_batch(specs, threads=16)
+        assert (status == 0).all()
+        sp = eng.upload_c(arr, R)
     drules = None
     n_nodes = 10_000
     if pn:
@@ -296,6 +323,7 @@ def main():
             "t0": t0,
             "zone": "UTC",
             "events_per_gpu_step": E,
+            "shard": shard_info or {"lo": 0, "hi": R},
             "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard totals / per-node counts)",
         },
         "hbm_gbps_step": algo_bytes * world / (elapsed / args.steps) / 1e9,

@@ -469,8 +469,10 @@ int cg_lock_ttl_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int6
 }  // extern "C"
 
 // --------------------------------------------------------------- expansion
-int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
-                         int64_t* n_events) {
+// plan (cached) + k_count + scan of the run counts: c->run_off holds the run
+// offsets afterwards.  *empty = true when there is nothing to count.
+static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                       bool* empty) {
   HIPCHK(hipSetDevice(c->device));
   if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
     return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON");
@@ -497,8 +499,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   if (R == 0 || G == 0) {
     HIPCHK(hipMemsetAsync(c->offsets.p, 0, (R + 1) * 8, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    c->last_E = 0;
-    *n_events = 0;
+    *empty = true;
     return CG_OK;
   }
   const int64_t nruns = R * G;
@@ -516,6 +517,30 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   launch_scan(c->run_count.p, c->run_off.p, nruns, c->scan_tmp.p, c->st);
   (void)hipEventRecord(c->ev[2], c->st);
   HIPCHK(hipGetLastError());
+  *empty = false;
+  return CG_OK;
+}
+
+static int stuck_error(unsigned long long stuck) {
+  return cg_fail(CG_ERANGE, "rule " + std::to_string(stuck) +
+                                ": the reference Next loop never terminates inside this horizon "
+                                "(Next does not return, or returns a time <= its input and cycles)");
+}
+
+int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                         int64_t* n_events) {
+  bool empty = true;
+  int rc = count_phase(c, s, z, t0, t1, &empty);
+  if (rc) return rc;
+  if (empty) {
+    c->last_E = 0;
+    *n_events = 0;
+    return CG_OK;
+  }
+  const int64_t R = int64_t(s->n);
+  const PlanArgs& pa = c->pa;
+  const int64_t G = pa.G;
+  const int64_t nruns = R * G;
   // Write phase without a host round trip: the chunk map and writers read the
   // event total from device memory and size their work from it.  Output
   // capacity comes from earlier calls; the first call (or a larger result)
@@ -551,10 +576,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
     HIPCHK(hipMemcpyAsync(&E, c->run_off.p + nruns, 8, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipMemcpyAsync(&stuck, c->stuck.p, 8, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
-    if (stuck != ~0ULL)
-      return cg_fail(CG_ERANGE, "rule " + std::to_string(stuck) +
-                                    ": the reference Next loop never terminates inside this horizon "
-                                    "(Next does not return, or returns a time <= its input and cycles)");
+    if (stuck != ~0ULL) return stuck_error(stuck);
     if (E <= cap) break;
     if ((rc = c->times.ensure(E))) return rc;  // grow and redo the write phase
   }
@@ -566,6 +588,35 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   (void)hipEventElapsedTime(&c->kt[5], c->ev[6], c->ev[7]);
   c->last_E = E;
   *n_events = E;
+  return CG_OK;
+}
+
+extern "C" int cg_count(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                        int64_t* counts, int64_t* total) {
+  if (!c || !s || !z || !total || (s->n && !counts)) return cg_fail(CG_EINVAL, "cg_count: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  bool empty = true;
+  int rc = count_phase(c, s, z, t0, t1, &empty);
+  if (rc) return rc;
+  const int64_t R = int64_t(s->n);
+  if (empty) {
+    for (int64_t r = 0; r < R; r++) counts[r] = 0;
+    *total = 0;
+    return CG_OK;
+  }
+  launch_rule_offsets(c->run_off.p, R, int32_t(c->pa.G), c->offsets.p, c->st);
+  HIPCHK(hipGetLastError());
+  std::vector<int64_t> off(size_t(R) + 1);
+  unsigned long long stuck = 0;
+  HIPCHK(hipMemcpyAsync(off.data(), c->offsets.p, (R + 1) * 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(&stuck, c->stuck.p, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  if (stuck != ~0ULL) return stuck_error(stuck);
+  for (int64_t r = 0; r < R; r++) counts[r] = off[size_t(r) + 1] - off[size_t(r)];
+  *total = off[size_t(R)];
+  c->last_R = 0;  // no expansion result to read after a count
+  c->last_E = 0;
   return CG_OK;
 }
 

@@ -264,6 +264,15 @@ class Engine:
         check(lib().cg_result_copy_times(self._h, 0, n.value, times.ctypes.data))
         return off, times[:n.value]
 
+    def count(self, specs, loc, t0, t1):
+        """Fires per rule in (t0, t1] (count pass only, cg_count)."""
+        sp = self._specs(specs)
+        out = np.empty(max(sp.n, 1), dtype=np.int64)
+        tot = C.c_int64()
+        check(lib().cg_count(self._h, sp._h, self._loc(loc).handle, int(t0), int(t1),
+                             out.ctypes.data, C.byref(tot)))
+        return out[:sp.n]
+
     def expand_device(self, specs, loc, t0, t1):
         n = C.c_int64()
         check(lib().cg_expand_device(self._h, specs._h, self._loc(loc).handle, int(t0), int(t1),

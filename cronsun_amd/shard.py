@@ -5,6 +5,11 @@ with no data-path collective.  The only exchanges are small:
 
   global_offsets   all-gather of per-rank event totals -> each rank's base
                    offset in the global rule-major CSR
+  event_balanced_range
+                   the cheap count pass: each rank counts the fires of a
+                   provisional equal slice, the per-block sums are
+                   all-gathered, and every rank cuts the job-ID order into
+                   ranges of equal estimated events (block granularity)
   node_offsets     all-gather of per-node event counts (N int64 per rank) ->
                    offset[g][n] = node_base[n] + sum_{g' < g} count[g'][n], so
                    each node's global list keeps job-ID order across ranks
@@ -27,9 +32,50 @@ def shard_range(n_rules, world, rank, weights=None):
     w = np.asarray(weights, dtype=np.float64)
     c = np.concatenate([[0.0], np.cumsum(w)])
     total = c[-1]
-    cuts = [0] + [int(np.searchsorted(c, total * k / world, side="left")) for k in range(1, world)] + [n_rules]
+    def cut(target):  # the prefix boundary nearest to the target weight
+        k = int(np.searchsorted(c, target, side="left"))
+        if k > 0 and (k > n_rules or target - c[k - 1] <= c[k] - target):
+            return k - 1
+        return k
+    cuts = [0] + [cut(total * k / world) for k in range(1, world)] + [n_rules]
     cuts = np.maximum.accumulate(np.clip(cuts, 0, n_rules))
     return int(cuts[rank]), int(cuts[rank + 1])
+
+
+def provisional_blocks(n_rules, world, rank, block):
+    """[b0, b1) block range of an equal split in blocks of `block` rules."""
+    nb = (n_rules + block - 1) // block
+    return nb * rank // world, nb * (rank + 1) // world
+
+
+def event_balanced_range(n_rules, count_fn, dist, block=4096, device=None):
+    """This rank's [lo, hi) job-ID range with balanced estimated events.
+
+    count_fn(lo, hi) -> per-rule event counts of rules [lo, hi) (e.g.
+    Engine.count over the rank's provisional slice).  One all-gather of
+    ceil(blocks / world) int64 per rank; the cut is made at block
+    granularity, so every rank computes the same cuts and job-ID order is
+    kept.  Returns (lo, hi, global block weights)."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    nb = (n_rules + block - 1) // block
+    b0, b1 = provisional_blocks(n_rules, world, rank, block)
+    lo, hi = b0 * block, min(b1 * block, n_rules)
+    counts = np.asarray(count_fn(lo, hi), dtype=np.int64) if hi > lo else np.zeros(0, np.int64)
+    mine = np.zeros(b1 - b0, dtype=np.int64)
+    if hi > lo:
+        mine = np.add.reduceat(counts, np.arange(0, hi - lo, block))
+    width = (nb + world - 1) // world + 1
+    buf = torch.zeros(width, dtype=torch.int64, device=device)
+    buf[:len(mine)] = torch.from_numpy(mine).to(buf.device)
+    allw = torch.zeros(world * width, dtype=torch.int64, device=device)
+    dist.all_gather_into_tensor(allw, buf)
+    allw = allw.cpu().numpy().reshape(world, width)
+    weights = np.concatenate([allw[g, :provisional_blocks(n_rules, world, g, block)[1] -
+                                   provisional_blocks(n_rules, world, g, block)[0]]
+                              for g in range(world)])
+    c0, c1 = shard_range(nb, world, rank, weights=weights.astype(np.float64) + 1e-9)
+    return c0 * block, min(c1 * block, n_rules), weights
 
 
 def global_offsets(local_total, dist, device=None):

@@ -224,6 +224,13 @@ int cg_dispatcher_remove(cg_dispatcher* d, const int64_t* idx, size_t k);
 int cg_dispatcher_snapshot(const cg_dispatcher* d, int64_t* next, int64_t* prev, uint8_t* live);
 
 /* --------------------------------------------------------- expansion --- */
+/* counts[r] = number of fires of rule r in (t0, t1] (the expansion's count
+ * pass alone: plan + k_count + scan; no times are written), *total = their
+ * sum.  The cheap pass that balances job-ID-range shards by estimated events
+ * (SURVEY.md §8e).  Leaves no expansion result behind. */
+int cg_count(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0, int64_t t1,
+             int64_t* counts, int64_t* total);
+
 /* Fire times of every rule over (t0, t1]: for each rule,
  *   t = t0; loop { t = Next(t); if t.IsZero() || t > t1 break; emit t }
  * i.e. the reference Next loop, batched.  Output is a rule-major CSR:
