@@ -31,6 +31,7 @@
 // is sequential.
 #include <cstring>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -680,30 +681,40 @@ int cg_jobset_ingest_jobs(cg_jobset* js, const char* const* docs, const size_t* 
     if (nul) st[i] = CG_INGEST_UNSUPPORTED;
   });
   // jobs[job.ID] = job: the last valid value of an ID wins (job.go:353-364)
-  std::unordered_map<std::string, size_t> last;
+  std::unordered_map<std::string_view, size_t> last;
+  last.reserve(n);
   for (size_t i = 0; i < n; i++)
     if (st[i] == CG_INGEST_OK) last[jobs[i].id] = i;
+  js->node_idx.reserve(js->node_idx.size() + n / 4);
   for (size_t i = 0; i < n; i++) {
     if (st[i] != CG_INGEST_OK) continue;
-    if (last[jobs[i].id] != i) {
+    if (last.find(jobs[i].id)->second != i) {
       st[i] = CG_INGEST_REPLACED;
       continue;
     }
-    const PJob& j = jobs[i];
-    int rc = cg_jobset_add_job(js, j.id.c_str(), j.pause ? 1 : 0);
-    if (rc) return rc;
-    js->job_kind.back() = int32_t(j.kind);
-    js->job_avg.back() = j.avg_time;
-    js->job_parallels.back() = j.parallels;
+    PJob& j = jobs[i];
+    // cg_jobset_add_job + cg_jobset_add_rule, interning straight from the
+    // decoded strings
+    js->job_ids.push_back(j.id);  // (j.id backs a key of `last`: copied, not moved)
+    js->job_pause.push_back(j.pause ? 1 : 0);
+    js->job_first_rule.push_back(int32_t(js->rule_ids.size()));
+    js->job_kind.push_back(int32_t(j.kind));
+    js->job_avg.push_back(j.avg_time);
+    js->job_parallels.push_back(j.parallels);
+    const int32_t job = int32_t(js->job_ids.size()) - 1;
     for (size_t k = 0; k < j.rules.len; k++) {
-      const PRule& r = j.pool[size_t(j.rules.backing[k])];
-      auto g = visible(r.gids), nn = visible(r.nids), ex = visible(r.ex);
-      auto cg = cstrs(g), cn = cstrs(nn), ce = cstrs(ex);
-      rc = cg_jobset_add_rule(js, r.id.c_str(), cg.data(), cg.size(), cn.data(), cn.size(),
-                              ce.data(), ce.size());
-      if (rc) return rc;
-      js->rule_sched.back() = sched[i][k];
-      js->rule_has_sched.back() = 1;
+      PRule& r = j.pool[size_t(j.rules.backing[k])];
+      js->rule_ids.push_back(std::move(r.id));
+      js->rule_job.push_back(job);
+      std::vector<int32_t> a(r.gids.len), b(r.nids.len), c(r.ex.len);
+      for (size_t q = 0; q < r.gids.len; q++) a[q] = js->group(r.gids.backing[q]);
+      for (size_t q = 0; q < r.nids.len; q++) b[q] = js->node(r.nids.backing[q]);
+      for (size_t q = 0; q < r.ex.len; q++) c[q] = js->node(r.ex.backing[q]);
+      js->r_gids.push_back(std::move(a));
+      js->r_nids.push_back(std::move(b));
+      js->r_ex.push_back(std::move(c));
+      js->rule_sched.push_back(sched[i][k]);
+      js->rule_has_sched.push_back(1);
     }
   }
   if (status) std::copy(st.begin(), st.end(), status);

@@ -31,6 +31,24 @@ struct cg_jobset {
   std::vector<int64_t> f_group_off, f_nid_off, f_gid_off, f_ex_off;
   std::vector<int32_t> f_group_nodes, f_nids, f_gids, f_ex;
 
+  int32_t node(const std::string& id) {
+    auto it = node_idx.find(id);
+    if (it != node_idx.end()) return it->second;
+    int32_t k = int32_t(node_ids.size());
+    node_ids.push_back(id);
+    node_idx.emplace(id, k);
+    return k;
+  }
+  int32_t group(const std::string& id) {
+    auto it = group_idx.find(id);
+    if (it != group_idx.end()) return it->second;
+    int32_t k = int32_t(group_ids.size());
+    group_ids.push_back(id);
+    group_idx.emplace(id, k);
+    group_nodes.emplace_back();
+    group_exists.push_back(0);
+    return k;
+  }
   int32_t node(const char* id) {
     auto it = node_idx.find(id);
     if (it != node_idx.end()) return it->second;
