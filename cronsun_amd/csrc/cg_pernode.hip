@@ -189,11 +189,6 @@ __global__ void k_pair_block_map(const int64_t* __restrict__ pair_pos, int64_t n
   task_pair[b] = b == ntasks ? nnz - 1 : search_le(pair_pos, 0, nnz - 1, b * int64_t(kNodeTask));
 }
 
-#ifndef CG_NODE_UNROLL
-#define CG_NODE_UNROLL 1
-#endif
-constexpr int kNodeUnroll = CG_NODE_UNROLL;
-
 __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
   const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), i));
   const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v) >> 32)), i));
@@ -206,8 +201,8 @@ __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
 // the rule's fire-list start) and fills its task in aligned 64-event blocks:
 // lane l finds the pair of event b + l by a 6-step shuffle search, gathers the
 // fire time (rule lists are re-read once per node of the rule: L2/MALL hits)
-// and the block is stored whole (8-B times, 4-B rule indices).  kNodeUnroll
-// blocks per round keep that many independent searches and gathers in flight.
+// and the block is stored whole (8-B times, 4-B rule indices).  (Two blocks
+// per round with independent searches measured slower: 7 waves per SIMD.)
 // (A wave-uniform walk over the pairs instead of the search measured 1.5x
 // slower: ~10 fires per pair make the per-pair readlane chain the bottleneck.)
 template <int V>
@@ -263,55 +258,51 @@ __global__ __launch_bounds__(256) void k_node_write(
     };
     fetch(jw);
     load();
-    for (int64_t b = B0; b < B1; b += 64 * kNodeUnroll) {
-      int64_t e[kNodeUnroll], val[kNodeUnroll];
-      int32_t rv[kNodeUnroll];
-      bool done[kNodeUnroll];
+    // jc: window lane of the pair that holds event b (wave-uniform), -1 when
+    // unknown.  A full block inside that one pair (long fire lists: second-
+    // granularity and frequent @every rules carry most node events) needs no
+    // search: one uniform shift, a coalesced 512-B read and the stores.
+    int jc = -1;
+    for (int64_t b = B0; b < B1; b += 64) {
+      const int64_t e = b + lane;
+      int64_t val = 0;
+      int32_t rv = 0;
+      if (jc >= 0 && b + 64 <= B1 && rl64n(dend, jc) >= b + 64) {
+        const int64_t d = rl64n(delta, jc);
+        val = (V & 1) ? e + d : times[e + d];
+        rv = __builtin_amdgcn_readlane(rr, jc);
+      } else {
+        bool done = e >= B1;
+        int j = 0;
+        for (;;) {
+          const int L = 63 - __builtin_clzll(__ballot(dst != INT32_MAX));
+          const int64_t wend = rl64n(dend, L);
+          j = 0;
 #pragma unroll
-      for (int u = 0; u < kNodeUnroll; u++) {
-        e[u] = b + 64 * u + lane;
-        done[u] = e[u] >= B1;
-        val[u] = 0;
-        rv[u] = 0;
-      }
-      for (;;) {
-        const int L = 63 - __builtin_clzll(__ballot(dst != INT32_MAX));
-        const int64_t wend = rl64n(dend, L);
-        int j[kNodeUnroll];
-#pragma unroll
-        for (int u = 0; u < kNodeUnroll; u++) j[u] = 0;
-#pragma unroll
-        for (int st = 32; st > 0; st >>= 1) {
-#pragma unroll
-          for (int u = 0; u < kNodeUnroll; u++) {
-            const int32_t v = __shfl(dst, (j[u] + st) & 63, 64);
-            if (j[u] + st < 64 && int64_t(v) <= e[u] - B0) j[u] += st;
+          for (int st = 32; st > 0; st >>= 1) {
+            const int32_t v = __shfl(dst, (j + st) & 63, 64);
+            if (j + st < 64 && int64_t(v) <= e - B0) j += st;
           }
-        }
-        bool pending = false;
-#pragma unroll
-        for (int u = 0; u < kNodeUnroll; u++) {
-          const int64_t jdelta = __shfl(delta, j[u], 64);
-          const int32_t jr = __shfl(rr, j[u], 64);
-          if (!done[u] && e[u] < wend) {
-            val[u] = (V & 1) ? e[u] + jdelta : times[e[u] + jdelta];
-            rv[u] = jr;
-            done[u] = true;
+          const int64_t jdelta = __shfl(delta, j, 64);
+          const int32_t jr = __shfl(rr, j, 64);
+          if (!done && e < wend) {
+            val = (V & 1) ? e + jdelta : times[e + jdelta];
+            rv = jr;
+            done = true;
           }
-          pending |= !done[u];
+          if (__ballot(!done) == 0) break;
+          jw += 64;  // some lane's event lies past the window's last pair
+          load();
         }
-        if (__ballot(pending) == 0) break;
-        jw += 64;  // some lane's event lies past the window's last pair
-        load();
+        // the pair of the block's last event, in the final window (a full
+        // block's lane 63 is found in the last window visited)
+        jc = b + 64 <= B1 ? __builtin_amdgcn_readlane(j, 63) : -1;
       }
-#pragma unroll
-      for (int u = 0; u < kNodeUnroll; u++) {
-        if (V & 2) {
-          asm volatile("" ::"v"(val[u]), "v"(rv[u]));
-        } else if (e[u] < B1) {
-          out_time[e[u]] = val[u];
-          out_rule[e[u]] = rv[u];
-        }
+      if (V & 2) {
+        asm volatile("" ::"v"(val), "v"(rv));
+      } else if (e < B1) {
+        out_time[e] = val;
+        out_rule[e] = rv;
       }
     }
   }
