@@ -509,8 +509,10 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   if ((rc = c->run_off.ensure(nruns + 1))) return rc;
   if ((rc = c->scan_tmp.ensure(scan_temp_bytes(nruns)))) return rc;
 
-  if ((rc = c->stuck.ensure(1))) return rc;
-  HIPCHK(hipMemsetAsync(c->stuck.p, 0xFF, sizeof(unsigned long long), c->st));
+  if ((rc = c->stuck.ensure(1)) || (rc = c->res.ensure(2))) return rc;
+  if (!c->res_host) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->res_host), 16));
+  if (!c->stuck_armed) HIPCHK(hipMemsetAsync(c->stuck.p, 0xFF, sizeof(unsigned long long), c->st));
+  c->stuck_armed = false;  // until a k_rule_offsets of this call re-arms it
   (void)hipEventRecord(c->ev[0], c->st);
   launch_count(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->stuck.p, c->st);
   (void)hipEventRecord(c->ev[1], c->st);
@@ -570,12 +572,14 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
       launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p,
                         c->run_off.p, cap, c->times.p, c->st);
     (void)hipEventRecord(c->ev[6], c->st);
-    launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->st);
+    launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->res.p, c->stuck.p, c->st);
     (void)hipEventRecord(c->ev[7], c->st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(&E, c->run_off.p + nruns, 8, hipMemcpyDeviceToHost, c->st));
-    HIPCHK(hipMemcpyAsync(&stuck, c->stuck.p, 8, hipMemcpyDeviceToHost, c->st));
+    HIPCHK(hipMemcpyAsync(c->res_host, c->res.p, 16, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
+    c->stuck_armed = true;
+    E = c->res_host[0];
+    stuck = static_cast<unsigned long long>(c->res_host[1]);
     if (stuck != ~0ULL) return stuck_error(stuck);
     if (E <= cap) break;
     if ((rc = c->times.ensure(E))) return rc;  // grow and redo the write phase
@@ -605,13 +609,14 @@ extern "C" int cg_count(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t 
     *total = 0;
     return CG_OK;
   }
-  launch_rule_offsets(c->run_off.p, R, int32_t(c->pa.G), c->offsets.p, c->st);
+  launch_rule_offsets(c->run_off.p, R, int32_t(c->pa.G), c->offsets.p, c->res.p, c->stuck.p, c->st);
   HIPCHK(hipGetLastError());
   std::vector<int64_t> off(size_t(R) + 1);
-  unsigned long long stuck = 0;
   HIPCHK(hipMemcpyAsync(off.data(), c->offsets.p, (R + 1) * 8, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipMemcpyAsync(&stuck, c->stuck.p, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipMemcpyAsync(c->res_host, c->res.p, 16, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
+  c->stuck_armed = true;
+  const unsigned long long stuck = static_cast<unsigned long long>(c->res_host[1]);
   if (stuck != ~0ULL) return stuck_error(stuck);
   for (int64_t r = 0; r < R; r++) counts[r] = off[size_t(r) + 1] - off[size_t(r)];
   *total = off[size_t(R)];

@@ -91,7 +91,10 @@ struct cg_ctx {
   DBuf<int32_t> run_count, lt_kind;
   DBuf<uint32_t> run_dmask;
   DBuf<char> scan_tmp;
-  DBuf<unsigned long long> stuck;
+  DBuf<unsigned long long> stuck;  // ~0 between calls (k_rule_offsets re-arms it)
+  bool stuck_armed = false;        // false: memset it before the next k_count
+  DBuf<int64_t> res;               // {event total, stuck rule} of the last expansion
+  int64_t* res_host = nullptr;     // pinned 16 B: one async D2H read per call
   int64_t last_E = 0, last_R = 0, last_G = 0;
 
   // per-node buffers
@@ -109,7 +112,9 @@ struct cg_ctx {
     plan_dev.release();
     run_anchor.release(); run_off.release(); offsets.release(); times.release();
     block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
-    lt_avg.release(); lt_kind.release();
+    lt_avg.release(); lt_kind.release(); res.release();
+    if (res_host) (void)hipHostFree(res_host);
+    res_host = nullptr;
     run_dmask.release(); scan_tmp.release(); stuck.release();
     rn_off.release(); rn_cnt64.release(); pair_pos.release(); pair_src.release(); node_off.release();
     node_time.release(); nt_off.release(); rn_cnt.release(); rn_nodes.release();

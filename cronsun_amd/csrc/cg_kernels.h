@@ -87,6 +87,6 @@ void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const i
                        int64_t cap, int64_t* times, hipStream_t st);
 
 void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,
-                         hipStream_t st);
+                         int64_t* res, unsigned long long* stuck, hipStream_t st);
 
 }  // namespace cg

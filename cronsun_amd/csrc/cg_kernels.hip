@@ -1021,10 +1021,19 @@ __global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ sp
   }
 }
 
+// Rule-major CSR offsets; thread 0 also hands the host the event total and
+// the stuck-rule flag in one 16-B record and re-arms the flag for the next
+// call (no separate reads, no memset before k_count).
 __global__ void k_rule_offsets(const int64_t* __restrict__ run_off, int64_t R, int32_t G,
-                               int64_t* __restrict__ offsets) {
+                               int64_t* __restrict__ offsets, int64_t* __restrict__ res,
+                               unsigned long long* __restrict__ stuck) {
   int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
   if (r <= R) offsets[r] = run_off[r * G];
+  if (r == 0) {
+    res[0] = run_off[R * G];
+    res[1] = int64_t(*stuck);
+    *stuck = ~0ull;
+  }
 }
 
 int grid_for(int64_t n, int threads, int max_blocks) {
@@ -1225,9 +1234,9 @@ void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const i
 }
 
 void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,
-                         hipStream_t st) {
+                         int64_t* res, unsigned long long* stuck, hipStream_t st) {
   hipLaunchKernelGGL(k_rule_offsets, dim3(grid_for(R + 1, 256, 1 << 30)), dim3(256), 0, st,
-                     run_off, R, G, offsets);
+                     run_off, R, G, offsets, res, stuck);
 }
 
 }  // namespace cg
