@@ -250,6 +250,31 @@ def main():
     elapsed = time.perf_counter() - start
     wake["loop_s"], wake["tail_s"] = t_loop, elapsed - t_loop
 
+    e2e = None
+    if wl == "config2":
+        # end to end, outside the timed region: H2D of the
+        # packed specs, the expansion, D2H of the rule-major CSR into pinned
+        # host memory (the host parse is reported by the CPU baseline)
+        from cronsun_amd._lib import check as _check, lib as _cglib
+        host_times = torch.empty(E, dtype=torch.int64, pin_memory=True)
+        host_off = torch.empty(R + 1, dtype=torch.int64, pin_memory=True)
+        torch.cuda.synchronize()
+        te = time.perf_counter()
+        sp2 = eng.upload_c(arr, R)
+        t_h2d = time.perf_counter() - te
+        E2 = eng.expand_device(sp2, utc, t0, t1)
+        t_exp = time.perf_counter() - te - t_h2d
+        _check(_cglib().cg_result_copy_offsets(eng._h, host_off.data_ptr()))
+        _check(_cglib().cg_result_copy_times(eng._h, 0, E2, host_times.data_ptr()))
+        t_all = time.perf_counter() - te
+        assert E2 == E and int(host_off[-1]) == E
+        e2e = {"ms": t_all * 1e3, "h2d_specs_ms": t_h2d * 1e3, "expand_ms": t_exp * 1e3,
+               "d2h_csr_ms": (t_all - t_h2d - t_exp) * 1e3,
+               "d2h_gbps": (E + R + 1) * 8 / max(t_all - t_h2d - t_exp, 1e-9) / 1e9,
+               "events_per_s": E / t_all}
+        sp2.free()
+        del host_times, host_off
+
     el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
     ev = torch.tensor([E], dtype=torch.int64, device=cdev)
     if world > 1:
@@ -341,6 +366,8 @@ def main():
         },
         "cpu_baseline": cpu,
     }
+    if e2e is not None:
+        out["end_to_end_rank0"] = e2e
     if pn:
         out["kernel_ms"].update({"rule_node_join": nkt[0], "transpose": nkt[1], "node_write": nkt[2]})
         out["config"]["nnz_rule_node_pairs"] = last["nnz"]
