@@ -14,6 +14,10 @@ with no data-path collective.  The only exchanges are small:
                    offset[g][n] = node_base[n] + sum_{g' < g} count[g'][n], so
                    each node's global list keeps job-ID order across ranks
 
+  gather_csr       the optional second collective: every rank's slice of the
+                   rule-major CSR to rank 0 with grouped point-to-point
+                   send/recv (variable sizes; xGMI: one link per peer)
+
 Works with torch.distributed over RCCL ("nccl", one process per MI355X) and
 over gloo on CPU (tests).
 """
@@ -107,3 +111,48 @@ def node_offsets(local_counts, dist):
     node_base[1:] = torch.cumsum(per_node_total, dim=0)
     before = allc[:r].sum(dim=0) if r > 0 else torch.zeros(N, dtype=torch.int64, device=local_counts.device)
     return node_base[:-1] + before, node_base
+
+
+def gather_csr(local_offsets, local_times, dist, dst=0):
+    """Gather the job-ID-ordered rule-major CSR on rank `dst`.
+
+    local_offsets: int64 tensor [R_local + 1] (starting at 0), local_times:
+    int64 tensor [E_local], on the collective's device.  Returns (offsets
+    [R + 1], times [E]) on `dst` (None elsewhere).  Sizes are exchanged with
+    one all-gather; the payload moves with batched isend/irecv, each peer
+    straight into its slice of the destination buffers."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = local_times.device
+    sizes = torch.tensor([local_offsets.numel() - 1, local_times.numel()], dtype=torch.int64, device=dev)
+    alls = torch.zeros(world * 2, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(alls, sizes)
+    alls = alls.view(world, 2).cpu().numpy()
+    if rank != dst:
+        ops = [dist.P2POp(dist.isend, local_offsets.contiguous(), dst),
+               dist.P2POp(dist.isend, local_times.contiguous(), dst)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        return None
+    R, E = int(alls[:, 0].sum()), int(alls[:, 1].sum())
+    offsets = torch.zeros(R + 1, dtype=torch.int64, device=dev)
+    times = torch.empty(E, dtype=torch.int64, device=dev)
+    rbase = np.concatenate([[0], np.cumsum(alls[:, 0])])
+    ebase = np.concatenate([[0], np.cumsum(alls[:, 1])])
+    recv_off, ops = {}, []
+    for g in range(world):
+        if g == dst:
+            continue
+        recv_off[g] = torch.empty(int(alls[g, 0]) + 1, dtype=torch.int64, device=dev)
+        ops.append(dist.P2POp(dist.irecv, recv_off[g], g))
+        ops.append(dist.P2POp(dist.irecv, times[int(ebase[g]):int(ebase[g + 1])], g))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    for g in range(world):
+        lo = int(rbase[g])
+        part = local_offsets if g == dst else recv_off[g]
+        if g == dst:
+            times[int(ebase[g]):int(ebase[g + 1])] = local_times
+        offsets[lo:lo + int(alls[g, 0]) + 1] = part + int(ebase[g])
+    return offsets, times

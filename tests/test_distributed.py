@@ -45,8 +45,11 @@ def _worker(rank, world, port, outdir):
     for k, r in enumerate(range(lo, hi)):
         counts[r % N] += int(off[k + 1] - off[k])
     my_off, node_base = shard.node_offsets(counts, dist)
+    g = shard.gather_csr(torch.from_numpy(off.astype(np.int64)), torch.from_numpy(times.astype(np.int64)),
+                         dist)
+    extra = {} if g is None else {"g_off": g[0].numpy(), "g_times": g[1].numpy()}
     np.savez(os.path.join(outdir, f"r{rank}.npz"), off=off, times=times, base=base, total=total,
-             lo=lo, hi=hi, my_off=my_off.numpy(), node_base=node_base.numpy())
+             lo=lo, hi=hi, my_off=my_off.numpy(), node_base=node_base.numpy(), **extra)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -77,6 +80,9 @@ def test_two_rank_gloo_stitch(tmp_path):
     assert np.array_equal(stitched, times)
     stitched_off = np.concatenate([r0["off"][:-1], r1["off"] + r0["off"][-1]])
     assert np.array_equal(stitched_off, off)
+    # the optional CSR gather to rank 0 (grouped point-to-point)
+    assert np.array_equal(r0["g_off"], off) and np.array_equal(r0["g_times"], times)
+    assert "g_off" not in r1
     # per-node offsets: rank 1's slice of node n starts after rank 0's
     N = 7
     cnt = np.zeros(N, dtype=np.int64)
