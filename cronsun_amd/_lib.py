@@ -127,6 +127,7 @@ def _declare(L):
         "cg_result_copy_times": ([vp, i64, i64, vp], C.c_int),
         "cg_result_copy_offsets": ([vp, vp], C.c_int),
         "cg_last_kernel_times": ([vp, P(C.c_float), C.c_int], C.c_int),
+        "cg_set_phase_timing": ([vp, C.c_int], C.c_int),
         "cg_expand_per_node": ([vp, vp, vp, i64, i64, P(cg_rules_in), C.c_int, P(cg_node_csr)], C.c_int),
         "cg_expand_per_node_device": ([vp, vp, vp, i64, i64, P(cg_rules_in), C.c_int, P(i64), P(i64)], C.c_int),
         "cg_node_result_device": ([vp, P(vp), P(vp), P(vp), P(i64)], C.c_int),

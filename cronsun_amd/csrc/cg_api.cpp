@@ -513,11 +513,12 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   if (!c->res_host) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->res_host), 16));
   if (!c->stuck_armed) HIPCHK(hipMemsetAsync(c->stuck.p, 0xFF, sizeof(unsigned long long), c->st));
   c->stuck_armed = false;  // until a k_rule_offsets of this call re-arms it
-  (void)hipEventRecord(c->ev[0], c->st);
+  const bool all_phases = c->phase_timing >= 2;
+  if (all_phases) (void)hipEventRecord(c->ev[0], c->st);
   launch_count(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->stuck.p, c->st);
-  (void)hipEventRecord(c->ev[1], c->st);
+  if (all_phases) (void)hipEventRecord(c->ev[1], c->st);
   launch_scan(c->run_count.p, c->run_off.p, nruns, c->scan_tmp.p, c->st);
-  (void)hipEventRecord(c->ev[2], c->st);
+  if (all_phases) (void)hipEventRecord(c->ev[2], c->st);
   HIPCHK(hipGetLastError());
   *empty = false;
   return CG_OK;
@@ -555,6 +556,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   }
   // walked runs: WALK windows, or CF segments whose entry fire does not fully
   // match (only possible when the plan has zone transitions)
+  const bool all_phases = c->phase_timing >= 2;
   bool has_walk = c->plan.table.when.size() > 1;
   for (const Segment& sg : c->plan.segs) has_walk |= sg.kind != 0;
   int64_t E = 0;
@@ -562,7 +564,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(c->times.cap);
     if ((rc = c->block_run.ensure(cap / kSuper + 2 + kTicketWords + 8))) return rc;
-    (void)hipEventRecord(c->ev[3], c->st);
+    if (all_phases) (void)hipEventRecord(c->ev[3], c->st);
     launch_chunk_map(c->run_off.p, nruns, cap, c->block_run.p, c->st);
     (void)hipEventRecord(c->ev[4], c->st);
     launch_write_cf(s->d, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->run_off.p, nruns,
@@ -571,9 +573,9 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
     if (has_walk)
       launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p,
                         c->run_off.p, cap, c->times.p, c->st);
-    (void)hipEventRecord(c->ev[6], c->st);
+    if (all_phases) (void)hipEventRecord(c->ev[6], c->st);
     launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->res.p, c->stuck.p, c->st);
-    (void)hipEventRecord(c->ev[7], c->st);
+    if (all_phases) (void)hipEventRecord(c->ev[7], c->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->res_host, c->res.p, 16, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -584,12 +586,16 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
     if (E <= cap) break;
     if ((rc = c->times.ensure(E))) return rc;  // grow and redo the write phase
   }
-  (void)hipEventElapsedTime(&c->kt[0], c->ev[0], c->ev[1]);
-  (void)hipEventElapsedTime(&c->kt[1], c->ev[1], c->ev[2]);
-  (void)hipEventElapsedTime(&c->kt[2], c->ev[3], c->ev[4]);
   (void)hipEventElapsedTime(&c->kt[3], c->ev[4], c->ev[5]);
-  (void)hipEventElapsedTime(&c->kt[4], c->ev[5], c->ev[6]);
-  (void)hipEventElapsedTime(&c->kt[5], c->ev[6], c->ev[7]);
+  if (all_phases) {
+    (void)hipEventElapsedTime(&c->kt[0], c->ev[0], c->ev[1]);
+    (void)hipEventElapsedTime(&c->kt[1], c->ev[1], c->ev[2]);
+    (void)hipEventElapsedTime(&c->kt[2], c->ev[3], c->ev[4]);
+    (void)hipEventElapsedTime(&c->kt[4], c->ev[5], c->ev[6]);
+    (void)hipEventElapsedTime(&c->kt[5], c->ev[6], c->ev[7]);
+  } else {
+    c->kt[0] = c->kt[1] = c->kt[2] = c->kt[4] = c->kt[5] = -1.f;
+  }
   c->last_E = E;
   *n_events = E;
   return CG_OK;
@@ -678,6 +684,13 @@ int cg_result_copy_offsets(cg_ctx* c, int64_t* host) {
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemcpy(host, c->offsets.p, (c->last_R + 1) * 8, hipMemcpyDeviceToHost));
+  return CG_OK;
+}
+
+int cg_set_phase_timing(cg_ctx* c, int level) {
+  if (!c || level < 1 || level > 2) return cg_fail(CG_EINVAL, "cg_set_phase_timing: level 1 or 2");
+  std::lock_guard<std::mutex> g(c->mu);
+  c->phase_timing = level;
   return CG_OK;
 }
 

@@ -76,6 +76,11 @@ struct cg_ctx {
   // offsets, k_node_write) of the last per-node call, [9..11] dispatcher
   // wake (scan, due compaction, advance) of the last cg_dispatcher_fire
   float kt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // expansion phase timing: 2 = an event between every phase (kt[0..5]);
+  // 1 = events around k_write_cf only (kt[3]; the others read -1).  Each
+  // event recorded between two kernels costs 6-12 us of idle GPU on this
+  // stack, so throughput runs use 1 (cg_set_phase_timing).
+  int phase_timing = 2;
 
   // plan cache
   cg::Plan plan;

@@ -296,6 +296,11 @@ class Engine:
         k = lib().cg_last_kernel_times(self._h, buf, 12)
         return list(buf)[:min(k, 6)]
 
+    def set_phase_timing(self, level):
+        """2: HIP events between all expansion phases (default); 1: around
+        k_write_cf only (the other phases then read -1)."""
+        check(lib().cg_set_phase_timing(self._h, int(level)))
+
     def node_kernel_times(self):
         """ms per phase of the last per-node call: rule->node join,
         transpose + per-node offsets, per-node write."""

@@ -266,6 +266,11 @@ int cg_result_copy_offsets(cg_ctx* ctx, int64_t* host_offsets /* [R+1] */);
  * dispatcher wake: [9] scan, [10] due compaction, [11] advance.  n = entries
  * written. */
 int cg_last_kernel_times(cg_ctx* ctx, float* ms, int n);
+/* Expansion phase timing: 2 (default) = a HIP event between every phase;
+ * 1 = events around k_write_cf only ([3]; [0..2], [4], [5] read -1).  Events
+ * recorded between kernels leave the GPU idle for several us each, so
+ * throughput measurements use 1.  (No reference counterpart: instrumentation.) */
+int cg_set_phase_timing(cg_ctx* ctx, int level);
 
 /* --------------------------------------------- rule -> node resolution --- */
 /* Integer-interned jobs/groups (host interns string IDs; see cg_jobset_*).

@@ -166,3 +166,25 @@ def test_plan_cache_survives_other_entry_points(eng):
     eng.lock_ttl_batch(sp, product_zone("Pacific/Apia"), t0, 0, 0)
     again = eng.expand(sp, ny, t0, t0 + 3 * DAY)
     assert np.array_equal(first[0], again[0]) and np.array_equal(first[1], again[1])
+
+
+def test_lean_phase_timing_same_result(eng):
+    """cg_set_phase_timing(1) drops the events between phases (throughput
+    runs): the result is unchanged, k_write_cf is still timed and the
+    untimed phases read -1."""
+    rng = np.random.default_rng(12)
+    scheds = [cron.Parse(random_spec(rng)) for _ in range(2000)]
+    sp = eng.upload(scheds)
+    ny = product_zone("America/New_York")
+    t0 = 1772900000
+    full = eng.expand(sp, ny, t0, t0 + 2 * DAY)
+    eng.set_phase_timing(1)
+    try:
+        lean = eng.expand(sp, ny, t0, t0 + 2 * DAY)
+        kt = eng.kernel_times()
+    finally:
+        eng.set_phase_timing(2)
+    assert np.array_equal(full[0], lean[0]) and np.array_equal(full[1], lean[1])
+    assert kt[3] > 0 and kt[0] == kt[1] == kt[2] == kt[4] == kt[5] == -1
+    with pytest.raises(_lib.CgError):
+        eng.set_phase_timing(3)
