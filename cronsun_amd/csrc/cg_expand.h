@@ -221,7 +221,9 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
       if (e <= b) {
         cnt = 1 + cf_count(c, sg, dm, e, b);
         anchor = e;
-        pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
+        // the run's last fire starts the next segment's search (not needed
+        // after the last segment: one closed-form seek saved per rule)
+        if (s + 1 < G) pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
       } else {
         dm = 0;  // no fire in this segment; the next one searches from its start
       }
@@ -235,7 +237,9 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
         dm = seg_daymask(sp, sg, dtab);
         cnt = 1 + cf_count(c, sg, dm, e, b);
         anchor = e;
-        pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
+        // the run's last fire starts the next segment's search (not needed
+        // after the last segment: one closed-form seek saved per rule)
+        if (s + 1 < G) pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
       } else {
         // walked run: a WALK segment, or a CF segment entered by a fire the
         // closed form cannot continue from
