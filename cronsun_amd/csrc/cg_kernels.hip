@@ -351,6 +351,7 @@ __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, 
 constexpr int kScanThreads = 256;
 constexpr int kScanPerThread = 16;
 constexpr int kScanTile = kScanThreads * kScanPerThread;
+constexpr int64_t kScanFuseTiles = 1024;  // up to 4M elements: carries summed per block
 
 __device__ __forceinline__ int64_t wave_incl_scan(int64_t x) {
   const int lane = threadIdx.x & 63;
@@ -407,10 +408,23 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_top(int64_t* __restrict__
   }
 }
 
+// kFused: the tile's carry is the sum of the earlier tiles' totals, summed by
+// the block itself (no k_scan_top launch; used while nb <= kScanFuseTiles)
+template <bool kFused>
 __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __restrict__ in,
                                                               int64_t n,
                                                               const int64_t* __restrict__ partial,
                                                               int64_t* __restrict__ out) {
+  int64_t carry;
+  if (kFused) {
+    int64_t x = 0;
+    for (int64_t i = threadIdx.x; i < int64_t(blockIdx.x); i += kScanThreads) x += partial[i];
+    int64_t all;
+    block_excl_scan(x, &all);
+    carry = all;
+  } else {
+    carry = partial[blockIdx.x];
+  }
   int64_t base = int64_t(blockIdx.x) * kScanTile + int64_t(threadIdx.x) * kScanPerThread;
   int32_t v[kScanPerThread];
   int64_t acc = 0;
@@ -421,7 +435,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __re
     acc += v[i];
   }
   int64_t tot;
-  int64_t run = partial[blockIdx.x] + block_excl_scan(acc, &tot);
+  int64_t run = carry + block_excl_scan(acc, &tot);
   if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
 #pragma unroll
   for (int i = 0; i < kScanPerThread; i++) {
@@ -1133,8 +1147,12 @@ void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStre
   int64_t nb = (n + kScanTile - 1) / kScanTile;
   int64_t* partial = static_cast<int64_t*>(temp);
   hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial);
+  if (nb <= kScanFuseTiles) {
+    hipLaunchKernelGGL(k_scan_apply<true>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out);
+    return;
+  }
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanThreads), 0, st, partial, nb);
-  hipLaunchKernelGGL(k_scan_apply, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out);
+  hipLaunchKernelGGL(k_scan_apply<false>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out);
 }
 
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
