@@ -512,12 +512,13 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   if ((rc = c->stuck.ensure(1)) || (rc = c->res.ensure(2))) return rc;
   if (!c->res_host) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->res_host), 16));
   if (!c->stuck_armed) HIPCHK(hipMemsetAsync(c->stuck.p, 0xFF, sizeof(unsigned long long), c->st));
-  c->stuck_armed = false;  // until a k_rule_offsets of this call re-arms it
+  c->stuck_armed = false;  // until this call's scan re-arms it
   const bool all_phases = c->phase_timing >= 2;
   if (all_phases) (void)hipEventRecord(c->ev[0], c->st);
   launch_count(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->stuck.p, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[1], c->st);
-  launch_scan(c->run_count.p, c->run_off.p, nruns, c->scan_tmp.p, c->st);
+  launch_scan_runs(c->run_count.p, c->run_off.p, R, int32_t(G), c->scan_tmp.p, c->offsets.p, c->res.p,
+                   c->stuck.p, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[2], c->st);
   HIPCHK(hipGetLastError());
   *empty = false;
@@ -574,8 +575,6 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
       launch_write_walk(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p,
                         c->run_off.p, cap, c->times.p, c->st);
     if (all_phases) (void)hipEventRecord(c->ev[6], c->st);
-    launch_rule_offsets(c->run_off.p, R, int32_t(G), c->offsets.p, c->res.p, c->stuck.p, c->st);
-    if (all_phases) (void)hipEventRecord(c->ev[7], c->st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->res_host, c->res.p, 16, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
@@ -592,7 +591,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
     (void)hipEventElapsedTime(&c->kt[1], c->ev[1], c->ev[2]);
     (void)hipEventElapsedTime(&c->kt[2], c->ev[3], c->ev[4]);
     (void)hipEventElapsedTime(&c->kt[4], c->ev[5], c->ev[6]);
-    (void)hipEventElapsedTime(&c->kt[5], c->ev[6], c->ev[7]);
+    c->kt[5] = 0.f;  // per-rule offsets: written by the scan (k_scan_apply)
   } else {
     c->kt[0] = c->kt[1] = c->kt[2] = c->kt[4] = c->kt[5] = -1.f;
   }
@@ -615,7 +614,6 @@ extern "C" int cg_count(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t 
     *total = 0;
     return CG_OK;
   }
-  launch_rule_offsets(c->run_off.p, R, int32_t(c->pa.G), c->offsets.p, c->res.p, c->stuck.p, c->st);
   HIPCHK(hipGetLastError());
   std::vector<int64_t> off(size_t(R) + 1);
   HIPCHK(hipMemcpyAsync(off.data(), c->offsets.p, (R + 1) * 8, hipMemcpyDeviceToHost, c->st));

@@ -96,7 +96,7 @@ struct cg_ctx {
   DBuf<int32_t> run_count, lt_kind;
   DBuf<uint32_t> run_dmask;
   DBuf<char> scan_tmp;
-  DBuf<unsigned long long> stuck;  // ~0 between calls (k_rule_offsets re-arms it)
+  DBuf<unsigned long long> stuck;  // ~0 between calls (the expansion scan re-arms it)
   bool stuck_armed = false;        // false: memset it before the next k_count
   DBuf<int64_t> res;               // {event total, stuck rule} of the last expansion
   int64_t* res_host = nullptr;     // pinned 16 B: one async D2H read per call

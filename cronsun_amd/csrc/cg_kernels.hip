@@ -4,14 +4,14 @@
 //   k_count      one lane per rule: per plan segment, the first fire (exact
 //                Go walk, next_exact) and the closed-form count of the rest,
 //                or the walked count inside WALK windows -> run records
-//   k_scan_*     exclusive scan of run counts -> run offsets (int64)
+//   k_scan_*     exclusive scan of run counts -> run offsets (int64); the
+//                last pass also writes the rule-major CSR offsets
 //   k_chunk_map  first run touched by each 16384-event output slice
 //   k_write_cf   persistent, output-parallel: each wave walks its slices;
 //                long runs are written wave-cooperatively (64 consecutive
 //                fires per store instruction, mixed-radix digits + lane rank
 //                tables), stretches of short runs lane-parallel via LDS staging
 //   k_write_walk re-walks the (rare) WALK-window runs
-//   k_rule_offs  rule-major CSR offsets
 // Integer and HBM-bound throughout: no MFMA.
 #include <hip/hip_runtime.h>
 
@@ -408,13 +408,25 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_top(int64_t* __restrict__
   }
 }
 
+// RunTail (expansion scan only, else all null): per-rule CSR offsets
+// offsets[r] = out[r*G], the result words res = {E, stuck rule} and the
+// stuck flag re-armed for the next call: the host reads E and the stuck rule
+// in one 16-B record, with no memset before k_count.
+struct RunTail {
+  int64_t* offsets;
+  int64_t* res;
+  unsigned long long* stuck;
+  int32_t G;
+};
+
 // kFused: the tile's carry is the sum of the earlier tiles' totals, summed by
 // the block itself (no k_scan_top launch; used while nb <= kScanFuseTiles)
 template <bool kFused>
 __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __restrict__ in,
                                                               int64_t n,
                                                               const int64_t* __restrict__ partial,
-                                                              int64_t* __restrict__ out) {
+                                                              int64_t* __restrict__ out,
+                                                              RunTail tail) {
   int64_t carry;
   if (kFused) {
     int64_t x = 0;
@@ -436,12 +448,30 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __re
   }
   int64_t tot;
   int64_t run = carry + block_excl_scan(acc, &tot);
-  if (blockIdx.x == 0 && threadIdx.x == 0) out[0] = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    out[0] = 0;
+    if (tail.offsets) tail.offsets[0] = 0;
+  }
 #pragma unroll
   for (int i = 0; i < kScanPerThread; i++) {
     int64_t idx = base + i;
     run += v[i];
     if (idx < n) out[idx + 1] = run;
+  }
+  if (tail.offsets) {
+    int64_t r = run;  // out[idx + 1] for the last idx of this thread, walked back
+#pragma unroll
+    for (int i = kScanPerThread - 1; i >= 0; i--) {
+      const int64_t idx = base + i;
+      if (idx < n && (tail.G == 1 || (idx + 1) % tail.G == 0))
+        tail.offsets[(idx + 1) / tail.G] = r;
+      r -= v[i];
+    }
+    if (base <= n - 1 && n - 1 < base + kScanPerThread) {
+      tail.res[0] = run;  // = out[n]: the thread's values past n - 1 are zeros
+      tail.res[1] = int64_t(*tail.stuck);
+      *tail.stuck = ~0ull;
+    }
   }
 }
 
@@ -1035,21 +1065,6 @@ __global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ sp
   }
 }
 
-// Rule-major CSR offsets; thread 0 also hands the host the event total and
-// the stuck-rule flag in one 16-B record and re-arms the flag for the next
-// call (no separate reads, no memset before k_count).
-__global__ void k_rule_offsets(const int64_t* __restrict__ run_off, int64_t R, int32_t G,
-                               int64_t* __restrict__ offsets, int64_t* __restrict__ res,
-                               unsigned long long* __restrict__ stuck) {
-  int64_t r = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (r <= R) offsets[r] = run_off[r * G];
-  if (r == 0) {
-    res[0] = run_off[R * G];
-    res[1] = int64_t(*stuck);
-    *stuck = ~0ull;
-  }
-}
-
 int grid_for(int64_t n, int threads, int max_blocks) {
   int64_t b = (n + threads - 1) / threads;
   if (b < 1) b = 1;
@@ -1139,20 +1154,32 @@ size_t scan_temp_bytes(int64_t n) {
   return size_t(nb + 1) * sizeof(int64_t);
 }
 
+static void scan_impl(const int32_t* in, int64_t* out, int64_t n, void* temp, RunTail tail,
+                      hipStream_t st) {
+  int64_t nb = (n + kScanTile - 1) / kScanTile;
+  int64_t* partial = static_cast<int64_t*>(temp);
+  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial);
+  if (nb <= kScanFuseTiles) {
+    hipLaunchKernelGGL(k_scan_apply<true>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out,
+                       tail);
+    return;
+  }
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanThreads), 0, st, partial, nb);
+  hipLaunchKernelGGL(k_scan_apply<false>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out,
+                     tail);
+}
+
 void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st) {
   if (n <= 0) {
     (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
     return;
   }
-  int64_t nb = (n + kScanTile - 1) / kScanTile;
-  int64_t* partial = static_cast<int64_t*>(temp);
-  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial);
-  if (nb <= kScanFuseTiles) {
-    hipLaunchKernelGGL(k_scan_apply<true>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out);
-    return;
-  }
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanThreads), 0, st, partial, nb);
-  hipLaunchKernelGGL(k_scan_apply<false>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out);
+  scan_impl(in, out, n, temp, RunTail{nullptr, nullptr, nullptr, 1}, st);
+}
+
+void launch_scan_runs(const int32_t* run_count, int64_t* run_off, int64_t R, int32_t G, void* temp,
+                      int64_t* offsets, int64_t* res, unsigned long long* stuck, hipStream_t st) {
+  scan_impl(run_count, run_off, R * G, temp, RunTail{offsets, res, stuck, G}, st);
 }
 
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
@@ -1251,10 +1278,5 @@ void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const i
                      cap, times);
 }
 
-void launch_rule_offsets(const int64_t* run_off, int64_t R, int32_t G, int64_t* offsets,
-                         int64_t* res, unsigned long long* stuck, hipStream_t st) {
-  hipLaunchKernelGGL(k_rule_offsets, dim3(grid_for(R + 1, 256, 1 << 30)), dim3(256), 0, st,
-                     run_off, R, G, offsets, res, stuck);
-}
 
 }  // namespace cg
