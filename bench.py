@@ -236,6 +236,9 @@ def main():
     for _ in range(args.warmup):
         E = step()
     log(f"[rank {rank}] warmup done: {E} events/step")
+    if not pn and wl != "dispatch":
+        _, d_times, _ = eng.result_device()
+        log(f"[rank {rank}] times buffer at {d_times:#x} ({d_times % (1 << 21):#x} past a 2 MiB boundary)")
     barrier()
     torch.cuda.synchronize()
     start = time.perf_counter()
