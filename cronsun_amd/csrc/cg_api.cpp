@@ -509,15 +509,21 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   if ((rc = c->run_off.ensure(nruns + 1))) return rc;
   if ((rc = c->scan_tmp.ensure(scan_temp_bytes(nruns)))) return rc;
 
-  if ((rc = c->stuck.ensure(1)) || (rc = c->res.ensure(2))) return rc;
-  if (!c->res_host) HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->res_host), 16));
+  if ((rc = c->stuck.ensure(1))) return rc;
+  if (!c->res_host) {
+    // mapped, coherent pinned memory: the scan kernel stores the 16-B record
+    // straight into it (no D2H copy launch); read after the stream sync
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->res_host), 16,
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->res_dev), c->res_host, 0));
+  }
   if (!c->stuck_armed) HIPCHK(hipMemsetAsync(c->stuck.p, 0xFF, sizeof(unsigned long long), c->st));
   c->stuck_armed = false;  // until this call's scan re-arms it
   const bool all_phases = c->phase_timing >= 2;
   if (all_phases) (void)hipEventRecord(c->ev[0], c->st);
   launch_count(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->stuck.p, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[1], c->st);
-  launch_scan_runs(c->run_count.p, c->run_off.p, R, int32_t(G), c->scan_tmp.p, c->offsets.p, c->res.p,
+  launch_scan_runs(c->run_count.p, c->run_off.p, R, int32_t(G), c->scan_tmp.p, c->offsets.p, c->res_dev,
                    c->stuck.p, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[2], c->st);
   HIPCHK(hipGetLastError());
@@ -576,7 +582,6 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
                         c->run_off.p, cap, c->times.p, c->st);
     if (all_phases) (void)hipEventRecord(c->ev[6], c->st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(c->res_host, c->res.p, 16, hipMemcpyDeviceToHost, c->st));
     HIPCHK(hipStreamSynchronize(c->st));
     c->stuck_armed = true;
     E = c->res_host[0];
@@ -617,7 +622,6 @@ extern "C" int cg_count(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t 
   HIPCHK(hipGetLastError());
   std::vector<int64_t> off(size_t(R) + 1);
   HIPCHK(hipMemcpyAsync(off.data(), c->offsets.p, (R + 1) * 8, hipMemcpyDeviceToHost, c->st));
-  HIPCHK(hipMemcpyAsync(c->res_host, c->res.p, 16, hipMemcpyDeviceToHost, c->st));
   HIPCHK(hipStreamSynchronize(c->st));
   c->stuck_armed = true;
   const unsigned long long stuck = static_cast<unsigned long long>(c->res_host[1]);

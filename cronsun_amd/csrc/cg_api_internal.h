@@ -98,8 +98,8 @@ struct cg_ctx {
   DBuf<char> scan_tmp;
   DBuf<unsigned long long> stuck;  // ~0 between calls (the expansion scan re-arms it)
   bool stuck_armed = false;        // false: memset it before the next k_count
-  DBuf<int64_t> res;               // {event total, stuck rule} of the last expansion
-  int64_t* res_host = nullptr;     // pinned 16 B: one async D2H read per call
+  int64_t* res_host = nullptr;     // {E, stuck rule}: mapped pinned 16 B the scan writes
+  int64_t* res_dev = nullptr;      // res_host's device address
   int64_t last_E = 0, last_R = 0, last_G = 0;
 
   // per-node buffers
@@ -117,9 +117,10 @@ struct cg_ctx {
     plan_dev.release();
     run_anchor.release(); run_off.release(); offsets.release(); times.release();
     block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
-    lt_avg.release(); lt_kind.release(); res.release();
+    lt_avg.release(); lt_kind.release();
     if (res_host) (void)hipHostFree(res_host);
     res_host = nullptr;
+    res_dev = nullptr;
     run_dmask.release(); scan_tmp.release(); stuck.release();
     rn_off.release(); rn_cnt64.release(); pair_pos.release(); pair_src.release(); node_off.release();
     node_time.release(); nt_off.release(); rn_cnt.release(); rn_nodes.release();
