@@ -271,7 +271,7 @@ def main():
         kts = [[ph[0], ph[1], ph[2], k[3], ph[4], ph[5]] for k in kts]
 
     e2e = None
-    if wl == "config2":
+    if wl == "config2" and rank == 0:
         # end to end, outside the timed region: H2D of the
         # packed specs, the expansion, D2H of the rule-major CSR into pinned
         # host memory (the host parse is reported by the CPU baseline)
