@@ -219,8 +219,11 @@ int cg_init(int device, cg_ctx** out) {
     delete c;
     return cg_fail(CG_EHIP, "hipStreamCreate failed");
   }
-  for (auto& e : c->ev) (void)hipEventCreate(&e);
-  for (auto& e : c->pev) (void)hipEventCreate(&e);
+  // timing-only events (read after a stream sync): no system-scope fence
+  // when they complete -- a fenced event between two kernels idles the GPU
+  // for several us (cache writeback + invalidate)
+  for (auto& e : c->ev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  for (auto& e : c->pev) (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   *out = c;
   return CG_OK;
 }
