@@ -474,8 +474,10 @@ int cg_lock_ttl_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int6
 // --------------------------------------------------------------- expansion
 // plan (cached) + k_count + scan of the run counts: c->run_off holds the run
 // offsets afterwards.  *empty = true when there is nothing to count.
+// map_cap > 0: the scan also builds k_write_cf's slice map in c->block_run
+// for an output capacity of map_cap events (no k_chunk_map launch).
 static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
-                       bool* empty) {
+                       bool* empty, int64_t map_cap = 0) {
   HIPCHK(hipSetDevice(c->device));
   if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
     return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON");
@@ -526,8 +528,9 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   if (all_phases) (void)hipEventRecord(c->ev[0], c->st);
   launch_count(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->stuck.p, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[1], c->st);
+  if (map_cap > 0 && (rc = c->block_run.ensure(map_cap / kSuper + 2 + kTicketWords + 8))) return rc;
   launch_scan_runs(c->run_count.p, c->run_off.p, R, int32_t(G), c->scan_tmp.p, c->offsets.p, c->res_dev,
-                   c->stuck.p, c->st);
+                   c->stuck.p, map_cap > 0 ? c->block_run.p : nullptr, map_cap, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[2], c->st);
   HIPCHK(hipGetLastError());
   *empty = false;
@@ -543,7 +546,10 @@ static int stuck_error(unsigned long long stuck) {
 int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
                          int64_t* n_events) {
   bool empty = true;
-  int rc = count_phase(c, s, z, t0, t1, &empty);
+  // steady state: the output buffer exists, so the scan builds the writer's
+  // slice map for its capacity (a first or a growing call maps separately)
+  const int64_t cap0 = int64_t(c->times.cap);
+  int rc = count_phase(c, s, z, t0, t1, &empty, cap0);
   if (rc) return rc;
   if (empty) {
     c->last_E = 0;
@@ -575,7 +581,8 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
     const int64_t cap = int64_t(c->times.cap);
     if ((rc = c->block_run.ensure(cap / kSuper + 2 + kTicketWords + 8))) return rc;
     if (all_phases) (void)hipEventRecord(c->ev[3], c->st);
-    launch_chunk_map(c->run_off.p, nruns, cap, c->block_run.p, c->st);
+    if (!(cap0 > 0 && cap == cap0))
+      launch_chunk_map(c->run_off.p, nruns, cap, c->block_run.p, c->st);
     (void)hipEventRecord(c->ev[4], c->st);
     launch_write_cf(s->d, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->run_off.p, nruns,
                     c->block_run.p, cap, c->times.p, c->write_blocks, c->st);

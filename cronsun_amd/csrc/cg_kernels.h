@@ -72,9 +72,12 @@ void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run
 size_t scan_temp_bytes(int64_t n);
 void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st);
 // expansion scan (R*G > 0 run counts): also writes the per-rule offsets
-// (offsets[r] = run_off[r*G]), res = {E, stuck rule} and re-arms *stuck
+// (offsets[r] = run_off[r*G]), res = {E, stuck rule} and re-arms *stuck;
+// with chunk_run (else null) also the writer's slice map for capacity cap
+// (as launch_chunk_map)
 void launch_scan_runs(const int32_t* run_count, int64_t* run_off, int64_t R, int32_t G, void* temp,
-                      int64_t* offsets, int64_t* res, unsigned long long* stuck, hipStream_t st);
+                      int64_t* offsets, int64_t* res, unsigned long long* stuck,
+                      int64_t* chunk_run, int64_t cap, hipStream_t st);
 
 // chunk_run needs cap / kSuper + 2 + kTicketWords + 8 entries (slice map, the
 // writer's slice tickets, 8 diagnostic counters); both read E = run_off[nruns]

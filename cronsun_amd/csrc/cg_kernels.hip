@@ -412,11 +412,16 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_top(int64_t* __restrict__
 // offsets[r] = out[r*G], the result words res = {E, stuck rule} and the
 // stuck flag re-armed for the next call: the host reads E and the stuck rule
 // in one 16-B record, with no memset before k_count.
+// With chunk_run set it also builds k_write_cf's slice map for an output
+// capacity of cap events (what k_chunk_map does, from the run bounds the
+// thread already holds) and resets the writer's slice tickets.
 struct RunTail {
   int64_t* offsets;
   int64_t* res;
   unsigned long long* stuck;
   int32_t G;
+  int64_t* chunk_run;
+  int64_t cap;
 };
 
 // kFused: the tile's carry is the sum of the earlier tiles' totals, summed by
@@ -459,18 +464,30 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __re
     if (idx < n) out[idx + 1] = run;
   }
   if (tail.offsets) {
+    const int64_t last_sup = tail.cap / kSuper;  // map entries 0 .. last_sup + 1
+    if (tail.chunk_run && blockIdx.x == 0 && threadIdx.x < kTicketWords + 8)
+      tail.chunk_run[last_sup + 2 + threadIdx.x] = 0;
     int64_t r = run;  // out[idx + 1] for the last idx of this thread, walked back
 #pragma unroll
     for (int i = kScanPerThread - 1; i >= 0; i--) {
       const int64_t idx = base + i;
       if (idx < n && (tail.G == 1 || (idx + 1) % tail.G == 0))
         tail.offsets[(idx + 1) / tail.G] = r;
+      if (tail.chunk_run && idx < n && v[i] > 0) {
+        // slices whose first event lies in this (non-empty) run: the largest
+        // j with run_off[j] <= c*kSuper, as k_chunk_map's search finds it
+        const int64_t lo = r - v[i];
+        for (int64_t c = (lo + kSuper - 1) / kSuper; c * kSuper < r && c <= last_sup; c++)
+          tail.chunk_run[c] = idx;
+      }
       r -= v[i];
     }
     if (base <= n - 1 && n - 1 < base + kScanPerThread) {
       tail.res[0] = run;  // = out[n]: the thread's values past n - 1 are zeros
       tail.res[1] = int64_t(*tail.stuck);
       *tail.stuck = ~0ull;
+      const int64_t nsup = (run + kSuper - 1) / kSuper;
+      if (tail.chunk_run && nsup <= last_sup + 1) tail.chunk_run[nsup] = n - 1;
     }
   }
 }
@@ -1174,12 +1191,13 @@ void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStre
     (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
     return;
   }
-  scan_impl(in, out, n, temp, RunTail{nullptr, nullptr, nullptr, 1}, st);
+  scan_impl(in, out, n, temp, RunTail{nullptr, nullptr, nullptr, 1, nullptr, 0}, st);
 }
 
 void launch_scan_runs(const int32_t* run_count, int64_t* run_off, int64_t R, int32_t G, void* temp,
-                      int64_t* offsets, int64_t* res, unsigned long long* stuck, hipStream_t st) {
-  scan_impl(run_count, run_off, R * G, temp, RunTail{offsets, res, stuck, G}, st);
+                      int64_t* offsets, int64_t* res, unsigned long long* stuck,
+                      int64_t* chunk_run, int64_t cap, hipStream_t st) {
+  scan_impl(run_count, run_off, R * G, temp, RunTail{offsets, res, stuck, G, chunk_run, cap}, st);
 }
 
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
