@@ -188,3 +188,18 @@ def test_lean_phase_timing_same_result(eng):
     assert kt[3] > 0 and kt[0] == kt[1] == kt[2] == kt[4] == kt[5] == -1
     with pytest.raises(_lib.CgError):
         eng.set_phase_timing(3)
+
+
+def test_output_growth_and_reuse():
+    """A fresh context: first call (no output buffer: separate slice map),
+    a larger call (E beyond the capacity: the scan's slice map is discarded,
+    buffers grow, the write phase reruns), then smaller calls that reuse the
+    capacity (slice map built by the scan) -- all bit-exact."""
+    from cronsun_amd.engine import Engine
+    eng = Engine(0)
+    rng = np.random.default_rng(21)
+    small = [cron.Parse(random_spec(rng)) for _ in range(300)]
+    big = small + [cron.Parse("*/2 * * * * *")] * 40 + [cron.Parse(random_spec(rng)) for _ in range(700)]
+    t0 = synth.T0_2026
+    for scheds, t1 in ((small, t0 + DAY), (big, t0 + 2 * DAY), (small, t0 + DAY), (big, t0 + DAY)):
+        check_same(eng, scheds, "UTC", t0, t1)
