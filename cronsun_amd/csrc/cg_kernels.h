@@ -26,7 +26,11 @@ constexpr int kWriteWaves = 4;
 #define CG_WRITE_BPC 4
 #endif
 constexpr int kWriteBlocksPerCU = CG_WRITE_BPC;  // persistent grid: blocks of 4 waves per CU
-constexpr int kSuper = 16384;
+#ifndef CG_SUPER
+#define CG_SUPER 2048
+#endif
+constexpr int kSuper = CG_SUPER;  // events per writer slice (multiple of 64)
+static_assert(kSuper % 64 == 0, "writer slices are whole 64-event blocks");
 // writer slice tickets: one u32 counter per group of blocks, 128 B apart
 constexpr int kTicketGroups = 8;
 constexpr int kTicketStride = 32;                                  // u32 words

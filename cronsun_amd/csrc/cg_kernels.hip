@@ -6,7 +6,7 @@
 //                or the walked count inside WALK windows -> run records
 //   k_scan_*     exclusive scan of run counts -> run offsets (int64); the
 //                last pass also writes the rule-major CSR offsets
-//   k_chunk_map  first run touched by each 16384-event output slice
+//   k_chunk_map  first run touched by each kSuper-event output slice
 //   k_write_cf   persistent, output-parallel: each wave walks its slices;
 //                long runs are written wave-cooperatively (64 consecutive
 //                fires per store instruction, mixed-radix digits + lane rank

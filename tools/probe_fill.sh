@@ -6,7 +6,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-probe_fill}
 mkdir -p "$OUT"
 for round in 1 2; do
-  for pr in 0 1 2 5; do
+  for pr in ${PROBES:-0 1 2 5}; do
     CG_WRITE_PROBE=$pr timeout -k 10 300 python bench.py --steps 20 --warmup 3 --cpu-sample 0 \
       > "$OUT/p${pr}_$round.json" 2> "$OUT/p${pr}_$round.err" || { tail -20 "$OUT/p${pr}_$round.err"; exit 1; }
     python3 -c "import json; d=json.load(open('$OUT/p${pr}_$round.json')); print('probe $pr r$round write_cf=%.4f ms' % d['kernel_ms']['write_cf'])"
