@@ -32,7 +32,10 @@ constexpr int kWriteBlocksPerCU = CG_WRITE_BPC;  // persistent grid: blocks of 4
 constexpr int kSuper = CG_SUPER;  // events per writer slice (multiple of 64)
 static_assert(kSuper % 64 == 0, "writer slices are whole 64-event blocks");
 // writer slice tickets: one u32 counter per group of blocks, 128 B apart
-constexpr int kTicketGroups = 8;
+#ifndef CG_TICKET_GROUPS
+#define CG_TICKET_GROUPS 32
+#endif
+constexpr int kTicketGroups = CG_TICKET_GROUPS;
 constexpr int kTicketStride = 32;                                  // u32 words
 constexpr int kTicketWords = kTicketGroups * kTicketStride / 2;    // int64 words
 

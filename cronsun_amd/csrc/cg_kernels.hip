@@ -465,8 +465,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __re
   }
   if (tail.offsets) {
     const int64_t last_sup = tail.cap / kSuper;  // map entries 0 .. last_sup + 1
-    if (tail.chunk_run && blockIdx.x == 0 && threadIdx.x < kTicketWords + 8)
-      tail.chunk_run[last_sup + 2 + threadIdx.x] = 0;
+    if (tail.chunk_run && blockIdx.x == 0)
+      for (int i = threadIdx.x; i < kTicketWords + 8; i += kScanThreads)
+        tail.chunk_run[last_sup + 2 + i] = 0;
     int64_t r = run;  // out[idx + 1] for the last idx of this thread, walked back
 #pragma unroll
     for (int i = kScanPerThread - 1; i >= 0; i--) {
@@ -509,8 +510,8 @@ __device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, i
 // writer's slice ticket counters, reset here)
 __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, int64_t cap,
                             int64_t* __restrict__ chunk_run) {
-  if (blockIdx.x == 0 && threadIdx.x < kTicketWords + 8)
-    chunk_run[cap / kSuper + 2 + threadIdx.x] = 0;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < kTicketWords + 8; i += blockDim.x) chunk_run[cap / kSuper + 2 + i] = 0;
   const int64_t E = run_off[nruns];
   if (E > cap) return;
   const int64_t nsup = (E + kSuper - 1) / kSuper;
