@@ -81,7 +81,24 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="rules in the CPU-baseline sample (0 = skip; default 40k, 1M for dispatch)")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--verify-sample", type=int, default=2000,
+                    help="rules (rule-major) or nodes/250 (per-node) of the timed result checked "
+                         "against the oracle after the timed region (0 = skip)")
+    ap.add_argument("--diagnostic", action="store_true",
+                    help="allow the diagnostic library / CG_WRITE_* CG_NODE_* switches (the line is "
+                         "then marked diagnostic and is not a headline)")
     args = ap.parse_args()
+
+    # A headline must come from the production library with every output
+    # store in place: the diagnostic build's probe/variant switches replace or
+    # drop stores (cronsun_amd/csrc/Makefile `diag`).
+    from cronsun_amd import _lib as _cg
+    diag_env = {k: v for k, v in os.environ.items() if k.startswith(("CG_WRITE_", "CG_NODE_"))}
+    build_info = _cg.lib().cg_build_info()
+    if (diag_env or build_info & 1) and not args.diagnostic:
+        log(f"bench.py: refusing to run: diagnostic switches {sorted(diag_env)} / library build "
+            f"info {build_info} ({_cg.LIB_PATH}); pass --diagnostic for a non-headline probe run")
+        sys.exit(2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -103,13 +120,13 @@ def main():
     cdev_early = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
 
     wl = args.workload
-    if args.cpu_sample is None:
-        args.cpu_sample = 1_000_000 if wl == "dispatch" else 40_000
+    if args.cpu_sample is None:  # config2: -1 = adaptive (the whole workload when it fits ~30 s)
+        args.cpu_sample = 1_000_000 if wl == "dispatch" else -1
     if wl == "config2":
-        R = args.rules or 1_000_000
+        R = args.rules or 1_000_000  # per GPU (weak scaling): the global set has R * world rules
         H = args.horizon or 86400
         mix = synth.MIX_CONFIG2
-        seed = 0x5EED + rank
+        seed = 0x5EED
     elif wl == "dispatch":
         R = args.rules or 10_000_000
         H = 0
@@ -144,7 +161,8 @@ def main():
         # the global 10M-rule set is the 1M-rule light-mix block tiled in
         # job-ID order (rule i = block[i % 1M]), so any rank can build any range
         base_n = min(total, 1_000_000)
-        base_arr, status = cron.parse_batch(synth.spec_mix(base_n, seed=seed, mix=mix), threads=16)
+        base_specs = synth.spec_mix(base_n, seed=seed, mix=mix)
+        base_arr, status = cron.parse_batch(base_specs, threads=16)
         assert (status == 0).all()
         base_np = np.ctypeslib.as_array(base_arr)
 
@@ -165,6 +183,24 @@ def main():
         R = hi - lo
         sp = upload_range(lo, hi)
         specs = None
+        shard_lo = lo
+
+        def spec_of(i):  # local rule i of this rank's range
+            return base_specs[(shard_lo + i) % base_n]
+    elif wl == "config2":
+        # one global rule set of R * world rules in job-ID order, built from
+        # R-rule blocks (block b: seed 0x5EED + b, so the N = 1 set is block 0);
+        # rank g expands its job-ID range [g R, (g + 1) R)
+        glob = R * world
+        lo, hi = shard.shard_range(glob, world, rank)
+        specs = []
+        for b in range(lo // R, (hi - 1) // R + 1):
+            blk = synth.spec_mix(R, seed=seed + b, mix=mix)
+            specs += blk[max(lo - b * R, 0):min(hi - b * R, R)]
+        shard_info = {"lo": lo, "hi": hi, "global_rules": glob}
+        arr, status = cron.parse_batch(specs, threads=16)
+        assert (status == 0).all()
+        sp = eng.upload_c(arr, R)
     else:
         if wl == "dispatch" and R > 1_000_000:
             # the 1M-rule config-2 set tiled (Python generation of 10M strings
@@ -176,6 +212,9 @@ def main():
         arr, status = cron.parse_batch(specs, threads=16)
         assert (status == 0).all()
         sp = eng.upload_c(arr, R)
+    if specs is not None:
+        def spec_of(i):
+            return specs[i]
     drules = None
     n_nodes = 10_000
     if pn:
@@ -211,6 +250,7 @@ def main():
                 En_w, nnz = eng.expand_per_node_rules_device(sp, utc, a, min(a + W, t1), drules,
                                                              xmode)
                 En += En_w
+                last["En_last"] = En_w
                 kt_sum += np.array(eng.kernel_times())
                 nkt_sum += np.array(eng.node_kernel_times())
                 last.setdefault("first_nkt", eng.node_kernel_times())  # the uncached join
@@ -258,6 +298,25 @@ def main():
     barrier()
     elapsed = time.perf_counter() - start
     wake["loop_s"], wake["tail_s"] = t_loop, elapsed - t_loop
+
+    # The timed steps' own output, checked on a seeded sample against the
+    # oracle (outside the timed region): a step that skipped work would fail.
+    verify = None
+    if args.verify_sample > 0 and wl != "dispatch":
+        tv = time.perf_counter()
+        if pn:
+            a_last = list(range(t0, t1, W))[-1]
+            verify = verify_per_node(eng, spec_of, rin, xmode, a_last, min(a_last + W, t1), last["En_last"],
+                                     max(2, args.verify_sample // 250), seed=0x5EED + 77 + rank)
+        else:
+            verify = verify_rule_major(eng, spec_of, R, t0, t1, E, args.verify_sample,
+                                       seed=0x5EED + 99 + rank)
+        verify["seconds"] = time.perf_counter() - tv
+        ok = torch.tensor([1 if verify["verified"] else 0], dtype=torch.int64, device=cdev)
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        verify["verified_all_ranks"] = bool(ok.item())
+        log(f"[rank {rank}] verify: {verify}")
 
     if lean:
         # per-phase breakdown of a few untimed steps (events between phases)
@@ -313,7 +372,7 @@ def main():
         return
 
     if wl == "dispatch":
-        print(json.dumps(dispatch_line(args, R, world, elapsed, wake, nkt,
+        print(json.dumps(dispatch_line(args, R, world, elapsed, wake, nkt, build_info,
                                        cpu_dispatch(specs[:args.cpu_sample], t0)
                                        if world == 1 and args.cpu_sample > 0 else None)), flush=True)
         if world > 1:
@@ -346,8 +405,8 @@ def main():
     achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
 
     cpu = None
-    if world == 1 and args.cpu_sample > 0 and wl == "config2":
-        cpu = cpu_baseline(specs[:args.cpu_sample], t0, t1, args.cpu_threads)
+    if world == 1 and args.cpu_sample != 0 and wl == "config2":
+        cpu = cpu_baseline(specs, args.cpu_sample, t0, t1, args.cpu_threads)
 
     out = {
         "metric": metric,
@@ -389,7 +448,12 @@ def main():
             "algo_bytes_per_launch": algo_bytes,
         },
         "cpu_baseline": cpu,
+        "verified": bool(verify and verify["verified_all_ranks"]),
+        "verify": verify,
+        "library": {"path": os.path.relpath(_cg.LIB_PATH, ROOT), "build_info": build_info},
     }
+    if args.diagnostic:
+        out["diagnostic"] = {"env": diag_env, "note": "probe/variant run: not a headline"}
     if e2e is not None:
         out["end_to_end_rank0"] = e2e
     if pn:
@@ -405,7 +469,7 @@ def main():
         dist.destroy_process_group()
 
 
-def dispatch_line(args, R, world, elapsed, wake, nkt, cpu):
+def dispatch_line(args, R, world, elapsed, wake, nkt, build_info, cpu):
     import numpy as np
     wall = np.array(wake["wall"] or [0.0])
     due = wake["due"] / max(wake["wakes"], 1)
@@ -438,7 +502,92 @@ def dispatch_line(args, R, world, elapsed, wake, nkt, cpu):
                      "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                      "traffic": None, "algo_bytes_per_launch": algo},
         "cpu_baseline": cpu,
+        "verified": None,
+        "verify": "dispatcher wakes are checked wake by wake against the oracle in "
+                  "tests/test_gpu_dispatch.py, not in the bench",
+        "library": {"build_info": build_info},
     }
+
+
+def host_cpus():
+    """CPUs this process may use: the affinity mask, capped by a cgroup CPU
+    quota when one is set (a GPU box's share of a larger host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except Exception:
+        pass
+    return (min(aff, quota) if quota else aff), {"affinity_cpus": aff, "cgroup_quota_cpus": quota}
+
+
+def _oracle():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as O
+    return O
+
+
+def _oracle_scheds(O, specs):
+    memo, out = {}, []
+    for s in specs:
+        if s not in memo:
+            sc, err = O.parse(s)  # the oracle's own parser (parser.go restated)
+            if err is not None:
+                raise RuntimeError(f"oracle rejects {s!r}: {err}")
+            memo[s] = sc
+        out.append(memo[s])
+    return O.sched_array(out)
+
+
+def verify_rule_major(eng, spec_of, R, t0, t1, E, sample, seed):
+    """The last timed step's rule-major CSR against the oracle's Next loop on
+    a seeded sample of rules (checker only; outside the timed region)."""
+    import numpy as np
+    from cronsun_amd._lib import check, lib
+    O = _oracle()
+    off = np.empty(R + 1, dtype=np.int64)
+    check(lib().cg_result_copy_offsets(eng._h, off.ctypes.data))
+    idx = np.sort(np.random.default_rng(seed).choice(R, min(sample, R), replace=False))
+    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(i)) for i in idx]), t0, t1, O.Loc("UTC"),
+                            threads=host_cpus()[0])
+    bad = 0
+    for k, i in enumerate(idx):
+        got = eng.copy_times(off[i], off[i + 1] - off[i])
+        bad += not np.array_equal(got, et[eo[k]:eo[k + 1]])
+    mono = bool(off[0] == 0 and off[-1] == E and (np.diff(off) >= 0).all())
+    return {"verified": bad == 0 and mono, "kind": "rule-major CSR vs oracle Next loop",
+            "rules_checked": int(len(idx)), "events_checked": int(eo[-1]),
+            "mismatched_rules": int(bad), "offsets_consistent": mono}
+
+
+def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed):
+    """The last timed window's per-node lists against each sampled node's own
+    filter over every rule (node.go:121-158 -> Job.Cmds) composed with the
+    oracle's Next loop (checker only; outside the timed region)."""
+    import numpy as np
+    from cronsun_amd._lib import check, lib
+    O = _oracle()
+    threads = host_cpus()[0]
+    node_off = np.empty(rin.n_nodes + 1, dtype=np.int64)
+    check(lib().cg_node_result_copy(eng._h, node_off.ctypes.data, None, None, 0))
+    nodes = np.sort(np.random.default_rng(seed).choice(rin.n_nodes, n_nodes_sample, replace=False))
+    roff, rules = O.node_rules(rin, mode, nodes, threads=threads)
+    union = np.unique(rules)
+    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(r)) for r in union]), a, b, O.Loc("UTC"),
+                            threads=threads)
+    bad, ev = 0, 0
+    for k, n in enumerate(nodes):
+        pos = np.searchsorted(union, rules[roff[k]:roff[k + 1]])
+        exp_t, exp_p = O.node_list(eo, et, pos)
+        got_t, got_r = eng.node_copy_range(node_off[n], node_off[n + 1] - node_off[n])
+        ev += len(exp_t)
+        bad += not (np.array_equal(got_t, exp_t) and np.array_equal(got_r, union[exp_p]))
+    mono = bool(node_off[0] == 0 and node_off[-1] == En and (np.diff(node_off) >= 0).all())
+    return {"verified": bad == 0 and mono, "kind": "per-node lists of the last window vs oracle",
+            "nodes_checked": int(len(nodes)), "events_checked": int(ev),
+            "mismatched_nodes": int(bad), "offsets_consistent": mono}
 
 
 def cpu_dispatch(specs, t0):
@@ -471,24 +620,38 @@ def cpu_dispatch(specs, t0):
                       f"({dt * 1e3:.1f} ms per wake: qsort by Next + Next for the due prefix)"}
 
 
-def cpu_baseline(specs, t0, t1, threads):
+def cpu_baseline(specs, sample, t0, t1, threads):
     """The oracle's literal Next loop (reference semantics, port of
-    spec.go:55-158 + Go time) on this host's cores, bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib as O
-    threads = threads or min(16, os.cpu_count() or 1)
-    tp = time.perf_counter()
-    scheds = [O.parse(s)[0] for s in specs]
-    arr = O.sched_array(scheds)
-    parse_s = time.perf_counter() - tp
+    spec.go:55-158 + Go time) on this host's CPUs: one pass of
+    `t = Next(t)` until > T1 per rule, parallel over rules (the Go baseline's
+    goroutine worker pool).  sample < 0: a strided calibration
+    sample first, then the whole workload if it fits ~30 s, else a strided
+    sample sized for ~15 s; sample > 0: that many rules, strided."""
+    O = _oracle()
+    avail, cpuinfo = host_cpus()
+    threads = threads or avail
     loc = O.Loc("UTC")
-    # one pass of the reference loop over every rule (t = Next(t) until > T1);
-    # the oracle's batch form needs a second, identical pass to place the
-    # times, which would double the CPU time, so only the first is timed
-    ts = time.perf_counter()
-    off, _ = O.expand_batch(arr, t0, t1, loc, threads=threads, with_times=False)
-    dt = time.perf_counter() - ts
-    ev = int(off[-1])
+
+    def timed(sub):
+        tp = time.perf_counter()
+        arr = _oracle_scheds(O, sub)
+        parse_s = time.perf_counter() - tp
+        ts = time.perf_counter()
+        off, _ = O.expand_batch(arr, t0, t1, loc, threads=threads, with_times=False)
+        return int(off[-1]), time.perf_counter() - ts, parse_s
+
+    n = len(specs)
+    if sample < 0:
+        stride = max(1, n // 20_000)
+        ev, dt, _ = timed(specs[::stride])
+        est = dt * stride
+        if est <= 30.0:
+            sample = n
+        else:
+            sample = max(20_000, int(n * 15.0 / est))
+    stride = max(1, n // sample)
+    sub = specs[::stride][:sample]
+    ev, dt, parse_s = timed(sub)
     cpu_model = ""
     try:
         for line in open("/proc/cpuinfo"):
@@ -497,11 +660,12 @@ def cpu_baseline(specs, t0, t1, threads):
                 break
     except Exception:
         pass
+    what = ("the whole workload" if len(sub) == n else
+            f"every {stride}th rule ({len(sub)} of {n})")
     return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
-            "sample": f"first {len(specs)} of the same rules x {t1 - t0}s horizon, UTC "
-                      f"({ev} events, {dt:.2f}s for one pass of the Next loop; parse excluded, "
-                      f"+{parse_s:.2f}s parse)",
-            "value_incl_parse": ev / (dt + parse_s), "cpu_model": cpu_model,
+            "sample": f"{what} x {t1 - t0}s horizon, UTC ({ev} events, {dt:.2f}s for one pass of "
+                      f"the Next loop on {threads} threads; parse excluded, +{parse_s:.2f}s parse)",
+            "value_incl_parse": ev / (dt + parse_s), "cpu_model": cpu_model, **cpuinfo,
             "go_toolchain": "absent on the box image (oracle C port timed instead)"}
 
 

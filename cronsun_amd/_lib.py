@@ -87,6 +87,7 @@ def _declare(L):
         "cg_abi_version": ([], C.c_int),
         "cg_last_error": ([], C.c_char_p),
         "cg_device_count": ([], C.c_int),
+        "cg_build_info": ([], C.c_int),
         "cg_parse": ([C.c_int, C.c_char_p, sz, P(cg_schedule), C.c_char_p, sz], C.c_int),
         "cg_parse_batch": ([C.c_int, vp, vp, sz, vp, vp, C.c_int], C.c_int),
         "cg_get_range": ([C.c_char_p, sz, C.c_uint, C.c_uint, C.c_int, P(u64), C.c_char_p, sz], C.c_int),
@@ -133,6 +134,8 @@ def _declare(L):
         "cg_node_result_device": ([vp, P(vp), P(vp), P(vp), P(i64)], C.c_int),
         "cg_node_result_copy": ([vp, vp, vp, vp, i64], C.c_int),
         "cg_node_counts_to_device": ([vp, vp], C.c_int),
+        "cg_node_result_copy_range": ([vp, i64, i64, vp, vp], C.c_int),
+        "cg_checksum_device": ([vp, vp, i64, C.c_int, i64, i64, P(u64)], C.c_int),
         "cg_rules_upload": ([vp, P(cg_rules_in), P(vp)], C.c_int),
         "cg_rules_free": ([vp], None),
         "cg_expand_per_node_rules_device": ([vp, vp, vp, i64, i64, vp, C.c_int, P(i64), P(i64)],

@@ -48,6 +48,14 @@ int cg_abi_version(void) { return CG_ABI_VERSION; }
 
 const char* cg_last_error(void) { return g_err.c_str(); }
 
+int cg_build_info(void) {
+#ifdef CG_DIAG
+  return CG_BUILD_DIAG;
+#else
+  return 0;
+#endif
+}
+
 int cg_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -213,7 +221,9 @@ int cg_init(int device, cg_ctx** out) {
   cg_ctx* c = new cg_ctx();
   c->device = device;
   int per_cu = kWriteBlocksPerCU;
-  if (const char* e = getenv("CG_WRITE_BLOCKS_PER_CU")) per_cu = std::max(1, atoi(e));  // diagnostic
+#ifdef CG_DIAG
+  if (const char* e = getenv("CG_WRITE_BLOCKS_PER_CU")) per_cu = std::max(1, atoi(e));
+#endif
   c->write_blocks = std::max(1, prop.multiProcessorCount) * per_cu;
   if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
     delete c;
@@ -478,6 +488,9 @@ int cg_lock_ttl_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int6
 // for an output capacity of map_cap events (no k_chunk_map launch).
 static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
                        bool* empty, int64_t map_cap = 0) {
+  // no readable result until this call succeeds (the accessors check last_R/E)
+  c->last_R = 0;
+  c->last_E = 0;
   HIPCHK(hipSetDevice(c->device));
   if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
     return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON");
@@ -497,7 +510,6 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   }
   const PlanArgs& pa = c->pa;
   const int64_t G = pa.G;
-  c->last_R = R;
   c->last_G = G;
   for (int i = 0; i < 6; i++) c->kt[i] = 0;
   if ((rc = c->offsets.ensure(R + 1))) return rc;
@@ -551,12 +563,13 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   const int64_t cap0 = int64_t(c->times.cap);
   int rc = count_phase(c, s, z, t0, t1, &empty, cap0);
   if (rc) return rc;
+  const int64_t R = int64_t(s->n);
   if (empty) {
+    c->last_R = R;  // offsets are all zero
     c->last_E = 0;
     *n_events = 0;
     return CG_OK;
   }
-  const int64_t R = int64_t(s->n);
   const PlanArgs& pa = c->pa;
   const int64_t G = pa.G;
   const int64_t nruns = R * G;
@@ -610,6 +623,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   } else {
     c->kt[0] = c->kt[1] = c->kt[2] = c->kt[4] = c->kt[5] = -1.f;
   }
+  c->last_R = R;
   c->last_E = E;
   *n_events = E;
   return CG_OK;
@@ -638,9 +652,7 @@ extern "C" int cg_count(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t 
   if (stuck != ~0ULL) return stuck_error(stuck);
   for (int64_t r = 0; r < R; r++) counts[r] = off[size_t(r) + 1] - off[size_t(r)];
   *total = off[size_t(R)];
-  c->last_R = 0;  // no expansion result to read after a count
-  c->last_E = 0;
-  return CG_OK;
+  return CG_OK;  // (no expansion result to read after a count: last_R = last_E = 0)
 }
 
 extern "C" {
@@ -681,9 +693,9 @@ int cg_result_device(cg_ctx* c, const int64_t** d_off, const int64_t** d_times, 
 
 int cg_result_copy_times(cg_ctx* c, int64_t first, int64_t count, int64_t* host) {
   if (!c || (count && !host)) return cg_fail(CG_EINVAL, "cg_result_copy_times: null");
+  std::lock_guard<std::mutex> g(c->mu);
   if (first < 0 || count < 0 || first + count > c->last_E)
     return cg_fail(CG_EINVAL, "range outside the last result");
-  std::lock_guard<std::mutex> g(c->mu);
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
   if (count) HIPCHK(hipMemcpy(host, c->times.p + first, count * 8, hipMemcpyDeviceToHost));
@@ -696,6 +708,25 @@ int cg_result_copy_offsets(cg_ctx* c, int64_t* host) {
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
   HIPCHK(hipMemcpy(host, c->offsets.p, (c->last_R + 1) * 8, hipMemcpyDeviceToHost));
+  return CG_OK;
+}
+
+int cg_checksum_device(cg_ctx* c, const void* d_ptr, int64_t n, int elem_bytes, int64_t first_index,
+                       int64_t add, uint64_t* out) {
+  if (!c || !out || (n > 0 && !d_ptr) || n < 0 || (elem_bytes != 8 && elem_bytes != 4))
+    return cg_fail(CG_EINVAL, "cg_checksum_device: bad argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  int rc = c->cksum.ensure(1);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(c->cksum.p, 0, 8, c->st));
+  launch_checksum(d_ptr, n, elem_bytes, first_index, add, c->cksum.p, c->st);
+  HIPCHK(hipGetLastError());
+  unsigned long long v = 0;
+  HIPCHK(hipMemcpyAsync(&v, c->cksum.p, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  *out = v;
   return CG_OK;
 }
 

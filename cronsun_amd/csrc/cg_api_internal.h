@@ -97,6 +97,7 @@ struct cg_ctx {
   DBuf<uint32_t> run_dmask;
   DBuf<char> scan_tmp;
   DBuf<unsigned long long> stuck;  // ~0 between calls (the expansion scan re-arms it)
+  DBuf<unsigned long long> cksum;  // cg_checksum_device accumulator
   bool stuck_armed = false;        // false: memset it before the next k_count
   int64_t* res_host = nullptr;     // {E, stuck rule}: mapped pinned 16 B the scan writes
   int64_t* res_dev = nullptr;      // res_host's device address
@@ -121,7 +122,7 @@ struct cg_ctx {
     if (res_host) (void)hipHostFree(res_host);
     res_host = nullptr;
     res_dev = nullptr;
-    run_dmask.release(); scan_tmp.release(); stuck.release();
+    run_dmask.release(); scan_tmp.release(); stuck.release(); cksum.release();
     rn_off.release(); rn_cnt64.release(); pair_pos.release(); pair_src.release(); node_off.release();
     node_time.release(); nt_off.release(); rn_cnt.release(); rn_nodes.release();
     pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();

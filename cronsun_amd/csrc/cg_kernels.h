@@ -41,6 +41,11 @@ constexpr int kTicketWords = kTicketGroups * kTicketStride / 2;    // int64 word
 
 size_t plan_lds_bytes(const PlanArgs& p);
 
+// *out += order-sensitive checksum of n elements (int64 or int32) of v,
+// positions first.., values + add (cg_checksum_device)
+void launch_checksum(const void* v, int64_t n, int elem_bytes, int64_t first, int64_t add,
+                     unsigned long long* out, hipStream_t st);
+
 void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,
                        int64_t* t_out, hipStream_t st);
 // GPU-resident dispatcher (cg_dispatch.cpp): one block per kDispatchTile entries

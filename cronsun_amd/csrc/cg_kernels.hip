@@ -1083,6 +1083,35 @@ __global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ sp
   }
 }
 
+// Order-sensitive checksum of a device array: sum over i of
+// mix(first + i, v[i] + add) mod 2^64 (splitmix64 finaliser), so checksums of
+// consecutive ranges add up and a shard's output can be compared with its
+// range of an unsharded result without moving either.
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void k_checksum(const T* __restrict__ v, int64_t n, int64_t first,
+                                                   int64_t add, unsigned long long* __restrict__ out) {
+  uint64_t acc = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x) {
+    const uint64_t x = uint64_t(int64_t(v[i]) + add);
+    acc += mix64(x ^ mix64(uint64_t(first + i) * 0x9E3779B97F4A7C15ull));
+  }
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  __shared__ uint64_t s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
+}
+
 int grid_for(int64_t n, int threads, int max_blocks) {
   int64_t b = (n + threads - 1) / threads;
   if (b < 1) b = 1;
@@ -1094,6 +1123,18 @@ int grid_for(int64_t n, int threads, int max_blocks) {
 size_t plan_lds_bytes(const PlanArgs& p) {
   return align_up(size_t(p.zn) * 8, 16) + align_up(size_t(p.zn) * 4, 16) +
          align_up(size_t(p.G) * sizeof(Segment), 16) + align_up(size_t(p.nd) * 4, 16);
+}
+
+void launch_checksum(const void* v, int64_t n, int elem_bytes, int64_t first, int64_t add,
+                     unsigned long long* out, hipStream_t st) {
+  if (n <= 0) return;
+  const int grid = grid_for(n, 256 * 8, 256 * 32);
+  if (elem_bytes == 8)
+    hipLaunchKernelGGL(k_checksum<int64_t>, dim3(grid), dim3(256), 0, st,
+                       static_cast<const int64_t*>(v), n, first, add, out);
+  else
+    hipLaunchKernelGGL(k_checksum<int32_t>, dim3(grid), dim3(256), 0, st,
+                       static_cast<const int32_t*>(v), n, first, add, out);
 }
 
 void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,
@@ -1212,7 +1253,14 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
                      int64_t nruns, int64_t* chunk_run, int64_t cap, int64_t* times,
                      int n_blocks, hipStream_t st) {
-  // CG_WRITE_PROBE (diagnostic only, never set in production): replace the
+  const size_t lds = size_t(p.G) * sizeof(Segment);
+#ifndef CG_DIAG
+  // production build: the writer, nothing else (the probes and store-dropping
+  // variants below exist only in the diagnostic library, `make diag`)
+  hipLaunchKernelGGL(k_write_cf<0>, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p,
+                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
+#else
+  // CG_WRITE_PROBE (diagnostic build only): replace the
   // writer by a plain fill of the same E*8 output bytes, same grid and slices,
   // with 8 B (1) or 16 B (2) per lane per store -- the store ceiling the
   // writer is compared against.
@@ -1258,8 +1306,7 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
     const char* e = getenv("CG_WRITE_VARIANT");  // diagnostic only (see put<V>)
     return e ? atoi(e) : 0;
   }();
-  const size_t lds = size_t(p.G) * sizeof(Segment);
-#define CG_WCF(V)                                                                                \
+#define CG_WCF(V)                                                                             \
   hipLaunchKernelGGL(k_write_cf<V>, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p, \
                      run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times)
   switch (variant) {
@@ -1286,6 +1333,7 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
             d[7], double(d[0]) / d[7], double(d[1]) / d[7], double(d[2]) / d[7], double(d[3]) / d[7],
             double(d[4]) / d[7], double(d[5]) / d[7], double(d[6]) / d[7]);
   }
+#endif  // CG_DIAG
 }
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,

@@ -488,6 +488,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   if (En > 0) {
     hipLaunchKernelGGL(k_pair_block_map, dim3(gridn(ntasks + 1, 256, 1 << 30)), dim3(256), 0, st,
                        c->pair_pos.p, nnz, ntasks, c->block_run.p);
+#ifdef CG_DIAG
     static const int variant = [] {  // diagnostic: 1 no gather, 2 no stores, 3 neither
       const char* e = getenv("CG_NODE_VARIANT");
       return e ? atoi(e) : 0;
@@ -496,6 +497,9 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
       const char* e = getenv("CG_NODE_BLOCKS_PER_CU");
       return e ? std::max(1, atoi(e)) : 8;
     }();
+#else
+    constexpr int variant = 0, per_cu = 8;
+#endif
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
 #define CG_NW(V)                                                                              \
   hipLaunchKernelGGL(k_node_write<V>, dim3(gridn(ntasks, 4, nw_blocks)), dim3(256), 0, st,      \
@@ -661,6 +665,25 @@ int cg_node_result_copy(cg_ctx* c, int64_t* node_off, int64_t* time, int32_t* ru
                            "copy rule")))
       return rc;
   }
+  return CG_OK;
+}
+
+int cg_node_result_copy_range(cg_ctx* c, int64_t first, int64_t count, int64_t* time, int32_t* rule) {
+  if (!c || (count && !time && !rule)) return cg_fail(CG_EINVAL, "cg_node_result_copy_range: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  if (first < 0 || count < 0 || first + count > c->pn_E)
+    return cg_fail(CG_EINVAL, "range outside the last per-node result");
+  if (count && time &&
+      (rc = cg_hip_check(hipMemcpy(time, c->node_time.p + first, size_t(count) * 8, hipMemcpyDeviceToHost),
+                         "copy time")))
+    return rc;
+  if (count && rule &&
+      (rc = cg_hip_check(hipMemcpy(rule, c->node_rule.p + first, size_t(count) * 4, hipMemcpyDeviceToHost),
+                         "copy rule")))
+    return rc;
   return CG_OK;
 }
 

@@ -376,8 +376,24 @@ class Engine:
                                         rule.ctypes.data, n_events))
         return node_off, time[:n_events], rule[:n_events]
 
+    def node_copy_range(self, first, count):
+        """Events [first, first+count) of the last per-node result (time, rule)."""
+        time = np.empty(max(count, 1), dtype=np.int64)
+        rule = np.empty(max(count, 1), dtype=np.int32)
+        check(lib().cg_node_result_copy_range(self._h, int(first), int(count), time.ctypes.data,
+                                              rule.ctypes.data))
+        return time[:count], rule[:count]
+
     def node_counts_to_device(self, d_ptr):
         check(lib().cg_node_counts_to_device(self._h, C.c_void_p(d_ptr)))
+
+    def checksum(self, d_ptr, n, elem_bytes=8, first_index=0, add=0):
+        """Order-sensitive checksum of a device array (cg_checksum_device);
+        checksums of consecutive ranges add up mod 2^64."""
+        out = C.c_uint64()
+        check(lib().cg_checksum_device(self._h, C.c_void_p(d_ptr), int(n), int(elem_bytes),
+                                       int(first_index), int(add), C.byref(out)))
+        return out.value
 
 
 _default = None

@@ -78,6 +78,12 @@ int cg_abi_version(void);
 const char* cg_last_error(void);
 /* number of gfx950 devices visible (0 on a host without one) */
 int cg_device_count(void);
+/* Build flags of the loaded library (instrumentation; no reference
+ * counterpart).  CG_BUILD_DIAG: the diagnostic build (`make diag`), whose
+ * writer honours probe/variant environment switches that replace or drop
+ * output stores -- never a production or benchmark library. */
+#define CG_BUILD_DIAG 1
+int cg_build_info(void);
 
 /* ------------------------------------------------------ parse (host) --- */
 /* Parser{options}.Parse(spec) -- parser.go:78-136; cron.Parse is options =
@@ -272,6 +278,15 @@ int cg_last_kernel_times(cg_ctx* ctx, float* ms, int n);
  * throughput measurements use 1.  (No reference counterpart: instrumentation.) */
 int cg_set_phase_timing(cg_ctx* ctx, int level);
 
+/* Order-sensitive checksum of a device array on the ctx's device
+ * (instrumentation for integrity and parity checks; no reference
+ * counterpart): sum over i < n of mix(first_index + i, v[i] + add) mod 2^64,
+ * v = int64 (elem_bytes 8) or int32 (elem_bytes 4), mix = a 64-bit finaliser.
+ * Checksums of consecutive ranges add up, so a shard's output (first_index =
+ * its global base) can be compared with its range of another result. */
+int cg_checksum_device(cg_ctx* ctx, const void* d_ptr, int64_t n, int elem_bytes,
+                       int64_t first_index, int64_t add, uint64_t* out);
+
 /* --------------------------------------------- rule -> node resolution --- */
 /* Integer-interned jobs/groups (host interns string IDs; see cg_jobset_*).
  * Resolution modes:
@@ -324,6 +339,11 @@ int cg_node_result_device(cg_ctx* ctx, const int64_t** d_node_off, const int64_t
 /* copy the last per-node result to host buffers (node_off [N+1]; time/rule
  * [n_events], cap = their capacity); any pointer may be NULL */
 int cg_node_result_copy(cg_ctx* ctx, int64_t* node_off, int64_t* time, int32_t* rule, int64_t cap);
+/* copy events [first, first+count) of the last per-node result (one node's
+ * list is [node_off[n], node_off[n+1])) -- what a single node's scheduler
+ * fetches; either pointer may be NULL */
+int cg_node_result_copy_range(cg_ctx* ctx, int64_t first, int64_t count, int64_t* time,
+                              int32_t* rule);
 /* per-node event counts of the last per-node result, copied to a DEVICE
  * buffer of N int64 (e.g. a torch tensor for an RCCL allgather) */
 int cg_node_counts_to_device(cg_ctx* ctx, int64_t* d_counts);

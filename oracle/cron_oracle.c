@@ -1291,6 +1291,72 @@ int32_t or_job_nodes(const or_jobset *js, int32_t job, int32_t *out, int32_t cap
     return cnt;
 }
 
+/* Every node's own filter (node/node.go:121-158 loadJobs -> addJob ->
+ * Job.Cmds, job.go:591-614): node n walks every rule of every job and keeps
+ * the ones or_rule_on_node accepts, in ascending rule order.  Threaded over
+ * the requested nodes (each node is independent, as each cronsun node process
+ * is). */
+typedef struct {
+    const or_jobset *js;
+    int mode;
+    const int32_t *nodes;
+    size_t k;
+    int64_t *counts;       /* pass 1 */
+    const int64_t *off;    /* pass 2 */
+    int32_t *out;
+    size_t next;
+    pthread_mutex_t mu;
+} node_job;
+
+static void *node_worker(void *arg) {
+    node_job *b = (node_job *)arg;
+    for (;;) {
+        pthread_mutex_lock(&b->mu);
+        size_t i = b->next++;
+        pthread_mutex_unlock(&b->mu);
+        if (i >= b->k) break;
+        int32_t n = b->nodes[i];
+        int64_t c = 0;
+        for (int32_t r = 0; r < b->js->n_rules; r++) {
+            if (!or_rule_on_node(b->js, b->mode, r, n)) continue;
+            if (b->out) b->out[b->off[i] + c] = r;
+            c++;
+        }
+        if (!b->out) b->counts[i] = c;
+    }
+    return NULL;
+}
+
+static void run_nodes(node_job *b, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    pthread_t th[512];
+    if (nthreads > 512) nthreads = 512;
+    b->next = 0;
+    pthread_mutex_init(&b->mu, NULL);
+    for (int i = 0; i < nthreads; i++) pthread_create(&th[i], NULL, node_worker, b);
+    for (int i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    pthread_mutex_destroy(&b->mu);
+}
+
+int64_t or_node_rules_batch(const or_jobset *js, int mode, const int32_t *nodes, size_t k,
+                            int nthreads, int64_t *off, int32_t *out) {
+    node_job b;
+    memset(&b, 0, sizeof b);
+    b.js = js; b.mode = mode; b.nodes = nodes; b.k = k;
+    b.counts = (int64_t *)calloc(k ? k : 1, sizeof(int64_t));
+    run_nodes(&b, nthreads);
+    off[0] = 0;
+    for (size_t i = 0; i < k; i++) off[i + 1] = off[i] + b.counts[i];
+    free(b.counts);
+    b.counts = NULL;
+    if (out) {
+        b.off = off;
+        b.out = out;
+        run_nodes(&b, nthreads);
+    }
+    return off[k];
+}
+
 /* ------------------------------------------------------------------------ */
 /* job.go:194-233  Cmd.lockTtl                                              */
 /* ------------------------------------------------------------------------ */

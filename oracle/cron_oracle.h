@@ -159,6 +159,12 @@ int or_job_is_run_on(const or_jobset *js, int32_t job, int32_t n);
  * Returns the count; writes at most cap node ids. */
 int32_t or_job_nodes(const or_jobset *js, int32_t job, int32_t *out,
                      int32_t cap);
+/* Each requested node's own filter over every rule (node/node.go:121-158 ->
+ * Job.Cmds): off[k+1] offsets and out[] = the rules scheduled on nodes[i]
+ * (per mode, ascending), nthreads host threads.  out may be NULL (counts
+ * only).  Returns the total. */
+int64_t or_node_rules_batch(const or_jobset *js, int mode, const int32_t *nodes, size_t k,
+                            int nthreads, int64_t *off, int32_t *out);
 
 /* Cron.run (node/cron/cron.go:210-275), one wake at a time.  An entry is a
  * schedule + Next + Prev + id (the caller's handle). */

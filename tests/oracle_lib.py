@@ -84,6 +84,8 @@ def lib():
     L.or_job_is_run_on.argtypes = [C.POINTER(OrJobset), i32, i32]
     L.or_job_nodes.argtypes = [C.POINTER(OrJobset), i32, C.POINTER(i32), i32]
     L.or_job_nodes.restype = i32
+    L.or_node_rules_batch.argtypes = [C.POINTER(OrJobset), C.c_int, vp, C.c_size_t, C.c_int, vp, vp]
+    L.or_node_rules_batch.restype = i64
     L.or_cron_start.argtypes = [C.POINTER(OrEntry), C.c_size_t, i64, vp]
     L.or_cron_start.restype = None
     L.or_cron_effective.argtypes = [C.POINTER(OrEntry), C.c_size_t]
@@ -234,6 +236,44 @@ def expand_batch(arr, t0, t1, loc, threads=8, with_times=True):
     times = np.zeros(max(total, 1), dtype=np.int64)
     L.or_expand_batch(arr, R, t0, t1, loc.h, threads, off.ctypes.data, times.ctypes.data)
     return off, times[:total]
+
+
+def jobset(rin):
+    """OrJobset view of an integer-interned rule set (cronsun_amd RulesIn);
+    the arrays stay owned by rin."""
+    js = OrJobset()
+    js.n_nodes, js.n_groups, js.n_rules, js.n_jobs = rin.n_nodes, rin.n_groups, rin.n_rules, rin.n_jobs
+    for f in rin.FIELDS:
+        setattr(js, f, getattr(rin, f).ctypes.data)
+    return js
+
+
+def node_rules(rin, mode, nodes, threads=8):
+    """Rules scheduled on each of `nodes` (each node's own filter over every
+    rule, node.go:121-158 -> Job.Cmds): (off[k+1], rules[]) ascending."""
+    js = jobset(rin)
+    nd = np.ascontiguousarray(nodes, dtype=np.int32)
+    off = np.zeros(len(nd) + 1, dtype=np.int64)
+    L = lib()
+    total = L.or_node_rules_batch(C.byref(js), mode, nd.ctypes.data, len(nd), threads,
+                                  off.ctypes.data, None)
+    out = np.zeros(max(total, 1), dtype=np.int32)
+    L.or_node_rules_batch(C.byref(js), mode, nd.ctypes.data, len(nd), threads, off.ctypes.data,
+                          out.ctypes.data)
+    return off, out[:total]
+
+
+def node_list(eo, et, rules):
+    """A node's (time, rule) list: the fire lists of `rules` (ascending) in
+    rule-major order, from the oracle's rule-major CSR (eo, et)."""
+    rules = np.asarray(rules, dtype=np.int64)
+    lens = eo[rules + 1] - eo[rules]
+    total = int(lens.sum())
+    if total == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int32)
+    excl = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    idx = np.repeat(eo[rules] - excl, lens) + np.arange(total)
+    return et[idx], np.repeat(rules, lens).astype(np.int32)
 
 
 class NonTerminating(Exception):

@@ -4,10 +4,12 @@
 #   CG_WRITE_VARIANT=1   writer without stores (compute only); =2 non-temporal stores
 #   CG_WRITE_BLOCKS_PER_CU  persistent grid size
 set -o pipefail
+# the probe/variant switches exist only in the diagnostic build (make -C cronsun_amd/csrc diag)
+export CRONSUN_GPU_LIB=$PWD/cronsun_amd/libcronsun_gpu_diag.so
 mkdir -p gpurun_out/probe
 run() {  # name env...
   local name=$1; shift
-  env "$@" timeout -k 10 300 python bench.py --steps 10 --warmup 3 --cpu-sample 0 > gpurun_out/probe/$name.json 2> gpurun_out/probe/$name.err || exit 1
+  env "$@" timeout -k 10 300 python bench.py --diagnostic --steps 10 --warmup 3 --cpu-sample 0 > gpurun_out/probe/$name.json 2> gpurun_out/probe/$name.err || exit 1
   python3 -c "import json; d=json.load(open('gpurun_out/probe/$name.json')); print('%-14s write_cf_ms=%.4f' % ('$name', d['kernel_ms']['write_cf']))"
 }
 run base X=0
