@@ -89,6 +89,13 @@ def main():
                          "then marked diagnostic and is not a headline)")
     args = ap.parse_args()
 
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
     # A headline must come from the production library with every output
     # store in place: the diagnostic build's probe/variant switches replace or
     # drop stores (cronsun_amd/csrc/Makefile `diag`).
@@ -99,13 +106,6 @@ def main():
         log(f"bench.py: refusing to run: diagnostic switches {sorted(diag_env)} / library build "
             f"info {build_info} ({_cg.LIB_PATH}); pass --diagnostic for a non-headline probe run")
         sys.exit(2)
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    import numpy as np
-    import torch
-    import torch.distributed as dist
     # RCCL ("nccl") in production; CG_DIST_BACKEND=gloo rehearses the N > 1
     # path with several ranks sharing fewer GPUs (collectives on host tensors)
     backend = os.environ.get("CG_DIST_BACKEND", "nccl")
@@ -285,8 +285,11 @@ def main():
     kts, nkts = [], []
     wake["due"] = wake["wakes"] = 0
     wake["wall"] = []
+    step_wall = []
     for _ in range(args.steps):
+        ts = time.perf_counter()
         E = step()
+        step_wall.append(time.perf_counter() - ts)
         if pn:
             kts.append(last["kt"])
             nkts.append(last["nkt"])
@@ -448,6 +451,8 @@ def main():
             "algo_bytes_per_launch": algo_bytes,
         },
         "cpu_baseline": cpu,
+        "step_wall_ms": {"min": min(step_wall) * 1e3, "p50": float(np.median(step_wall)) * 1e3,
+                         "max": max(step_wall) * 1e3},
         "verified": bool(verify and verify["verified_all_ranks"]),
         "verify": verify,
         "library": {"path": os.path.relpath(_cg.LIB_PATH, ROOT), "build_info": build_info},
