@@ -22,7 +22,7 @@ CG_ENODEV = -7
 CG_EPANIC = -8
 ZERO_TIME = -62135596800
 NO_PROGRESS_TIME = -(1 << 63) + 1
-MAX_HORIZON = 366 * 86400
+MAX_HORIZON = 14610 * 86400  # 40 years (include/cronsun_gpu.h)
 
 PARSE_SECOND, PARSE_MINUTE, PARSE_HOUR, PARSE_DOM = 1, 2, 4, 8
 PARSE_MONTH, PARSE_DOW, PARSE_DOW_OPTIONAL, PARSE_DESCRIPTOR = 16, 32, 64, 128

@@ -369,7 +369,9 @@ int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* p
   const int32_t zn = int32_t(plan.table.when.size());
   const int32_t G = int32_t(plan.segs.size());
   const int32_t nd = int32_t(plan.dtab.size());
-  if (G > 64) return cg_fail(CG_ERANGE, "plan has more than 64 segments (horizon too long)");
+  if (G > kMaxSegments)
+    return cg_fail(CG_ERANGE, "plan has more than " + std::to_string(kMaxSegments) +
+                                  " segments (horizon too long for this zone)");
   // plan_dev is shared by every entry point: whatever it held is gone, so the
   // expansion's plan cache must not be trusted after this (expand re-validates)
   c->plan_valid = false;
@@ -396,10 +398,13 @@ int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* p
   pa->zn = zn;
   pa->G = G;
   pa->nd = nd;
-  pa->pad = 0;
+  pa->dtab_global = 0;
   pa->t0 = t0;
   pa->t1 = t1;
-  if (plan_lds_bytes(*pa) > 60 * 1024)
+  // long horizons: the day table (4 B per local day) stays in HBM and the
+  // zone table + segments alone are staged
+  if (plan_lds_bytes(*pa) > kPlanLdsBytes) pa->dtab_global = 1;
+  if (plan_lds_bytes(*pa) > kPlanLdsBytes)
     return cg_fail(CG_ERANGE, "zone table too large for LDS staging (narrow the time range)");
   return CG_OK;
 }
@@ -493,7 +498,7 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   c->last_E = 0;
   HIPCHK(hipSetDevice(c->device));
   if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
-    return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON");
+    return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON (40 years)");
   const int64_t R = int64_t(s->n);
   int rc;
   // plan (cached across identical calls)

@@ -187,18 +187,30 @@ CG_HD bool cf_full_match(const DSpec& sp, const CFRule& c, const Segment& sg,
   return ((c.H >> h) & 1u) && ((c.M >> m) & 1ull) && ((c.S >> s) & 1ull);
 }
 
+// Next's five-year limit (spec.go:70-76): the walk from t returns the zero time
+// instead of a match e whose local year is past Year(t + 1s) + 5 (it reaches a
+// WRAP in that year first).  Only a gap of more than five years can trip it
+// (e.g. Feb 29 across 2100), so the exact test runs only for such gaps.
+CG_HD bool past_year_limit(const ZoneView& z, int64_t t, int64_t e, int32_t e_off) {
+  if (e - t < 1800 * CG_SECS_PER_DAY) return false;
+  const int64_t u = t + 1;
+  const int32_t y0 = civil_from_days(floordiv64(u + zone_offset(z, u), CG_SECS_PER_DAY)).y;
+  const int32_t ye = civil_from_days(floordiv64(e + e_off, CG_SECS_PER_DAY)).y;
+  return ye > y0 + 5;
+}
+
 CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, int G,
                       const uint32_t* dtab, int64_t t0, int64_t t1, int64_t* anchor_out,
                       int32_t* count_out, uint32_t* dmask_out) {
   if (sp.kind == KIND_EVERY) {
-    // ConstantDelaySchedule: T0 + k*D for k >= 1 (constantdelay.go:25-27)
-    int64_t D = (int64_t)sp.sec;
-    anchor_out[0] = t0;
-    count_out[0] = (int32_t)((t1 - t0) / D);
-    dmask_out[0] = 0;
-    for (int s = 1; s < G; s++) {
-      anchor_out[s] = 0;
-      count_out[s] = 0;
+    // ConstantDelaySchedule: T0 + k*D for k >= 1 (constantdelay.go:25-27),
+    // one run per segment (k with T0 + kD in (a, b]; anchor = the time one
+    // period before its first fire), so no run outgrows int32 on long horizons
+    const int64_t D = (int64_t)sp.sec;
+    for (int s = 0; s < G; s++) {
+      const int64_t ka = (segs[s].a - t0) / D, kb = ((segs[s].b < t1 ? segs[s].b : t1) - t0) / D;
+      anchor_out[s] = t0 + ka * D;
+      count_out[s] = (int32_t)(kb > ka ? kb - ka : 0);
       dmask_out[s] = 0;
     }
     return true;
@@ -218,7 +230,10 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
       const int64_t b = sg.b < t1 ? sg.b : t1;
       dm = seg_daymask(sp, sg, dtab);
       const int64_t e = cf_first_after(c, sg, dm, pos > sg.a ? pos : sg.a);
-      if (e <= b) {
+      if (e <= b && past_year_limit(z, pos, e, sg.off)) {
+        dm = 0;  // Next(pos) is the zero time: the reference loop stops here
+        done = true;
+      } else if (e <= b) {
         cnt = 1 + cf_count(c, sg, dm, e, b);
         anchor = e;
         // the run's last fire starts the next segment's search (not needed

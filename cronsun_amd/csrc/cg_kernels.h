@@ -14,9 +14,15 @@ struct PlanArgs {
   const int32_t* zoff;
   const Segment* segs;
   const uint32_t* dtab;
-  int32_t zn, G, nd, pad;
+  int32_t zn, G, nd;
+  int32_t dtab_global;  // 1: the day table is read from HBM (too large to stage in LDS)
   int64_t t0, t1;
 };
+
+// Plan limits: segments (k_write_cf keeps all of them in LDS beside its 12 KB
+// run windows) and the LDS the zone table + segments (+ day table) may use.
+constexpr int kMaxSegments = 1024;
+constexpr size_t kPlanLdsBytes = 60 * 1024;
 
 // per-node writer (cg_pernode.hip): output tasks of kNodeTask events per wave
 constexpr int kNodeTask = 8192;

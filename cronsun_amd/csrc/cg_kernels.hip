@@ -51,14 +51,15 @@ __device__ PlanView stage_plan(const PlanArgs& p, char* lds) {
   const int64_t* sg = reinterpret_cast<const int64_t*>(p.segs);
   int64_t* sd = reinterpret_cast<int64_t*>(s);
   for (int i = threadIdx.x; i < p.G * int(sizeof(Segment) / 8); i += blockDim.x) sd[i] = sg[i];
-  for (int i = threadIdx.x; i < p.nd; i += blockDim.x) d[i] = p.dtab[i];
+  if (!p.dtab_global)
+    for (int i = threadIdx.x; i < p.nd; i += blockDim.x) d[i] = p.dtab[i];
   __syncthreads();
   PlanView v;
   v.z.when = w;
   v.z.off = o;
   v.z.n = p.zn;
   v.segs = s;
-  v.dtab = d;
+  v.dtab = p.dtab_global ? p.dtab : d;
   return v;
 }
 
@@ -1122,7 +1123,8 @@ int grid_for(int64_t n, int threads, int max_blocks) {
 
 size_t plan_lds_bytes(const PlanArgs& p) {
   return align_up(size_t(p.zn) * 8, 16) + align_up(size_t(p.zn) * 4, 16) +
-         align_up(size_t(p.G) * sizeof(Segment), 16) + align_up(size_t(p.nd) * 4, 16);
+         align_up(size_t(p.G) * sizeof(Segment), 16) +
+         (p.dtab_global ? 0 : align_up(size_t(p.nd) * 4, 16));
 }
 
 void launch_checksum(const void* v, int64_t n, int elem_bytes, int64_t first, int64_t add,

@@ -241,8 +241,14 @@ int cg_count(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0, i
  *   t = t0; loop { t = Next(t); if t.IsZero() || t > t1 break; emit t }
  * i.e. the reference Next loop, batched.  Output is a rule-major CSR:
  *   offsets[R+1] (int64), times[offsets[R]] (int64, ascending per rule).
- * t1 - t0 must be <= CG_MAX_HORIZON seconds. */
-#define CG_MAX_HORIZON (366LL * 86400)
+ * The reference loop takes any horizon (its only limit is Next's own: no
+ * match within five calendar years of t returns the zero time and ends the
+ * rule, spec.go:70-76 -- reproduced).  Internally the horizon is cut into
+ * closed-form segments of <= 30 days, each continuing from the previous
+ * segment's last fire; t1 - t0 may be up to CG_MAX_HORIZON seconds (40
+ * years; CG_ERANGE beyond, or if a zone's transitions need more than 1024
+ * segments). */
+#define CG_MAX_HORIZON (14610LL * 86400)
 typedef struct {
   int64_t* offsets;  /* [R+1], caller-allocated (may be NULL) */
   int64_t* times;    /* [times_cap], caller-allocated (may be NULL) */

@@ -17,18 +17,39 @@ static const char* atoms[6][16] = {
     {"*", "?", "1", "2", "Feb", "Jan,Jul", "Apr-Oct", "*/3", "Mar", "Nov", "Dec", "*", "*", "*", "Oct", "Sep-Dec"},
     {"*", "?", "0", "1-5", "Mon", "Sun", "mon/2", "Sat,Sun", "*/2", "3", "fri-sat", "*", "*", "0", "6", "?"}};
 
+// long-horizon mode: sparse specs (at most one fire per matching hour) so that
+// multi-year horizons stay cheap for the oracle's literal loop
+static const char* long_atoms[6][8] = {
+    {"0", "30", "15", "0", "0", "45", "0", "7"},
+    {"0", "30", "0,30", "15", "0", "59", "0", "1"},
+    {"*", "0", "9", "*/6", "12", "2", "1", "23"},
+    {"*", "?", "1", "15", "29", "31", "28-31", "1,15"},
+    {"*", "Feb", "Jan,Jul", "*/3", "Mar", "Nov", "*", "Feb"},
+    {"*", "?", "Mon", "Sun", "1-5", "?", "*", "Sat"}};
+static const char* long_specials[] = {"@yearly", "@monthly", "@weekly", "@daily", "0 0 0 29 Feb ?",
+                                      "59 59 23 28,29 Feb ?", "0 0 12 29 Feb Mon", "0 30 2 * * *",
+                                      "0 30 1 * * Sun", "0 0 0 31 * ?", "0 0 0 30 Feb ?"};
+
 int main(int argc, char** argv) {
   const char* zone = argc > 1 ? argv[1] : "UTC";
   int nspec = argc > 2 ? atoi(argv[2]) : 400;
+  const bool long_mode = argc > 4 && std::string(argv[4]) == "long";
   ZoneRules zr;
   or_loc* ol = nullptr;
   load_zone(zone, &zr, &ol);
   std::mt19937_64 rng(argc > 3 ? strtoull(argv[3], nullptr, 10) : 777);
   std::vector<or_sched> scheds;
   std::vector<std::string> names;
+  size_t nspecial = 0;
   while ((int)scheds.size() < nspec) {
     std::string spec;
-    if (rng() % 10 == 0) spec = "@every " + std::to_string(1 + rng() % 7200) + "s";
+    if (long_mode && nspecial < sizeof long_specials / sizeof long_specials[0])
+      spec = long_specials[nspecial++];
+    else if (long_mode && rng() % 10 == 0)
+      spec = "@every " + std::to_string(3600 + rng() % (3 * 86400)) + "s";
+    else if (long_mode)
+      for (int f = 0; f < 6; f++) { if (f) spec += " "; spec += long_atoms[f][rng() % 8]; }
+    else if (rng() % 10 == 0) spec = "@every " + std::to_string(1 + rng() % 7200) + "s";
     else for (int f = 0; f < 6; f++) { if (f) spec += " "; spec += atoms[f][rng() % 16]; }
     or_sched s;
     char err[256];
@@ -44,6 +65,8 @@ int main(int argc, char** argv) {
     hz.push_back({tt.when[i] - 43217, tt.when[i] + 43200});
     hz.push_back({tt.when[i] - 3 * 86400, tt.when[i] + 4 * 86400});
   }
+  if (long_mode)  // three years from 2026; 2095-06-01 .. 2106-06-01 (Feb 29 gap over 2100)
+    hz = {{1767571200 - 77, 1767571200 + 1096 * 86400}, {3957984000, 3957984000 + 4018 * 86400}};
   int bad = 0;
   long long total = 0;
   for (auto [t0, t1] : hz) {

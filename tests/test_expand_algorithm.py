@@ -37,3 +37,13 @@ def test_host_algorithm_matches_oracle(expand_host, zone):
                          timeout=300)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     assert " 0 mismatches" in out.stdout
+
+
+@pytest.mark.parametrize("zone", ["UTC", "America/New_York", "Australia/Lord_Howe", "Africa/Casablanca"])
+def test_host_algorithm_long_horizons(expand_host, zone):
+    """Multi-year horizons (3 years from 2026; 2095-2106, where Feb 29 skips
+    2100 and Next's five-year limit returns the zero time, spec.go:70-76)."""
+    out = subprocess.run([expand_host, zone, "60", "5", "long"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert " 0 mismatches" in out.stdout

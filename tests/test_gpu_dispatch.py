@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from common import oracle_zone, product_zone, random_spec, to_oracle_sched
+from common import oracle_parse_all, oracle_zone, product_zone, random_spec
 
 pytestmark = pytest.mark.gpu
 
@@ -48,7 +48,7 @@ def test_dispatcher_vs_oracle(eng, zone, t0):
     n = 1500
     specs = [random_spec(rng) for _ in range(n)]
     scheds = [cron.Parse(s) for s in specs]
-    osch = [to_oracle_sched(s.to_c()) for s in scheds]
+    osch = oracle_parse_all(specs)  # the oracle's own parser
     oc = O.OracleCron(osch, oracle_zone(zone))
     z = product_zone(zone)
     oc.start(t0)
@@ -71,10 +71,11 @@ def test_dispatcher_vs_oracle(eng, zone, t0):
             if rng.random() < 0.5:
                 slots.append(next_slot)
                 next_slot += 1
-            new = [cron.Parse(random_spec(rng)) for _ in slots]
+            new_specs = [random_spec(rng) for _ in slots]
+            new = [cron.Parse(x) for x in new_specs]
             d.set(slots, new, now)
-            for s, sc in zip(slots, new):
-                oc.set(s, to_oracle_sched(sc.to_c()), now)
+            for s, osc in zip(slots, oracle_parse_all(new_specs)):
+                oc.set(s, osc, now)
             rm = [int(x) for x in rng.choice(n, 3, replace=False) if int(x) not in slots]
             d.remove(rm)
             for s in rm:

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from common import ZONES, oracle_zone, product_zone, random_spec, to_oracle_sched
+from common import ZONES, oracle_parse_all, oracle_zone, product_zone, random_spec, to_oracle_sched
 from cronsun_amd import _lib, cron, synth
 
 pytestmark = pytest.mark.gpu
@@ -22,14 +22,19 @@ def eng():
     return Engine(0)
 
 
-def oracle_csr(scheds, zone, t0, t1):
-    arr = O.sched_array([to_oracle_sched(s.to_c()) for s in scheds])
+def oracle_csr(scheds, zone, t0, t1, specs=None):
+    """The oracle's Next loop; with the spec strings it parses them with its
+    own parser (parser.go restated), so the product parser is checked too."""
+    if specs is not None:
+        arr = O.sched_array(oracle_parse_all(specs))
+    else:
+        arr = O.sched_array([to_oracle_sched(s.to_c()) for s in scheds])
     return O.expand_batch(arr, t0, t1, oracle_zone(zone), threads=8)
 
 
 def check_same(eng, scheds, zone, t0, t1, specs=None):
     try:
-        eo, et = oracle_csr(scheds, zone, t0, t1)
+        eo, et = oracle_csr(scheds, zone, t0, t1, specs)
     except O.NonTerminating as e:
         # the reference loop cycles for these rules: the engine must refuse the
         # batch with CG_ERANGE, and agree with the oracle on every other rule
@@ -109,17 +114,43 @@ def test_edge_cases(eng):
     # empty rule set
     off, times = eng.expand([], z, 0, 100)
     assert off.tolist() == [0] and times.size == 0
-    # the horizon limit is enforced
+    # the horizon limit (40 years) is enforced
     with pytest.raises(_lib.CgError) as e:
         eng.expand(scheds, z, 0, _lib.MAX_HORIZON + 1)
     assert e.value.code == _lib.CG_ERANGE
 
 
+LONG_SPECS = ["@yearly", "@monthly", "@weekly", "@daily", "0 0 0 29 Feb ?", "59 59 23 28,29 Feb ?",
+              "0 0 12 29 Feb Mon", "0 30 2 * * *", "0 30 1 * * Sun", "0 0 0 31 * ?", "0 0 0 30 Feb ?",
+              "0 15 10 15 * ?", "0 0 9 * * 1-5", "0 0 */6 1 Jan,Jul *", "@every 7h", "@every 90000s",
+              "30 59 23 31 Dec ?", "0 0 0 1 Jan ?"]
+
+
+@pytest.mark.parametrize("zone", ["UTC", "America/New_York", "Australia/Lord_Howe"])
+def test_multi_year_horizons(eng, zone):
+    """Horizons past one year (spec.go:70-76): three years from 2026, and
+    2095-06-01 .. 2106-06-01 where Feb 29 skips 2100, so Next's five-year
+    limit returns the zero time after 2096-02-29 and ends that rule's loop."""
+    rng = np.random.default_rng(zlib.crc32(("long" + zone).encode()))
+    specs = list(LONG_SPECS)
+    while len(specs) < 60:  # sparse random specs: at most one fire per matching hour
+        f = random_spec(rng).split(" ")
+        if len(f) >= 5 and not f[0].startswith("@"):
+            specs.append(" ".join([str(rng.integers(0, 60)), str(rng.integers(0, 60))] + f[2:]))
+    scheds = [cron.Parse(s) for s in specs]
+    off, _ = check_same(eng, scheds, zone, synth.T0_2026 - 77, synth.T0_2026 + 1096 * DAY, specs)
+    assert off[-1] > 100_000
+    off, times = check_same(eng, scheds, zone, 3957984000, 3957984000 + 4018 * DAY, specs)
+    feb29 = specs.index("0 0 0 29 Feb ?")
+    assert off[feb29 + 1] - off[feb29] == 1  # 2096-02-29 only: 2104 is past the limit
+
+
 def test_feb29_across_leap_years(eng):
-    scheds = [cron.Parse("0 0 0 29 Feb ?"), cron.Parse("59 59 23 28,29 Feb ?")]
+    specs = ["0 0 0 29 Feb ?", "59 59 23 28,29 Feb ?"]
+    scheds = [cron.Parse(s) for s in specs]
     t0 = 1704067200  # 2024-01-01
-    check_same(eng, scheds, "UTC", t0, t0 + 365 * DAY, ["feb29", "feb28/29"])
-    check_same(eng, scheds, "America/New_York", t0 + 40 * DAY, t0 + 70 * DAY, ["feb29", "feb28/29"])
+    check_same(eng, scheds, "UTC", t0, t0 + 365 * DAY, specs)
+    check_same(eng, scheds, "America/New_York", t0 + 40 * DAY, t0 + 70 * DAY, specs)
 
 
 def test_config2_scale_properties(eng):
@@ -145,7 +176,7 @@ def test_config2_scale_properties(eng):
     rng = np.random.default_rng(9)
     idx = np.sort(rng.choice(n, 3000, replace=False))
     sample = [cron.Parse(specs[i]) for i in idx]
-    eo, et = oracle_csr(sample, "UTC", t0, t1)
+    eo, et = oracle_csr(sample, "UTC", t0, t1, [specs[i] for i in idx])
     for k, i in enumerate(idx):
         got = times[off[i]:off[i + 1]]
         exp = et[eo[k]:eo[k + 1]]

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from common import oracle_zone, product_zone, random_spec, to_oracle_sched
+from common import oracle_parse_all, oracle_zone, product_zone, random_spec
 
 pytestmark = pytest.mark.gpu
 
@@ -41,7 +41,7 @@ def test_lock_ttl_vs_oracle(eng, zone):
     pick = rng.integers(0, n, n // 5)
     avg[pick] = np.array(AVGS, dtype=np.int64)[rng.integers(0, len(AVGS), len(pick))]
     oz = oracle_zone(zone)
-    osch = [to_oracle_sched(s.to_c()) for s in scheds]
+    osch = oracle_parse_all(specs)  # the oracle's own parser
     sp = eng.upload(scheds)
     for L in (300, 2, 86400):
         got = eng.lock_ttl_batch(sp, z, now, kind, avg, L)

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from common import ZONES, oracle_zone, product_zone, random_spec, to_oracle_sched
+from common import ZONES, oracle_zone, product_zone, random_spec
 
 pytestmark = pytest.mark.gpu
 
@@ -81,8 +81,9 @@ def test_random_specs_vs_oracle(eng, zone):
     got = eng.next_batch(scheds, z, t)
     oz = oracle_zone(zone)
     for i in range(n):
-        c = scheds[i].to_c()
-        exp = O.sched_next(to_oracle_sched(c), int(t[i]), oz)
+        osched, err = O.parse(specs[i])  # the oracle's own parser, not the product's masks
+        assert err is None, (specs[i], err)
+        exp = O.sched_next(osched, int(t[i]), oz)
         assert int(got[i]) == exp, (zone, specs[i], int(t[i]), int(got[i]), exp)
 
 

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
-from common import oracle_zone, product_zone, to_oracle_sched
+from common import oracle_parse_all, oracle_zone, product_zone
 from cronsun_amd import _lib, cron, synth
 
 pytestmark = pytest.mark.gpu
@@ -57,7 +57,7 @@ def test_per_node_fire_lists_vs_oracle(eng, mode, zone):
         t0, t1 = 1772953200 - 12 * 3600, 1772953200 + 12 * 3600
     node_off, time, rule = eng.expand_per_node(scheds, product_zone(zone), t0, t1, rin, mode)
     # oracle: per rule fire times, per rule node set, then node-major lists
-    arr = O.sched_array([to_oracle_sched(s.to_c()) for s in scheds])
+    arr = O.sched_array(oracle_parse_all(specs))  # the oracle's own parser
     eo, et = O.expand_batch(arr, t0, t1, oracle_zone(zone))
     rn = oracle_rule_nodes(rin, mode)
     per_node = [[] for _ in range(rin.n_nodes)]
