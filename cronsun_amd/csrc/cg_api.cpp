@@ -68,103 +68,6 @@ int cg_device_count(void) {
   return ok;
 }
 
-// ------------------------------------------------------------------ parse
-static void fill_schedule(const Schedule& s, cg_schedule* out) {
-  std::memset(out, 0, sizeof *out);
-  out->kind = s.kind;
-  out->second = s.second;
-  out->minute = s.minute;
-  out->hour = s.hour;
-  out->dom = s.dom;
-  out->month = s.month;
-  out->dow = s.dow;
-  out->delay_ns = s.delay_ns;
-}
-
-int cg_parse(int options, const char* spec, size_t len, cg_schedule* out, char* err,
-             size_t err_cap) {
-  if (!out || (!spec && len)) return cg_fail(CG_EINVAL, "cg_parse: null argument");
-  Schedule s;
-  std::string e;
-  int rc = parse(options, std::string_view(spec ? spec : "", len), &s, &e);
-  if (rc != 0) {
-    if (err && err_cap) {
-      std::strncpy(err, e.c_str(), err_cap - 1);
-      err[err_cap - 1] = 0;
-    }
-    return cg_fail(rc == -2 ? CG_EPANIC : CG_EPARSE, e);
-  }
-  fill_schedule(s, out);
-  return CG_OK;
-}
-
-int cg_parse_batch(int options, const char* const* specs, const size_t* lens, size_t n,
-                   cg_schedule* out, int32_t* status, int nthreads) {
-  if (n && (!specs || !lens || !out || !status)) return cg_fail(CG_EINVAL, "cg_parse_batch: null");
-  if (nthreads < 1) nthreads = 1;
-  if (size_t(nthreads) > n / 1024 + 1) nthreads = int(n / 1024 + 1);
-  auto work = [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; i++) {
-      Schedule s;
-      std::string e;
-      int rc = parse(options, std::string_view(specs[i] ? specs[i] : "", lens[i]), &s, &e);
-      if (rc == 0) {
-        fill_schedule(s, &out[i]);
-        status[i] = CG_OK;
-      } else {
-        std::memset(&out[i], 0, sizeof out[i]);
-        status[i] = rc == -2 ? CG_EPANIC : CG_EPARSE;
-      }
-    }
-  };
-  std::vector<std::thread> th;
-  size_t chunk = (n + nthreads - 1) / nthreads;
-  for (int t = 0; t < nthreads; t++) {
-    size_t lo = t * chunk, hi = std::min(n, lo + chunk);
-    if (lo >= hi) break;
-    th.emplace_back(work, lo, hi);
-  }
-  for (auto& x : th) x.join();
-  return CG_OK;
-}
-
-static int range_common(bool field, const char* expr, size_t len, unsigned min, unsigned max,
-                        int names, uint64_t* bits, char* err, size_t err_cap) {
-  if (!bits || (!expr && len)) return cg_fail(CG_EINVAL, "cg_get_range: null");
-  std::string e;
-  std::string_view v(expr ? expr : "", len);
-  int rc = field ? get_field(v, min, max, names, bits, &e) : get_range(v, min, max, names, bits, &e);
-  if (rc) {
-    if (err && err_cap) {
-      std::strncpy(err, e.c_str(), err_cap - 1);
-      err[err_cap - 1] = 0;
-    }
-    return cg_fail(CG_EPARSE, e);
-  }
-  return CG_OK;
-}
-
-int cg_get_range(const char* expr, size_t len, unsigned min, unsigned max, int names,
-                 uint64_t* bits, char* err, size_t err_cap) {
-  return range_common(false, expr, len, min, max, names, bits, err, err_cap);
-}
-
-int cg_get_field(const char* expr, size_t len, unsigned min, unsigned max, int names,
-                 uint64_t* bits, char* err, size_t err_cap) {
-  return range_common(true, expr, len, min, max, names, bits, err, err_cap);
-}
-
-uint64_t cg_get_bits(unsigned min, unsigned max, unsigned step) { return get_bits(min, max, step); }
-
-int64_t cg_every(int64_t d) { return every(d); }
-
-int cg_parse_duration(const char* s, size_t len, int64_t* out) {
-  if (!out) return cg_fail(CG_EINVAL, "cg_parse_duration: null");
-  std::string e;
-  if (parse_duration(std::string_view(s ? s : "", len), out, &e)) return cg_fail(CG_EPARSE, e);
-  return CG_OK;
-}
-
 // ------------------------------------------------------------------ zones
 int cg_zone_from_tzif(const uint8_t* data, size_t len, cg_zone** out) {
   if (!data || !out) return cg_fail(CG_EINVAL, "cg_zone_from_tzif: null");
