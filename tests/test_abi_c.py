@@ -125,4 +125,8 @@ def test_c_consumer_expansion_rate(abi_c, tmp_path):
     b = lines["B"][0].split()
     rec = dict(zip(b[0::2], b[1::2]))
     print("C consumer:", rec)
+    if os.environ.get("CG_TEST_RECORD_DIR"):  # tools/gpu_check.sh keeps the record
+        import json
+        with open(os.path.join(os.environ["CG_TEST_RECORD_DIR"], "abi_c_bench.json"), "w") as f:
+            json.dump(rec, f)
     assert int(rec["rules"]) == 1_000_000 and int(rec["events"]) == 674766895

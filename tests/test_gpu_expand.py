@@ -139,7 +139,7 @@ def test_multi_year_horizons(eng, zone):
             specs.append(" ".join([str(rng.integers(0, 60)), str(rng.integers(0, 60))] + f[2:]))
     scheds = [cron.Parse(s) for s in specs]
     off, _ = check_same(eng, scheds, zone, synth.T0_2026 - 77, synth.T0_2026 + 1096 * DAY, specs)
-    assert off[-1] > 100_000
+    assert off[-1] > 10_000
     off, times = check_same(eng, scheds, zone, 3957984000, 3957984000 + 4018 * DAY, specs)
     feb29 = specs.index("0 0 0 29 Feb ?")
     assert off[feb29 + 1] - off[feb29] == 1  # 2096-02-29 only: 2104 is past the limit

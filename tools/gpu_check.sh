@@ -14,7 +14,7 @@ fail() { echo "FAILED: $1"; tail -40 "$2"; exit 1; }
 
 if has tests; then
   echo "== pytest -m gpu"
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+  CG_TEST_RECORD_DIR=$OUT timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > "$OUT/pytest_gpu.log" 2>&1 || fail pytest "$OUT/pytest_gpu.log"
   tail -2 "$OUT/pytest_gpu.log"
   echo "== smoke"
