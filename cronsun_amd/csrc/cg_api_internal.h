@@ -103,16 +103,21 @@ struct cg_ctx {
   int64_t* res_dev = nullptr;      // res_host's device address
   int64_t last_E = 0, last_R = 0, last_G = 0;
 
-  // per-node buffers
-  DBuf<int64_t> rn_off, rn_cnt64, pair_pos, pair_src, node_off, node_time, nt_off;
-  DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule;
+  // per-node buffers: the rule->node join (rule-major pairs), its node-major
+  // transpose, the (node, rule band) segments and the node CSR
+  DBuf<int64_t> rn_off, node_off, node_time, nt_off, rs_off, seg_pair, seg_cnt, seg_pos;
+  DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule, rs_hist;
+  DBuf<uint32_t> pn_tickets;
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
-  DBuf<char> pn_tmp;
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
+  int64_t* pn_res_host = nullptr;  // mapped pinned: per-node event total of the last call
+  int64_t* pn_res_dev = nullptr;
   // the rule->node join + transpose depend only on (rule set, exclude mode):
-  // kept across per-node calls on the same uploaded rule set (time windows)
+  // kept across per-node calls on the same uploaded rule set (time windows);
+  // the segment bounds also on the band width
   uint64_t pn_cache_serial = 0;
   int pn_cache_mode = -1;
+  int32_t pn_B = 0, pn_K = 0;  // rules per band, bands of the cached segment bounds (0: none)
 
   void free_all() {
     plan_dev.release();
@@ -123,10 +128,13 @@ struct cg_ctx {
     res_host = nullptr;
     res_dev = nullptr;
     run_dmask.release(); scan_tmp.release(); stuck.release(); cksum.release();
-    rn_off.release(); rn_cnt64.release(); pair_pos.release(); pair_src.release(); node_off.release();
-    node_time.release(); nt_off.release(); rn_cnt.release(); rn_nodes.release();
+    rn_off.release(); node_off.release(); node_time.release(); nt_off.release(); rs_off.release();
+    seg_pair.release(); seg_cnt.release(); seg_pos.release(); rn_cnt.release(); rn_nodes.release();
     pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();
-    rules.release(); pn_tmp.release();
+    rs_hist.release(); pn_tickets.release(); rules.release();
+    if (pn_res_host) (void)hipHostFree(pn_res_host);
+    pn_res_host = nullptr;
+    pn_res_dev = nullptr;
   }
 };
 

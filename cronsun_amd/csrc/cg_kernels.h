@@ -24,8 +24,6 @@ struct PlanArgs {
 constexpr int kMaxSegments = 1024;
 constexpr size_t kPlanLdsBytes = 60 * 1024;
 
-// per-node writer (cg_pernode.hip): output tasks of kNodeTask events per wave
-constexpr int kNodeTask = 8192;
 // closed-form writer: 4 waves per block; waves take kSuper-event output slices
 constexpr int kWriteWaves = 4;
 #ifndef CG_WRITE_BPC
@@ -89,6 +87,8 @@ void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run
 // exclusive scan of n int32 counts into out[0..n] (out[n] = total)
 size_t scan_temp_bytes(int64_t n);
 void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st);
+// the same over int64 counts
+void launch_scan64(const int64_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st);
 // expansion scan (R*G > 0 run counts): also writes the per-rule offsets
 // (offsets[r] = run_off[r*G]), res = {E, stuck rule} and re-arms *stuck;
 // with chunk_run (else null) also the writer's slice map for capacity cap

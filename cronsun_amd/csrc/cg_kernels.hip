@@ -381,8 +381,8 @@ __device__ int64_t block_excl_scan(int64_t x, int64_t* tot) {
   return base + inc - x;
 }
 
-__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const int32_t* __restrict__ in,
-                                                               int64_t n,
+template <class T>
+__global__ __launch_bounds__(kScanThreads) void k_scan_reduce(const T* __restrict__ in, int64_t n,
                                                                int64_t* __restrict__ partial) {
   int64_t base = int64_t(blockIdx.x) * kScanTile;
   int64_t acc = 0;
@@ -427,9 +427,8 @@ struct RunTail {
 
 // kFused: the tile's carry is the sum of the earlier tiles' totals, summed by
 // the block itself (no k_scan_top launch; used while nb <= kScanFuseTiles)
-template <bool kFused>
-__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __restrict__ in,
-                                                              int64_t n,
+template <class T, bool kFused>
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(const T* __restrict__ in, int64_t n,
                                                               const int64_t* __restrict__ partial,
                                                               int64_t* __restrict__ out,
                                                               RunTail tail) {
@@ -444,7 +443,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const int32_t* __re
     carry = partial[blockIdx.x];
   }
   int64_t base = int64_t(blockIdx.x) * kScanTile + int64_t(threadIdx.x) * kScanPerThread;
-  int32_t v[kScanPerThread];
+  T v[kScanPerThread];
   int64_t acc = 0;
 #pragma unroll
   for (int i = 0; i < kScanPerThread; i++) {
@@ -1215,22 +1214,30 @@ size_t scan_temp_bytes(int64_t n) {
   return size_t(nb + 1) * sizeof(int64_t);
 }
 
-static void scan_impl(const int32_t* in, int64_t* out, int64_t n, void* temp, RunTail tail,
-                      hipStream_t st) {
+template <class T>
+static void scan_impl(const T* in, int64_t* out, int64_t n, void* temp, RunTail tail, hipStream_t st) {
   int64_t nb = (n + kScanTile - 1) / kScanTile;
   int64_t* partial = static_cast<int64_t*>(temp);
-  hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial);
+  hipLaunchKernelGGL(k_scan_reduce<T>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial);
   if (nb <= kScanFuseTiles) {
-    hipLaunchKernelGGL(k_scan_apply<true>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out,
+    hipLaunchKernelGGL((k_scan_apply<T, true>), dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out,
                        tail);
     return;
   }
   hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanThreads), 0, st, partial, nb);
-  hipLaunchKernelGGL(k_scan_apply<false>, dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out,
+  hipLaunchKernelGGL((k_scan_apply<T, false>), dim3(nb), dim3(kScanThreads), 0, st, in, n, partial, out,
                      tail);
 }
 
 void launch_scan(const int32_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st) {
+  if (n <= 0) {
+    (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
+    return;
+  }
+  scan_impl(in, out, n, temp, RunTail{nullptr, nullptr, nullptr, 1, nullptr, 0}, st);
+}
+
+void launch_scan64(const int64_t* in, int64_t* out, int64_t n, void* temp, hipStream_t st) {
   if (n <= 0) {
     (void)hipMemsetAsync(out, 0, sizeof(int64_t), st);
     return;

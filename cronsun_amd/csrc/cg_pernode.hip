@@ -12,15 +12,16 @@
 //   k_rule_nodes<false>  one wave per rule: node bitmap in LDS (ds_or), count
 //   scan                 -> rule->node CSR offsets
 //   k_rule_nodes<true>   same bitmap, ballot/prefix-sum compaction of set bits
-//   radix sort (node)    stable transpose to node -> rules (rocPRIM)
+//   k_rs_hist/scatter    stable LSD radix transpose to node -> rules (8 bits a pass)
 //   k_node_bounds        per-node pair offsets (lower bound per node)
-//   pair event counts -> scan -> per-node offsets
-//   k_node_write         output-parallel copy of each rule's fire times into
-//                        every node list that contains the rule (whole
-//                        64-event blocks, pairs found by shuffle search)
+//   (cached per rule set and exclude mode up to here)
+//   k_seg_bounds         (node, rule band) segment bounds (cached per band width)
+//   k_seg_count -> scan  events per segment -> segment and node offsets
+//   k_node_write         per segment, in band-major order: each node's copy of
+//                        its rules' fire times (whole 64-event blocks; pairs
+//                        placed by a wave prefix sum, blocks spanning pairs
+//                        resolved by an LDS start mask + popcount)
 #include <hip/hip_runtime.h>
-
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <atomic>
@@ -147,46 +148,151 @@ __global__ void k_node_bounds(const uint32_t* __restrict__ keys, int64_t n, int3
   nt_off[v] = lo;
 }
 
-// per (node, rule) pair: its event count and its rule's fire-list start
-__global__ void k_pair_events(const int32_t* __restrict__ nt_rule, int64_t nnz,
-                              const int64_t* __restrict__ rule_off, int32_t* __restrict__ ev,
-                              int64_t* __restrict__ src) {
-  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < nnz;
-       i += int64_t(gridDim.x) * blockDim.x) {
-    const int32_t r = nt_rule[i];
-    const int64_t a = rule_off[r];
-    ev[i] = int32_t(rule_off[r + 1] - a);
-    src[i] = a;
-  }
-}
-
-__global__ void k_node_offsets(const int64_t* __restrict__ nt_off, const int64_t* __restrict__ pair_pos,
-                               int32_t N, int64_t* __restrict__ node_off) {
-  int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (n <= N) node_off[n] = pair_pos[nt_off[n]];
-}
-
 __global__ void k_node_counts(const int64_t* __restrict__ node_off, int32_t N, int64_t* __restrict__ out) {
   int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
   if (n < N) out[n] = node_off[n + 1] - node_off[n];
 }
 
-__device__ __forceinline__ int64_t search_le(const int64_t* __restrict__ off, int64_t lo, int64_t hi,
-                                             int64_t x) {
-  while (lo < hi) {
-    int64_t mid = (lo + hi + 1) >> 1;
-    if (off[mid] <= x) lo = mid;
-    else hi = mid - 1;
+// ---- transpose: stable LSD radix sort of the rule-major (node, rule) pairs
+// by node, 8 bits per pass.  Each pass keeps the order of equal digits, so
+// rules stay ascending within every node (the order Job.Cmds is evaluated in
+// when a node walks the jobs, job.go:591-614). ----
+constexpr int kRsItems = 16;
+constexpr int kRsTile = 256 * kRsItems;  // pairs per block
+constexpr int kRsBuckets = 256;
+
+__global__ __launch_bounds__(256) void k_rs_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
+                                                  int32_t* __restrict__ hist, int64_t nb) {
+  __shared__ uint32_t h[kRsBuckets];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t base = int64_t(blockIdx.x) * kRsTile;
+  for (int j = 0; j < kRsItems; j++) {
+    const int64_t i = base + j * 256 + threadIdx.x;
+    if (i < n) atomicAdd(&h[(keys[i] >> shift) & (kRsBuckets - 1)], 1u);
   }
-  return lo;
+  __syncthreads();
+  hist[int64_t(threadIdx.x) * nb + blockIdx.x] = int32_t(h[threadIdx.x]);  // digit-major
 }
 
-// first pair touched by each kNodeTask-event output task
-__global__ void k_pair_block_map(const int64_t* __restrict__ pair_pos, int64_t nnz, int64_t ntasks,
-                                 int64_t* __restrict__ task_pair) {
-  int64_t b = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (b > ntasks) return;
-  task_pair[b] = b == ntasks ? nnz - 1 : search_le(pair_pos, 0, nnz - 1, b * int64_t(kNodeTask));
+// One pass's stable scatter.  Input order inside a block: wave w owns pairs
+// [tile + w*1024, +1024), item j the 64 pairs [j*64, j*64 + 64) of those.  A
+// pair's rank among equal digits = earlier items of its wave (running counts
+// in LDS) + earlier lanes of its item (8-ballot multisplit) + earlier waves
+// (prefix per digit) + earlier blocks (the scanned digit-major histogram).
+__global__ __launch_bounds__(256) void k_rs_scatter(const uint32_t* __restrict__ kin,
+                                                     const int32_t* __restrict__ vin, int64_t n, int shift,
+                                                     const int64_t* __restrict__ off, int64_t nb,
+                                                     uint32_t* __restrict__ kout, int32_t* __restrict__ vout) {
+  __shared__ int32_t run[4][kRsBuckets];
+  __shared__ int64_t base_of[4][kRsBuckets];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 4 * kRsBuckets; i += 256) (&run[0][0])[i] = 0;
+  __syncthreads();
+  const int64_t base = int64_t(blockIdx.x) * kRsTile + int64_t(w) * (64 * kRsItems);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t key[kRsItems];
+  int32_t val[kRsItems], rk[kRsItems];
+#pragma unroll
+  for (int j = 0; j < kRsItems; j++) {
+    const int64_t i = base + j * 64 + lane;
+    key[j] = i < n ? kin[i] : 0u;
+    val[j] = i < n ? vin[i] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kRsItems; j++) {
+    const bool valid = base + j * 64 + lane < n;
+    const uint32_t d = (key[j] >> shift) & (kRsBuckets - 1);
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; b++) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    // every lane reads the running count before the group's first lane adds
+    // the group size (a wave's LDS operations complete in program order)
+    const int32_t r0 = run[w][d];
+    rk[j] = r0 + __popcll(peers & lt);
+    if (valid && (peers & lt) == 0) run[w][d] = r0 + __popcll(peers);
+  }
+  __syncthreads();
+  {
+    const int d = threadIdx.x;
+    int64_t acc = off[int64_t(d) * nb + blockIdx.x];
+    for (int ww = 0; ww < 4; ww++) {
+      base_of[ww][d] = acc;
+      acc += run[ww][d];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRsItems; j++) {
+    if (base + j * 64 + lane >= n) continue;
+    const int64_t pos = base_of[w][(key[j] >> shift) & (kRsBuckets - 1)] + rk[j];
+    kout[pos] = key[j];
+    vout[pos] = val[j];
+  }
+}
+
+// ---- per-call segments: (node n, rule band k) = node n's pairs whose rule is
+// in [k*B, (k+1)*B).  Bands keep a band's rule fire lists (and their
+// offsets) L2-resident while every node's segment of the band is written. ----
+
+// seg_pair[n*K + k] = first pair of node n with rule >= k*B; [N*K] = nnz
+__global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* __restrict__ nt_rule,
+                             int32_t N, int32_t K, int32_t B, int64_t* __restrict__ seg_pair) {
+  const int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  const int64_t NK = int64_t(N) * K;
+  if (t > NK) return;
+  if (t == NK) {
+    seg_pair[t] = nt_off[N];
+    return;
+  }
+  const int32_t n = int32_t(t / K), k = int32_t(t - int64_t(n) * K);
+  int64_t lo = nt_off[n], hi = nt_off[n + 1];
+  const int64_t x = int64_t(k) * B;
+  while (lo < hi) {  // first pair with rule >= x
+    const int64_t mid = (lo + hi) >> 1;
+    if (int64_t(nt_rule[mid]) < x) lo = mid + 1;
+    else hi = mid;
+  }
+  seg_pair[t] = lo;
+}
+
+// Events per segment: sum over its pairs of the rule's fire count (rule-major
+// offsets of the expansion).  One wave per segment, band-major order so the
+// band's offsets stay in L2.  Block 0 also resets the writer's tickets.
+__global__ __launch_bounds__(256) void k_seg_count(const int64_t* __restrict__ seg_pair,
+                                                    const int32_t* __restrict__ nt_rule,
+                                                    const int64_t* __restrict__ rule_off, int32_t N,
+                                                    int32_t K, int64_t* __restrict__ seg_cnt,
+                                                    uint32_t* __restrict__ tickets) {
+  if (blockIdx.x == 0 && threadIdx.x < kTicketGroups * kTicketStride) tickets[threadIdx.x] = 0;
+  const int lane = threadIdx.x & 63;
+  const int64_t NK = int64_t(N) * K;
+  const int64_t nw = int64_t(gridDim.x) * (blockDim.x >> 6);
+  for (int64_t t = blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6); t < NK; t += nw) {
+    const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
+    const int64_t s = int64_t(n) * K + k;
+    const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
+    int64_t acc = 0;
+    for (int64_t p = p0 + lane; p < p1; p += 64) {
+      const int32_t r = nt_rule[p];
+      acc += rule_off[r + 1] - rule_off[r];
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if (lane == 0) seg_cnt[s] = acc;
+  }
+}
+
+// node_off[n] = seg_pos[n*K] (n <= N); the total is also stored to res
+__global__ void k_node_off_from_seg(const int64_t* __restrict__ seg_pos, int32_t N, int32_t K,
+                                    int64_t* __restrict__ node_off, int64_t* __restrict__ res) {
+  const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (n > N) return;
+  node_off[n] = seg_pos[n * K];
+  if (n == N) res[0] = seg_pos[n * K];
 }
 
 __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
@@ -194,116 +300,138 @@ __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
   const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v) >> 32)), i));
   return int64_t((uint64_t(hi) << 32) | lo);
 }
+__device__ __forceinline__ int64_t bperm64(int64_t v, int src) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, int(uint32_t(v)));
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, int(uint32_t(uint64_t(v) >> 32)));
+  return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+}
+__device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: push to lane dst
+  const int lo = __builtin_amdgcn_ds_permute(dst << 2, int(uint32_t(v)));
+  const int hi = __builtin_amdgcn_ds_permute(dst << 2, int(uint32_t(uint64_t(v) >> 32)));
+  return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+}
 
-// Per-node lists: node event e copies fire k of the rule of its (node, rule)
-// pair.  Waves take kNodeTask-event output tasks; a wave keeps 64 consecutive
-// pairs in registers (lane i: pair jw + i, its output start, end, rule and
-// the rule's fire-list start) and fills its task in aligned 64-event blocks:
-// lane l finds the pair of event b + l by a 6-step shuffle search, gathers the
-// fire time (rule lists are re-read once per node of the rule: L2/MALL hits)
-// and the block is stored whole (8-B times, 4-B rule indices).  (Two blocks
-// per round with independent searches measured slower: 7 waves per SIMD.)
-// (A wave-uniform walk over the pairs instead of the search measured 1.5x
-// slower: ~10 fires per pair make the per-pair readlane chain the bottleneck.)
+// Per-node lists, one (node, band) segment per wave task, tasks taken by
+// ticket in band-major order (every node's segment of band 0, then band 1, ...)
+// so the band's rule-major fire lists are read from L2 by all of them.  A
+// wave walks its segment's pairs 64 at a time: lane i loads pair i's rule,
+// the rule's fire-list start and count (rule-major offsets), a wave prefix
+// sum places the pairs, and the non-empty ones are compacted into lanes
+// 0..nc-1 (ds_permute).  The output is filled in aligned 64-event blocks:
+//   - inside one pair: one uniform shift, a coalesced 512-B gather;
+//   - across pairs: each pair starting in the block marks its first lane in a
+//     per-wave LDS row (tagged, no clearing), a ballot of the marks gives the
+//     start mask M, and lane l's pair is prev + popcount(M & lanes <= l).
+// A block shared with the next window of the same segment is carried in
+// registers; only blocks at segment edges are stored partially.
+// V (diagnostic build only): 1 = no gather (synthetic values), 2 = no stores.
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
-    const int64_t* __restrict__ pair_pos, const int32_t* __restrict__ nt_rule,
-    const int64_t* __restrict__ task_pair, const int64_t* __restrict__ pair_src,
-    const int64_t* __restrict__ times, int64_t En, int64_t nnz, int64_t* __restrict__ out_time,
-    int32_t* __restrict__ out_rule) {
+    const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
+    const int32_t* __restrict__ nt_rule, const int64_t* __restrict__ rule_off,
+    const int64_t* __restrict__ times, int32_t N, int32_t K, int64_t cap,
+    uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time, int32_t* __restrict__ out_rule) {
+  __shared__ uint32_t marks_all[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t ntasks = (En + kNodeTask - 1) / kNodeTask;
-  const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x >> 6);
-  for (int64_t t = int64_t(blockIdx.x) * (blockDim.x >> 6) + wave; t < ntasks; t += nwaves) {
-    const int64_t B0 = t * kNodeTask;
-    const int64_t B1 = En - B0 < kNodeTask ? En : B0 + kNodeTask;
-    const int64_t jend = task_pair[t + 1] + 1;  // pairs this task can touch
-    int64_t jw = task_pair[t];
-    // lane i: pair jw + i as (output start - B0) clamped to int32, and the
-    // fire-list shift delta = rule list start - output start (event e of the
-    // pair reads times[e + delta]): 3 shuffles per event instead of 5, and
-    // 32-bit search steps
-    int32_t dst = INT32_MAX;
-    int64_t delta = 0, dend = INT64_MAX;
-    int32_t rr = 0;
-    // the next window's raw loads are issued one window ahead
-    int64_t n_d = INT64_MAX, n_dend = INT64_MAX, n_src = 0;
-    int32_t n_r = 0;
-    auto fetch = [&](int64_t base) {
-      const int64_t p = base + lane;
-      if (p < jend) {
-        n_d = pair_pos[p];
-        n_dend = pair_pos[p + 1];
-        n_r = nt_rule[p];
-        n_src = pair_src[p];
-      } else {
-        n_d = INT64_MAX;
+  uint32_t* marks = marks_all[wave];
+  marks[lane] = 0u;
+  uint32_t tag = 0;
+  const int64_t NK = int64_t(N) * K;
+  if (seg_pos[NK] > cap) return;  // output too small: the host grows it and relaunches
+  const uint64_t le = (2ull << lane) - 1ull;  // lanes <= this one
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
+  const int grp = int(blockIdx.x % unsigned(ng));
+  auto take = [&]() -> int64_t {
+    unsigned int t = 0;
+    if (lane == 0) t = atomicAdd(tickets + grp * kTicketStride, 1u);
+    return grp + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
+  };
+  for (int64_t t = take(); t < NK;) {
+    const int64_t t_next = take();
+    const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
+    const int64_t s = int64_t(n) * K + k;
+    const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
+    const int64_t o0 = seg_pos[s], o1 = seg_pos[s + 1];
+    t = t_next;
+    if (o0 == o1) continue;
+    int64_t pblk = -1, ptime = 0;  // a block carried into the next window
+    int32_t prule = 0;
+    int64_t ow = o0;  // output start of the current window
+    int32_t nr = 0;
+    if (p0 + lane < p1) nr = nt_rule[p0 + lane];
+    for (int64_t pw = p0; pw < p1; pw += 64) {
+      const bool valid = pw + lane < p1;
+      const int32_t r = nr;
+      if (pw + 64 + lane < p1) nr = nt_rule[pw + 64 + lane];  // next window's rules, one ahead
+      const int64_t a = valid ? rule_off[r] : 0;
+      const int64_t c = valid ? rule_off[r + 1] - a : 0;
+      int64_t incl = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
       }
-    };
-    auto load = [&]() {  // window jw from the prefetched loads, then prefetch jw + 64
-      if (n_d != INT64_MAX) {
-        dend = n_dend;
-        rr = n_r;
-        delta = n_src - n_d;
-        dst = int32_t(n_d - B0 < int64_t(INT32_MAX)
-                          ? (n_d - B0 > INT32_MIN ? n_d - B0 : INT32_MIN + 1)
-                          : INT32_MAX - 1);
-      } else {
-        dst = INT32_MAX;
-        dend = INT64_MAX;
-        rr = 0;
-        delta = 0;
-      }
-      fetch(jw + 64);
-    };
-    fetch(jw);
-    load();
-    // jc: window lane of the pair that holds event b (wave-uniform), -1 when
-    // unknown.  A full block inside that one pair (long fire lists: second-
-    // granularity and frequent @every rules carry most node events) needs no
-    // search: one uniform shift, a coalesced 512-B read and the stores.
-    int jc = -1;
-    for (int64_t b = B0; b < B1; b += 64) {
-      const int64_t e = b + lane;
-      int64_t val = 0;
-      int32_t rv = 0;
-      if (jc >= 0 && b + 64 <= B1 && rl64n(dend, jc) >= b + 64) {
-        const int64_t d = rl64n(delta, jc);
-        val = (V & 1) ? e + d : times[e + d];
-        rv = __builtin_amdgcn_readlane(rr, jc);
-      } else {
-        bool done = e >= B1;
-        int j = 0;
-        for (;;) {
-          const int L = 63 - __builtin_clzll(__ballot(dst != INT32_MAX));
-          const int64_t wend = rl64n(dend, L);
-          j = 0;
-#pragma unroll
-          for (int st = 32; st > 0; st >>= 1) {
-            const int32_t v = __shfl(dst, (j + st) & 63, 64);
-            if (j + st < 64 && int64_t(v) <= e - B0) j += st;
+      const int64_t tot = rl64n(incl, 63);
+      if (tot == 0) continue;
+      // compact the non-empty pairs into lanes 0..nc-1 (a permutation)
+      const uint64_t NE = __ballot(c > 0);
+      const int nc = __popcll(NE);
+      const int ci = __popcll(NE & lt);
+      const int dstl = c > 0 ? ci : nc + (lane - ci);
+      const int64_t dst = perm64(ow + incl - c, dstl);  // output start of compacted pair
+      const int64_t delta = perm64(a - (ow + incl - c), dstl);  // fire-list index - output index
+      const int32_t rr = __builtin_amdgcn_ds_permute(dstl << 2, r);
+      const int64_t we = ow + tot;  // window output end
+      int cprev = -1;  // compacted pair holding event b - 1 (-1: before this window)
+      for (int64_t b = ow & ~int64_t(63); b < we; b += 64) {
+        const int64_t e = b + lane;
+        int64_t val = 0;
+        int32_t rv = 0;
+        int cb = cprev;  // the pair holding event b, when b lies in this window
+        if (b >= ow && cprev + 1 < nc && rl64n(dst, cprev + 1) == b) cb = cprev + 1;
+        const int64_t cb_end = cb >= 0 ? (cb + 1 < nc ? rl64n(dst, cb + 1) : we) : 0;
+        if (b >= ow && cb >= 0 && cb_end >= b + 64) {
+          const int64_t dl = rl64n(delta, cb);
+          val = (V & 1) ? e + dl : times[e + dl];
+          rv = __builtin_amdgcn_readlane(rr, cb);
+          cprev = cb;
+        } else {
+          tag++;
+          if (lane < nc && dst >= b && dst < b + 64) marks[dst - b] = tag;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const uint64_t M = __ballot(marks[lane] == tag);
+          int own = cprev + __popcll(M & le);
+          const bool mine = e >= ow && e < we;
+          own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
+          const int64_t dl = bperm64(delta, own);
+          const int32_t ro = __builtin_amdgcn_ds_bpermute(own << 2, rr);
+          if (mine) {
+            val = (V & 1) ? e + dl : times[e + dl];
+            rv = ro;
           }
-          const int64_t jdelta = __shfl(delta, j, 64);
-          const int32_t jr = __shfl(rr, j, 64);
-          if (!done && e < wend) {
-            val = (V & 1) ? e + jdelta : times[e + jdelta];
-            rv = jr;
-            done = true;
-          }
-          if (__ballot(!done) == 0) break;
-          jw += 64;  // some lane's event lies past the window's last pair
-          load();
+          cprev = __builtin_amdgcn_readlane(own, 63);
         }
-        // the pair of the block's last event, in the final window (a full
-        // block's lane 63 is found in the last window visited)
-        jc = b + 64 <= B1 ? __builtin_amdgcn_readlane(j, 63) : -1;
+        if (b == pblk && e < ow) {  // lanes of the previous window
+          val = ptime;
+          rv = prule;
+        }
+        if (b + 64 <= we || we == o1) {  // complete, or the segment's last block
+          if (!(V & 2) && e >= o0 && e < o1) {
+            out_time[e] = val;
+            out_rule[e] = rv;
+          } else if (V & 2) {
+            asm volatile("" ::"v"(val), "v"(rv));
+          }
+          pblk = -1;
+        } else {
+          pblk = b;
+          ptime = val;
+          prule = rv;
+        }
       }
-      if (V & 2) {
-        asm volatile("" ::"v"(val), "v"(rv));
-      } else if (e < B1) {
-        out_time[e] = val;
-        out_rule[e] = rv;
-      }
+      ow = we;
     }
   }
 }
@@ -422,6 +550,55 @@ int rule_nodes_locked(cg_ctx* c, const RulesStore& st, int mode, int64_t* nnz_ou
   return CG_OK;
 }
 
+// Stable transpose of the rule-major pairs (rn_nodes, pair_rule) into node
+// order: nt_rule (rules ascending within a node) and nt_off[N+1].
+int transpose_locked(cg_ctx* c, int64_t nnz, int32_t N) {
+  hipStream_t st = c->st;
+  int rc;
+  if ((rc = c->nt_rule.ensure(std::max<int64_t>(nnz, 1)))) return rc;
+  if ((rc = c->pair_node.ensure(std::max<int64_t>(nnz, 1)))) return rc;
+  if ((rc = c->nt_off.ensure(N + 1))) return rc;
+  uint32_t* kin = reinterpret_cast<uint32_t*>(c->rn_nodes.p);
+  int32_t* vin = c->pair_rule.p;
+  uint32_t* kout = reinterpret_cast<uint32_t*>(c->pair_node.p);
+  int32_t* vout = c->nt_rule.p;
+  if (nnz > 0) {
+    const int64_t nb = (nnz + kRsTile - 1) / kRsTile;
+    if ((rc = c->rs_hist.ensure(kRsBuckets * nb))) return rc;
+    if ((rc = c->rs_off.ensure(kRsBuckets * nb + 1))) return rc;
+    if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(kRsBuckets * nb))))) return rc;
+    int passes = 0;
+    for (int shift = 0; shift == 0 || (int64_t(1) << shift) < int64_t(N); shift += 8) {
+      hipLaunchKernelGGL(k_rs_hist, dim3(unsigned(nb)), dim3(256), 0, st, kin, nnz, shift, c->rs_hist.p, nb);
+      launch_scan(c->rs_hist.p, c->rs_off.p, kRsBuckets * nb, c->scan_tmp.p, st);
+      hipLaunchKernelGGL(k_rs_scatter, dim3(unsigned(nb)), dim3(256), 0, st, kin, vin, nnz, shift,
+                         c->rs_off.p, nb, kout, vout);
+      std::swap(kin, kout);
+      std::swap(vin, vout);
+      passes++;
+    }
+    // the sorted pairs are in (kin, vin): keep them in (pair_node, nt_rule)
+    if (passes % 2 == 0) {
+      std::swap(c->rn_nodes, c->pair_node);
+      std::swap(c->pair_rule, c->nt_rule);
+    }
+  }
+  hipLaunchKernelGGL(k_node_bounds, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
+                     reinterpret_cast<const uint32_t*>(c->pair_node.p), nnz, N, c->nt_off.p);
+  return cg_hip_check(hipGetLastError(), "transpose");
+}
+
+// Rules per band: the band's rule-major fire lists (E_band * 8 B) should sit
+// in one XCD's 4 MiB L2 beside the write stream; a power of two, so the
+// cached segment bounds stay valid across windows of similar volume.
+int32_t band_rules(int64_t R, int64_t E) {
+  const double per_rule = double(std::max<int64_t>(E, 1)) * 8.0 / double(std::max<int64_t>(R, 1));
+  int64_t B = int64_t(1.5 * 1024 * 1024 / per_rule);
+  int64_t p = 1024;
+  while (p < B && p < R) p <<= 1;
+  return int32_t(std::max<int64_t>(p, 1024));
+}
+
 int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
                     const RulesStore& in, int mode, int64_t* n_events, int64_t* nnz_out) {
   if (int64_t(s->n) != in.n_rules)
@@ -431,91 +608,88 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   if (rc) return rc;
   int64_t nnz = 0;
   const int32_t N = in.n_nodes;
+  const int64_t R = in.n_rules;
   hipStream_t st = c->st;
   const bool cached = in.serial != 0 && in.serial == c->pn_cache_serial && mode == c->pn_cache_mode;
-  (void)hipEventRecord(c->pev[0], c->st);
+  c->pn_E = 0;  // no readable result until this call succeeds
+  (void)hipEventRecord(c->pev[0], st);
   if (cached) {
     nnz = c->pn_nnz;
   } else {
     c->pn_cache_serial = 0;  // the transpose buffers are about to change
+    c->pn_K = 0;
     if ((rc = rule_nodes_locked(c, in, mode, &nnz))) return rc;
   }
-  (void)hipEventRecord(c->pev[1], c->st);
-  if ((rc = c->nt_off.ensure(N + 1))) return rc;
-  if ((rc = c->nt_rule.ensure(std::max<int64_t>(nnz, 1)))) return rc;
-  if ((rc = c->pair_node.ensure(std::max<int64_t>(nnz, 1)))) return rc;
-  if ((rc = c->node_off.ensure(N + 1))) return rc;
-  // transpose: stable radix sort of (node, rule) pairs by node
-  if (nnz > 0 && !cached) {
-    unsigned end_bit = 1;
-    while ((1u << end_bit) < unsigned(std::max(N, 2))) end_bit++;
-    size_t tmp_bytes = 0;
-    (void)rocprim::radix_sort_pairs(nullptr, tmp_bytes, reinterpret_cast<uint32_t*>(c->rn_nodes.p),
-                              reinterpret_cast<uint32_t*>(c->pair_node.p), c->pair_rule.p,
-                              c->nt_rule.p, size_t(nnz), 0, end_bit, st);
-    if ((rc = c->pn_tmp.ensure(tmp_bytes + 16))) return rc;
-    if ((rc = cg_hip_check(
-             rocprim::radix_sort_pairs(c->pn_tmp.p, tmp_bytes,
-                                       reinterpret_cast<uint32_t*>(c->rn_nodes.p),
-                                       reinterpret_cast<uint32_t*>(c->pair_node.p), c->pair_rule.p,
-                                       c->nt_rule.p, size_t(nnz), 0, end_bit, st),
-             "radix_sort_pairs")))
-      return rc;
-  }
-  if (!cached)
-    hipLaunchKernelGGL(k_node_bounds, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
-                       reinterpret_cast<const uint32_t*>(c->pair_node.p), nnz, N, c->nt_off.p);
-  if ((rc = c->scan_tmp.ensure(std::max(scan_temp_bytes(N), scan_temp_bytes(nnz))))) return rc;
-  // per-pair event counts -> positions
-  if ((rc = c->rn_cnt.ensure(std::max<int64_t>(nnz, 1)))) return rc;
-  if ((rc = c->pair_pos.ensure(nnz + 1))) return rc;
-  if ((rc = c->pair_src.ensure(std::max<int64_t>(nnz, 1)))) return rc;
-  if (nnz > 0)
-    hipLaunchKernelGGL(k_pair_events, dim3(gridn(nnz, 256, 4096)), dim3(256), 0, st, c->nt_rule.p,
-                       nnz, c->offsets.p, c->rn_cnt.p, c->pair_src.p);
-  launch_scan(c->rn_cnt.p, c->pair_pos.p, nnz, c->scan_tmp.p, st);
-  hipLaunchKernelGGL(k_node_offsets, dim3(gridn(N + 1, 256, 1 << 30)), dim3(256), 0, st,
-                     c->nt_off.p, c->pair_pos.p, N, c->node_off.p);
-  int64_t En = 0;
-  if ((rc = cg_hip_check(hipMemcpyAsync(&En, c->pair_pos.p + nnz, 8, hipMemcpyDeviceToHost, st), "En")))
+  (void)hipEventRecord(c->pev[1], st);
+  if (!cached && (rc = transpose_locked(c, nnz, N))) return rc;
+  // segments (node, rule band): bounds cached per band width
+  const int32_t B = band_rules(R, E);
+  const int32_t K = int32_t(std::max<int64_t>(1, (R + B - 1) / B));
+  const int64_t NK = int64_t(N) * K;
+  if ((rc = c->seg_pair.ensure(NK + 1)) || (rc = c->seg_cnt.ensure(std::max<int64_t>(NK, 1))) ||
+      (rc = c->seg_pos.ensure(NK + 1)) || (rc = c->node_off.ensure(N + 1)) ||
+      (rc = c->pn_tickets.ensure(kTicketGroups * kTicketStride)))
     return rc;
-  if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
-  if ((rc = c->node_time.ensure(std::max<int64_t>(En, 1)))) return rc;
-  if ((rc = c->node_rule.ensure(std::max<int64_t>(En, 1)))) return rc;
-  const int64_t ntasks = (En + kNodeTask - 1) / kNodeTask;
-  if ((rc = c->block_run.ensure(ntasks + 1))) return rc;
-  (void)hipEventRecord(c->pev[2], st);
-  if (En > 0) {
-    hipLaunchKernelGGL(k_pair_block_map, dim3(gridn(ntasks + 1, 256, 1 << 30)), dim3(256), 0, st,
-                       c->pair_pos.p, nnz, ntasks, c->block_run.p);
-#ifdef CG_DIAG
-    static const int variant = [] {  // diagnostic: 1 no gather, 2 no stores, 3 neither
-      const char* e = getenv("CG_NODE_VARIANT");
-      return e ? atoi(e) : 0;
-    }();
-    static const int per_cu = [] {  // persistent grid: blocks of 4 waves per CU
-      const char* e = getenv("CG_NODE_BLOCKS_PER_CU");
-      return e ? std::max(1, atoi(e)) : 8;
-    }();
-#else
-    constexpr int variant = 0, per_cu = 8;
-#endif
-    const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-#define CG_NW(V)                                                                              \
-  hipLaunchKernelGGL(k_node_write<V>, dim3(gridn(ntasks, 4, nw_blocks)), dim3(256), 0, st,      \
-                     c->pair_pos.p, c->nt_rule.p, c->block_run.p, c->pair_src.p, c->times.p, En, \
-                     nnz, c->node_time.p, c->node_rule.p)
-    switch (variant) {
-      case 1: CG_NW(1); break;
-      case 2: CG_NW(2); break;
-      case 3: CG_NW(3); break;
-      default: CG_NW(0); break;
-    }
-#undef CG_NW
+  if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(NK))))) return rc;
+  if (!(cached && c->pn_B == B && c->pn_K == K)) {
+    hipLaunchKernelGGL(k_seg_bounds, dim3(gridn(NK + 1, 256, 1 << 30)), dim3(256), 0, st, c->nt_off.p,
+                       c->nt_rule.p, N, K, B, c->seg_pair.p);
+    c->pn_B = B;
+    c->pn_K = K;
   }
-  (void)hipEventRecord(c->pev[3], st);
-  if ((rc = cg_hip_check(hipGetLastError(), "per-node kernels"))) return rc;
-  if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+  if (!c->pn_res_host) {
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pn_res_host), 16,
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pn_res_dev), c->pn_res_host, 0));
+  }
+  if (NK > 0)
+    hipLaunchKernelGGL(k_seg_count, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
+                       c->nt_rule.p, c->offsets.p, N, K, c->seg_cnt.p, c->pn_tickets.p);
+  launch_scan64(c->seg_cnt.p, c->seg_pos.p, NK, c->scan_tmp.p, st);
+  hipLaunchKernelGGL(k_node_off_from_seg, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
+                     c->seg_pos.p, N, K, c->node_off.p, c->pn_res_dev);
+  (void)hipEventRecord(c->pev[2], st);
+  // the writer reads the total on the device and does nothing if it exceeds
+  // the output capacity (first call or a larger result: grow, relaunch)
+#ifdef CG_DIAG
+  static const int variant = [] {  // diagnostic: 1 no gather, 2 no stores, 3 neither
+    const char* e = getenv("CG_NODE_VARIANT");
+    return e ? atoi(e) : 0;
+  }();
+  static const int per_cu = [] {  // persistent grid: blocks of 4 waves per CU
+    const char* e = getenv("CG_NODE_BLOCKS_PER_CU");
+    return e ? std::max(1, atoi(e)) : 8;
+  }();
+#else
+  constexpr int variant = 0, per_cu = 8;
+#endif
+  const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
+  int64_t En = 0;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
+    if (NK > 0 && cap > 0) {
+#define CG_NW(V)                                                                                    \
+  hipLaunchKernelGGL(k_node_write<V>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
+                     0, st, c->seg_pair.p, c->seg_pos.p, c->nt_rule.p, c->offsets.p, c->times.p, N, K, cap, \
+                     c->pn_tickets.p, c->node_time.p, c->node_rule.p)
+      switch (variant) {
+        case 1: CG_NW(1); break;
+        case 2: CG_NW(2); break;
+        case 3: CG_NW(3); break;
+        default: CG_NW(0); break;
+      }
+#undef CG_NW
+    }
+    (void)hipEventRecord(c->pev[3], st);
+    if ((rc = cg_hip_check(hipGetLastError(), "per-node kernels"))) return rc;
+    if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+    En = c->pn_res_host[0];
+    if (En <= cap) break;
+    // grow the output, reset the tickets the first launch consumed, rerun
+    if ((rc = c->node_time.ensure(En)) || (rc = c->node_rule.ensure(En))) return rc;
+    HIPCHK(hipMemsetAsync(c->pn_tickets.p, 0, kTicketGroups * kTicketStride * 4, st));
+    (void)hipEventRecord(c->pev[2], st);
+  }
   (void)hipEventElapsedTime(&c->kt[6], c->pev[0], c->pev[1]);
   (void)hipEventElapsedTime(&c->kt[7], c->pev[1], c->pev[2]);
   (void)hipEventElapsedTime(&c->kt[8], c->pev[2], c->pev[3]);
