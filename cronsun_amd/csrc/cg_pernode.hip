@@ -268,7 +268,8 @@ __global__ __launch_bounds__(256) void k_seg_count(const int64_t* __restrict__ s
                                                     const int64_t* __restrict__ rule_off, int32_t N,
                                                     int32_t K, int64_t* __restrict__ seg_cnt,
                                                     uint32_t* __restrict__ tickets) {
-  if (blockIdx.x == 0 && threadIdx.x < kTicketGroups * kTicketStride) tickets[threadIdx.x] = 0;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < kTicketGroups * kTicketStride; i += blockDim.x) tickets[i] = 0;
   const int lane = threadIdx.x & 63;
   const int64_t NK = int64_t(N) * K;
   const int64_t nw = int64_t(gridDim.x) * (blockDim.x >> 6);
