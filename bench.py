@@ -52,18 +52,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(path, kernel, rules, events):
-    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
-    (profiles/*.json written by tools/pmc_traffic.py), if it was measured on
-    the same workload."""
-    try:
-        with open(path) as f:
-            d = json.load(f)
-        k = d["kernels"][kernel]
-        if d.get("rules") == rules and d.get("events") == events:
-            return float(k["hbm_bytes_per_launch"])
-    except Exception:
-        pass
+def pmc_traffic(name, kernel, rules, events):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
+    PMC summary profiles/r*_<name> (written by tools/pmc_traffic.py) that was
+    measured on the same workload (same rules and events per launch)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_" + name)), reverse=True):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+            k = d["kernels"][kernel]
+            if d.get("rules") == rules and d.get("events") == events:
+                return float(k["hbm_bytes_per_launch"])
+        except Exception:
+            pass
     return None
 
 
@@ -394,8 +396,7 @@ def main():
                     f"{'config-2' if wl == 'config3' else 'light'} spec mix, {hz} horizon in "
                     f"{nw} window(s) of {W}s, UTC, per GPU; exclude mode {args.exclude_mode}"
                     + (" (job.go:591-630)" if xmode == 0 else ""))
-        traffic = pmc_traffic(os.path.join(ROOT, "profiles", "r01_pmc_traffic_pernode.json"),
-                              kname, R, E) if wl == "pernode" else None
+        traffic = pmc_traffic("pmc_traffic_pernode.json", kname, R, E) if wl == "pernode" else None
     else:
         algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
         kname, ksec = "k_write_cf", kt[3] / 1e3
@@ -403,8 +404,7 @@ def main():
         workload = ("config 2: 1M mixed cron rules x 24h horizon, UTC, per GPU (job-ID-range shards)"
                     if wl == "config2" else
                     "config 4: 10M rules x 7d horizon, light spec mix, UTC, job-ID-range shards over N GPUs")
-        traffic = pmc_traffic(os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"), kname, R, E) \
-            if wl == "config2" else None
+        traffic = pmc_traffic("pmc_traffic.json", kname, R, E) if wl == "config2" else None
     achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
 
     cpu = None

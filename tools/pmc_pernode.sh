@@ -6,7 +6,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-pn}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-B="bench.py --workload pernode --steps 3 --warmup 1 --cpu-sample 0"
+B="bench.py --workload pernode --steps 3 --warmup 1 --cpu-sample 0 --verify-sample 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_kt" -- \
   python3 $B > "$OUT/bench_prof.json" 2> "$OUT/prof_kt.err" || { tail -20 "$OUT/prof_kt.err"; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/prof_fetch" -- \

@@ -92,6 +92,9 @@ def main():
             e["write_kb_per_launch"] = sum(wr[k]) / len(wr[k])
         if "fetch_kb_per_launch" in e and "write_kb_per_launch" in e:
             e["hbm_bytes_per_launch"] = 2 * e["fetch_kb_per_launch"] * 1024 + e["write_kb_per_launch"] * 1024
+            # without the x2 read correction (stated for 16-B/lane streaming reads;
+            # gathers of 8-B words are uncalibrated)
+            e["hbm_bytes_raw_per_launch"] = (e["fetch_kb_per_launch"] + e["write_kb_per_launch"]) * 1024
         res["kernels"][k] = e
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
