@@ -278,9 +278,18 @@ __global__ __launch_bounds__(256) void k_seg_count(const int64_t* __restrict__ s
     const int64_t s = int64_t(n) * K + k;
     const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
     int64_t acc = 0;
-    for (int64_t p = p0 + lane; p < p1; p += 64) {
-      const int32_t r = nt_rule[p];
-      acc += rule_off[r + 1] - rule_off[r];
+    for (int64_t p = p0 + lane; p < p1; p += 64 * 4) {  // 4 pairs per lane in flight
+      int32_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) r[u] = p + 64 * u < p1 ? nt_rule[p + 64 * u] : -1;
+      int64_t lo[4], hi[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        lo[u] = r[u] >= 0 ? rule_off[r[u]] : 0;
+        hi[u] = r[u] >= 0 ? rule_off[r[u] + 1] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) acc += hi[u] - lo[u];
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
     if (lane == 0) seg_cnt[s] = acc;
@@ -326,6 +335,11 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 // A block shared with the next window of the same segment is carried in
 // registers; only blocks at segment edges are stored partially.
 // V (diagnostic build only): 1 = no gather (synthetic values), 2 = no stores.
+#ifndef CG_NODE_BATCH
+#define CG_NODE_BATCH 4
+#endif
+constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
+
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
@@ -359,14 +373,27 @@ __global__ __launch_bounds__(256) void k_node_write(
     int64_t pblk = -1, ptime = 0;  // a block carried into the next window
     int32_t prule = 0;
     int64_t ow = o0;  // output start of the current window
-    int32_t nr = 0;
-    if (p0 + lane < p1) nr = nt_rule[p0 + lane];
+    // window pipeline: this window's rules and their fire-list bounds are in
+    // registers; the next window's bounds and the one after's rules are in flight
+    int32_t r_nx = 0, r_nx2 = 0;
+    int64_t a_nx = 0, z_nx = 0;
+    if (p0 + lane < p1) {
+      r_nx = nt_rule[p0 + lane];
+      a_nx = rule_off[r_nx];
+      z_nx = rule_off[r_nx + 1];
+    }
+    if (p0 + 64 + lane < p1) r_nx2 = nt_rule[p0 + 64 + lane];
     for (int64_t pw = p0; pw < p1; pw += 64) {
       const bool valid = pw + lane < p1;
-      const int32_t r = nr;
-      if (pw + 64 + lane < p1) nr = nt_rule[pw + 64 + lane];  // next window's rules, one ahead
-      const int64_t a = valid ? rule_off[r] : 0;
-      const int64_t c = valid ? rule_off[r + 1] - a : 0;
+      const int32_t r = r_nx;
+      const int64_t a = valid ? a_nx : 0;
+      const int64_t c = valid ? z_nx - a_nx : 0;
+      if (pw + 64 + lane < p1) {
+        r_nx = r_nx2;
+        a_nx = rule_off[r_nx];
+        z_nx = rule_off[r_nx + 1];
+      }
+      if (pw + 128 + lane < p1) r_nx2 = nt_rule[pw + 128 + lane];
       int64_t incl = c;
       for (int o = 1; o < 64; o <<= 1) {
         const int64_t y = __shfl_up(incl, o, 64);
@@ -384,52 +411,72 @@ __global__ __launch_bounds__(256) void k_node_write(
       const int32_t rr = __builtin_amdgcn_ds_permute(dstl << 2, r);
       const int64_t we = ow + tot;  // window output end
       int cprev = -1;  // compacted pair holding event b - 1 (-1: before this window)
-      for (int64_t b = ow & ~int64_t(63); b < we; b += 64) {
-        const int64_t e = b + lane;
-        int64_t val = 0;
-        int32_t rv = 0;
-        int cb = cprev;  // the pair holding event b, when b lies in this window
-        if (b >= ow && cprev + 1 < nc && rl64n(dst, cprev + 1) == b) cb = cprev + 1;
-        const int64_t cb_end = cb >= 0 ? (cb + 1 < nc ? rl64n(dst, cb + 1) : we) : 0;
-        if (b >= ow && cb >= 0 && cb_end >= b + 64) {
-          const int64_t dl = rl64n(delta, cb);
-          val = (V & 1) ? e + dl : times[e + dl];
-          rv = __builtin_amdgcn_readlane(rr, cb);
-          cprev = cb;
-        } else {
-          tag++;
-          if (lane < nc && dst >= b && dst < b + 64) marks[dst - b] = tag;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          const uint64_t M = __ballot(marks[lane] == tag);
-          int own = cprev + __popcll(M & le);
-          const bool mine = e >= ow && e < we;
-          own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
-          const int64_t dl = bperm64(delta, own);
-          const int32_t ro = __builtin_amdgcn_ds_bpermute(own << 2, rr);
-          if (mine) {
-            val = (V & 1) ? e + dl : times[e + dl];
-            rv = ro;
+      // blocks in batches: every block's lanes are placed first (LDS and
+      // cross-lane work only), then the batch's gathers are issued together
+      // (kNodeBatch loads in flight per wave instead of one), then stored
+      for (int64_t bb = ow & ~int64_t(63); bb < we; bb += 64 * kNodeBatch) {
+        int64_t src[kNodeBatch];  // fire-list index of this lane's event (-1: none here)
+        int32_t rvs[kNodeBatch];
+#pragma unroll
+        for (int q = 0; q < kNodeBatch; q++) {
+          const int64_t b = bb + 64 * q;
+          src[q] = -1;
+          rvs[q] = 0;
+          if (b >= we) continue;
+          const int64_t e = b + lane;
+          int cb = cprev;  // the pair holding event b, when b lies in this window
+          if (b >= ow && cprev + 1 < nc && rl64n(dst, cprev + 1) == b) cb = cprev + 1;
+          const int64_t cb_end = cb >= 0 ? (cb + 1 < nc ? rl64n(dst, cb + 1) : we) : 0;
+          if (b >= ow && cb >= 0 && cb_end >= b + 64) {  // inside one pair
+            src[q] = e + rl64n(delta, cb);
+            rvs[q] = __builtin_amdgcn_readlane(rr, cb);
+            cprev = cb;
+          } else {
+            tag++;
+            if (lane < nc && dst >= b && dst < b + 64) marks[dst - b] = tag;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint64_t M = __ballot(marks[lane] == tag);
+            int own = cprev + __popcll(M & le);
+            own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
+            const int64_t dl = bperm64(delta, own);
+            const int32_t ro = __builtin_amdgcn_ds_bpermute(own << 2, rr);
+            if (e >= ow && e < we) {
+              src[q] = e + dl;
+              rvs[q] = ro;
+            }
+            cprev = __builtin_amdgcn_readlane(own, 63);
           }
-          cprev = __builtin_amdgcn_readlane(own, 63);
         }
-        if (b == pblk && e < ow) {  // lanes of the previous window
-          val = ptime;
-          rv = prule;
-        }
-        if (b + 64 <= we || we == o1) {  // complete, or the segment's last block
-          if (!(V & 2) && e >= o0 && e < o1) {
-            out_time[e] = val;
-            out_rule[e] = rv;
-          } else if (V & 2) {
-            asm volatile("" ::"v"(val), "v"(rv));
+        int64_t vals[kNodeBatch];
+#pragma unroll
+        for (int q = 0; q < kNodeBatch; q++)
+          vals[q] = src[q] < 0 ? 0 : ((V & 1) ? src[q] : times[src[q]]);
+#pragma unroll
+        for (int q = 0; q < kNodeBatch; q++) {
+          const int64_t b = bb + 64 * q;
+          if (b >= we) break;
+          const int64_t e = b + lane;
+          int64_t val = vals[q];
+          int32_t rv = rvs[q];
+          if (b == pblk && e < ow) {  // lanes of the previous window
+            val = ptime;
+            rv = prule;
           }
-          pblk = -1;
-        } else {
-          pblk = b;
-          ptime = val;
-          prule = rv;
+          if (b + 64 <= we || we == o1) {  // complete, or the segment's last block
+            if (!(V & 2) && e >= o0 && e < o1) {
+              out_time[e] = val;
+              out_rule[e] = rv;
+            } else if (V & 2) {
+              asm volatile("" ::"v"(val), "v"(rv));
+            }
+            pblk = -1;
+          } else {
+            pblk = b;
+            ptime = val;
+            prule = rv;
+          }
         }
       }
       ow = we;
