@@ -281,6 +281,17 @@ def main():
     if not pn and wl != "dispatch":
         _, d_times, _ = eng.result_device()
         log(f"[rank {rank}] times buffer at {d_times:#x} ({d_times % (1 << 21):#x} past a 2 MiB boundary)")
+    # Poison the result buffers (outside the timed region): whatever a timed
+    # step fails to write stays -1 and is counted after the timed loop.
+    def result_buffers():
+        if pn:
+            _, d_time, d_rule, n_ev = eng.node_result_device()
+            return [(d_time, n_ev, 8), (d_rule, n_ev, 4)]
+        _, d_times, n_ev = eng.result_device()
+        return [(d_times, n_ev, 8)]
+    if wl != "dispatch":
+        for ptr, n_ev, w in result_buffers():
+            eng.fill(ptr, n_ev * w, 0xFF)
     barrier()
     torch.cuda.synchronize()
     start = time.perf_counter()
@@ -307,6 +318,9 @@ def main():
     # The timed steps' own output, checked on a seeded sample against the
     # oracle (outside the timed region): a step that skipped work would fail.
     verify = None
+    unwritten = None
+    if wl != "dispatch":  # poisoned words the timed steps left unwritten (must be 0)
+        unwritten = sum(eng.count_value(ptr, n_ev, w, -1) for ptr, n_ev, w in result_buffers())
     if args.verify_sample > 0 and wl != "dispatch":
         tv = time.perf_counter()
         if pn:
@@ -317,6 +331,8 @@ def main():
             verify = verify_rule_major(eng, spec_of, R, t0, t1, E, args.verify_sample,
                                        seed=0x5EED + 99 + rank)
         verify["seconds"] = time.perf_counter() - tv
+        verify["unwritten_after_poison"] = unwritten
+        verify["verified"] = verify["verified"] and unwritten == 0
         ok = torch.tensor([1 if verify["verified"] else 0], dtype=torch.int64, device=cdev)
         if world > 1:
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)

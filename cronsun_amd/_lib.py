@@ -136,6 +136,8 @@ def _declare(L):
         "cg_node_counts_to_device": ([vp, vp], C.c_int),
         "cg_node_result_copy_range": ([vp, i64, i64, vp, vp], C.c_int),
         "cg_checksum_device": ([vp, vp, i64, C.c_int, i64, i64, P(u64)], C.c_int),
+        "cg_fill_device": ([vp, vp, i64, C.c_int], C.c_int),
+        "cg_count_value_device": ([vp, vp, i64, C.c_int, i64, P(i64)], C.c_int),
         "cg_rules_upload": ([vp, P(cg_rules_in), P(vp)], C.c_int),
         "cg_rules_free": ([vp], None),
         "cg_expand_per_node_rules_device": ([vp, vp, vp, i64, i64, vp, C.c_int, P(i64), P(i64)],

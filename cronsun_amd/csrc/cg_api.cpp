@@ -638,6 +638,35 @@ int cg_checksum_device(cg_ctx* c, const void* d_ptr, int64_t n, int elem_bytes, 
   return CG_OK;
 }
 
+int cg_fill_device(cg_ctx* c, void* d_ptr, int64_t bytes, int byte_value) {
+  if (!c || bytes < 0 || (bytes > 0 && !d_ptr)) return cg_fail(CG_EINVAL, "cg_fill_device: bad argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  if (bytes) HIPCHK(hipMemsetAsync(d_ptr, byte_value & 0xFF, size_t(bytes), c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  return CG_OK;
+}
+
+int cg_count_value_device(cg_ctx* c, const void* d_ptr, int64_t n, int elem_bytes, int64_t value,
+                          int64_t* count) {
+  if (!c || !count || (n > 0 && !d_ptr) || n < 0 || (elem_bytes != 8 && elem_bytes != 4))
+    return cg_fail(CG_EINVAL, "cg_count_value_device: bad argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  int rc = c->cksum.ensure(1);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(c->cksum.p, 0, 8, c->st));
+  launch_count_eq(d_ptr, n, elem_bytes, value, c->cksum.p, c->st);
+  HIPCHK(hipGetLastError());
+  unsigned long long v = 0;
+  HIPCHK(hipMemcpyAsync(&v, c->cksum.p, 8, hipMemcpyDeviceToHost, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));
+  *count = int64_t(v);
+  return CG_OK;
+}
+
 int cg_set_phase_timing(cg_ctx* c, int level) {
   if (!c || level < 1 || level > 2) return cg_fail(CG_EINVAL, "cg_set_phase_timing: level 1 or 2");
   std::lock_guard<std::mutex> g(c->mu);

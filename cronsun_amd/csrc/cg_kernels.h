@@ -50,6 +50,10 @@ size_t plan_lds_bytes(const PlanArgs& p);
 void launch_checksum(const void* v, int64_t n, int elem_bytes, int64_t first, int64_t add,
                      unsigned long long* out, hipStream_t st);
 
+// *out += count of elements (int64 or int32) of v equal to x (cg_count_value_device)
+void launch_count_eq(const void* v, int64_t n, int elem_bytes, int64_t x, unsigned long long* out,
+                     hipStream_t st);
+
 void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,
                        int64_t* t_out, hipStream_t st);
 // GPU-resident dispatcher (cg_dispatch.cpp): one block per kDispatchTile entries

@@ -1112,6 +1112,21 @@ __global__ __launch_bounds__(256) void k_checksum(const T* __restrict__ v, int64
   if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
 }
 
+// *out += number of elements of v equal to x (cg_count_value_device)
+template <class T>
+__global__ __launch_bounds__(256) void k_count_eq(const T* __restrict__ v, int64_t n, T x,
+                                                   unsigned long long* __restrict__ out) {
+  uint64_t c = 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n;
+       i += int64_t(gridDim.x) * blockDim.x)
+    c += v[i] == x;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  __shared__ uint64_t s[4];
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
+}
+
 int grid_for(int64_t n, int threads, int max_blocks) {
   int64_t b = (n + threads - 1) / threads;
   if (b < 1) b = 1;
@@ -1136,6 +1151,18 @@ void launch_checksum(const void* v, int64_t n, int elem_bytes, int64_t first, in
   else
     hipLaunchKernelGGL(k_checksum<int32_t>, dim3(grid), dim3(256), 0, st,
                        static_cast<const int32_t*>(v), n, first, add, out);
+}
+
+void launch_count_eq(const void* v, int64_t n, int elem_bytes, int64_t x, unsigned long long* out,
+                     hipStream_t st) {
+  if (n <= 0) return;
+  const int grid = grid_for(n, 256 * 8, 256 * 32);
+  if (elem_bytes == 8)
+    hipLaunchKernelGGL(k_count_eq<int64_t>, dim3(grid), dim3(256), 0, st, static_cast<const int64_t*>(v), n, x,
+                       out);
+  else
+    hipLaunchKernelGGL(k_count_eq<int32_t>, dim3(grid), dim3(256), 0, st, static_cast<const int32_t*>(v), n,
+                       int32_t(x), out);
 }
 
 void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,

@@ -367,6 +367,12 @@ class Engine:
                                                     C.byref(En), C.byref(nnz)))
         return En.value, nnz.value
 
+    def node_result_device(self):
+        """Device pointers of the last per-node result: (node_off, time, rule, n_events)."""
+        o, t, r, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int64()
+        check(lib().cg_node_result_device(self._h, C.byref(o), C.byref(t), C.byref(r), C.byref(n)))
+        return o.value, t.value, r.value, n.value
+
     def node_result(self, n_nodes, n_events):
         """Copy the last per-node result (node_off, time, rule) to host."""
         node_off = np.empty(n_nodes + 1, dtype=np.int64)
@@ -386,6 +392,17 @@ class Engine:
 
     def node_counts_to_device(self, d_ptr):
         check(lib().cg_node_counts_to_device(self._h, C.c_void_p(d_ptr)))
+
+    def fill(self, d_ptr, nbytes, byte_value=0xFF):
+        """Fill a device buffer with one byte value (cg_fill_device)."""
+        check(lib().cg_fill_device(self._h, C.c_void_p(d_ptr), int(nbytes), int(byte_value)))
+
+    def count_value(self, d_ptr, n, elem_bytes=8, value=-1):
+        """Elements of a device array equal to value (cg_count_value_device)."""
+        out = C.c_int64()
+        check(lib().cg_count_value_device(self._h, C.c_void_p(d_ptr), int(n), int(elem_bytes),
+                                          int(value), C.byref(out)))
+        return out.value
 
     def checksum(self, d_ptr, n, elem_bytes=8, first_index=0, add=0):
         """Order-sensitive checksum of a device array (cg_checksum_device);

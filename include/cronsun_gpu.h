@@ -292,6 +292,13 @@ int cg_set_phase_timing(cg_ctx* ctx, int level);
  * its global base) can be compared with its range of another result. */
 int cg_checksum_device(cg_ctx* ctx, const void* d_ptr, int64_t n, int elem_bytes,
                        int64_t first_index, int64_t add, uint64_t* out);
+/* Integrity helpers for benchmarks and tests (no reference counterpart):
+ * fill `bytes` of a device buffer with one byte value (e.g. poison an output
+ * before timed runs), and count the int64/int32 elements equal to `value`
+ * (e.g. poison a later run left unwritten). */
+int cg_fill_device(cg_ctx* ctx, void* d_ptr, int64_t bytes, int byte_value);
+int cg_count_value_device(cg_ctx* ctx, const void* d_ptr, int64_t n, int elem_bytes, int64_t value,
+                          int64_t* count);
 
 /* --------------------------------------------- rule -> node resolution --- */
 /* Integer-interned jobs/groups (host interns string IDs; see cg_jobset_*).
