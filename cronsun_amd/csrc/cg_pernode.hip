@@ -302,7 +302,10 @@ __global__ void k_node_off_from_seg(const int64_t* __restrict__ seg_pos, int32_t
   const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
   if (n > N) return;
   node_off[n] = seg_pos[n * K];
-  if (n == N) res[0] = seg_pos[n * K];
+  if (n == N) {
+    res[0] = seg_pos[n * K];
+    res[1] = 0;  // the writer's error flag
+  }
 }
 
 __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
@@ -344,8 +347,9 @@ template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
     const int32_t* __restrict__ nt_rule, const int64_t* __restrict__ rule_off,
-    const int64_t* __restrict__ times, int32_t N, int32_t K, int64_t cap,
-    uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time, int32_t* __restrict__ out_rule) {
+    const int64_t* __restrict__ times, int32_t N, int32_t K, int32_t B, int64_t R, int64_t cap,
+    uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time, int32_t* __restrict__ out_rule,
+    int64_t* __restrict__ err) {
   __shared__ uint32_t marks_all[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* marks = marks_all[wave];
@@ -366,15 +370,28 @@ __global__ __launch_bounds__(256) void k_node_write(
     const int64_t t_next = take();
     const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
     const int64_t s = int64_t(n) * K + k;
+    t = t_next;
     const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
     const int64_t o0 = seg_pos[s], o1 = seg_pos[s + 1];
-    t = t_next;
     if (o0 == o1) continue;
-    int64_t pblk = -1, ptime = 0;  // a block carried into the next window
-    int32_t prule = 0;
-    int64_t ow = o0;  // output start of the current window
-    // window pipeline: this window's rules and their fire-list bounds are in
-    // registers; the next window's bounds and the one after's rules are in flight
+    // the band's fire lists are one contiguous range of the rule-major times
+    const int64_t band_lo = rule_off[int64_t(k) * B];
+    const int64_t band_hi = rule_off[int64_t(k + 1) * B < R ? int64_t(k + 1) * B : R];
+    if (o1 - o0 > (int64_t(1) << 30) || band_hi - band_lo > (int64_t(1) << 30)) {
+      if (lane == 0) err[0] = 1;  // 32-bit offsets below: the host reports CG_ERANGE
+      continue;
+    }
+    // segment-local 32-bit positions: q = output index - abase (abase 64-aligned)
+    const int64_t abase = o0 & ~int64_t(63);
+    const int32_t q_lo = int32_t(o0 - abase), q_hi = q_lo + int32_t(o1 - o0);
+    const int64_t* __restrict__ tb = times + band_lo;
+    int64_t* __restrict__ ot = out_time + abase;
+    int32_t* __restrict__ orl = out_rule + abase;
+    int32_t pq = -1, prule = 0;  // a block carried into the next window
+    int64_t ptime = 0;
+    int32_t qw = q_lo;  // first q of the current window
+    // window pipeline: this window's rules and fire-list bounds are in
+    // registers; the next window's bounds and the one after's rules in flight
     int32_t r_nx = 0, r_nx2 = 0;
     int64_t a_nx = 0, z_nx = 0;
     if (p0 + lane < p1) {
@@ -386,50 +403,51 @@ __global__ __launch_bounds__(256) void k_node_write(
     for (int64_t pw = p0; pw < p1; pw += 64) {
       const bool valid = pw + lane < p1;
       const int32_t r = r_nx;
-      const int64_t a = valid ? a_nx : 0;
-      const int64_t c = valid ? z_nx - a_nx : 0;
+      const int32_t c = valid ? int32_t(z_nx - a_nx) : 0;
+      const int32_t arel = int32_t(a_nx - band_lo);
       if (pw + 64 + lane < p1) {
         r_nx = r_nx2;
         a_nx = rule_off[r_nx];
         z_nx = rule_off[r_nx + 1];
       }
       if (pw + 128 + lane < p1) r_nx2 = nt_rule[pw + 128 + lane];
-      int64_t incl = c;
+      int32_t incl = c;
       for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(incl, o, 64);
+        const int32_t y = __shfl_up(incl, o, 64);
         if (lane >= o) incl += y;
       }
-      const int64_t tot = rl64n(incl, 63);
+      const int32_t tot = __builtin_amdgcn_readlane(incl, 63);
       if (tot == 0) continue;
       // compact the non-empty pairs into lanes 0..nc-1 (a permutation)
       const uint64_t NE = __ballot(c > 0);
       const int nc = __popcll(NE);
       const int ci = __popcll(NE & lt);
       const int dstl = c > 0 ? ci : nc + (lane - ci);
-      const int64_t dst = perm64(ow + incl - c, dstl);  // output start of compacted pair
-      const int64_t delta = perm64(a - (ow + incl - c), dstl);  // fire-list index - output index
+      const int32_t d0 = qw + incl - c;  // q of the pair's first event
+      const int32_t dst = __builtin_amdgcn_ds_permute(dstl << 2, d0);
+      const int32_t dlt = __builtin_amdgcn_ds_permute(dstl << 2, arel - d0);  // band index - q
       const int32_t rr = __builtin_amdgcn_ds_permute(dstl << 2, r);
-      const int64_t we = ow + tot;  // window output end
-      int cprev = -1;  // compacted pair holding event b - 1 (-1: before this window)
+      const int32_t we = qw + tot;  // window end (q)
+      int cprev = -1;  // compacted pair holding q = b - 1 (-1: before this window)
       // blocks in batches: every block's lanes are placed first (LDS and
-      // cross-lane work only), then the batch's gathers are issued together
-      // (kNodeBatch loads in flight per wave instead of one), then stored
-      for (int64_t bb = ow & ~int64_t(63); bb < we; bb += 64 * kNodeBatch) {
-        int64_t src[kNodeBatch];  // fire-list index of this lane's event (-1: none here)
+      // cross-lane work only), then the batch's gathers are issued together,
+      // then stored
+      for (int32_t bq = qw & ~63; bq < we; bq += 64 * kNodeBatch) {
+        int32_t gi[kNodeBatch];  // band index of this lane's fire (-1: none here)
         int32_t rvs[kNodeBatch];
 #pragma unroll
-        for (int q = 0; q < kNodeBatch; q++) {
-          const int64_t b = bb + 64 * q;
-          src[q] = -1;
-          rvs[q] = 0;
+        for (int u = 0; u < kNodeBatch; u++) {
+          const int32_t b = bq + 64 * u;
+          gi[u] = -1;
+          rvs[u] = 0;
           if (b >= we) continue;
-          const int64_t e = b + lane;
-          int cb = cprev;  // the pair holding event b, when b lies in this window
-          if (b >= ow && cprev + 1 < nc && rl64n(dst, cprev + 1) == b) cb = cprev + 1;
-          const int64_t cb_end = cb >= 0 ? (cb + 1 < nc ? rl64n(dst, cb + 1) : we) : 0;
-          if (b >= ow && cb >= 0 && cb_end >= b + 64) {  // inside one pair
-            src[q] = e + rl64n(delta, cb);
-            rvs[q] = __builtin_amdgcn_readlane(rr, cb);
+          const int32_t q = b + lane;
+          int cb = cprev;  // the pair holding q = b, when b lies in this window
+          if (b >= qw && cprev + 1 < nc && __builtin_amdgcn_readlane(dst, cprev + 1) == b) cb = cprev + 1;
+          const int32_t cb_end = cb >= 0 ? (cb + 1 < nc ? __builtin_amdgcn_readlane(dst, cb + 1) : we) : 0;
+          if (b >= qw && cb >= 0 && cb_end >= b + 64) {  // inside one pair
+            gi[u] = q + __builtin_amdgcn_readlane(dlt, cb);
+            rvs[u] = __builtin_amdgcn_readlane(rr, cb);
             cprev = cb;
           } else {
             tag++;
@@ -440,46 +458,45 @@ __global__ __launch_bounds__(256) void k_node_write(
             const uint64_t M = __ballot(marks[lane] == tag);
             int own = cprev + __popcll(M & le);
             own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
-            const int64_t dl = bperm64(delta, own);
+            const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
             const int32_t ro = __builtin_amdgcn_ds_bpermute(own << 2, rr);
-            if (e >= ow && e < we) {
-              src[q] = e + dl;
-              rvs[q] = ro;
+            if (q >= qw && q < we) {
+              gi[u] = q + dl;
+              rvs[u] = ro;
             }
             cprev = __builtin_amdgcn_readlane(own, 63);
           }
         }
         int64_t vals[kNodeBatch];
 #pragma unroll
-        for (int q = 0; q < kNodeBatch; q++)
-          vals[q] = src[q] < 0 ? 0 : ((V & 1) ? src[q] : times[src[q]]);
+        for (int u = 0; u < kNodeBatch; u++) vals[u] = gi[u] < 0 ? 0 : ((V & 1) ? int64_t(gi[u]) : tb[gi[u]]);
 #pragma unroll
-        for (int q = 0; q < kNodeBatch; q++) {
-          const int64_t b = bb + 64 * q;
+        for (int u = 0; u < kNodeBatch; u++) {
+          const int32_t b = bq + 64 * u;
           if (b >= we) break;
-          const int64_t e = b + lane;
-          int64_t val = vals[q];
-          int32_t rv = rvs[q];
-          if (b == pblk && e < ow) {  // lanes of the previous window
+          const int32_t q = b + lane;
+          int64_t val = vals[u];
+          int32_t rv = rvs[u];
+          if (b == pq && q < qw) {  // lanes of the previous window
             val = ptime;
             rv = prule;
           }
-          if (b + 64 <= we || we == o1) {  // complete, or the segment's last block
-            if (!(V & 2) && e >= o0 && e < o1) {
-              out_time[e] = val;
-              out_rule[e] = rv;
-            } else if (V & 2) {
+          if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
+            if (V & 2) {
               asm volatile("" ::"v"(val), "v"(rv));
+            } else if (q >= q_lo && q < q_hi) {
+              ot[q] = val;
+              orl[q] = rv;
             }
-            pblk = -1;
+            pq = -1;
           } else {
-            pblk = b;
+            pq = b;
             ptime = val;
             prule = rv;
           }
         }
       }
-      ow = we;
+      qw = we;
     }
   }
 }
@@ -718,8 +735,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL(k_node_write<V>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
-                     0, st, c->seg_pair.p, c->seg_pos.p, c->nt_rule.p, c->offsets.p, c->times.p, N, K, cap, \
-                     c->pn_tickets.p, c->node_time.p, c->node_rule.p)
+                     0, st, c->seg_pair.p, c->seg_pos.p, c->nt_rule.p, c->offsets.p, c->times.p, N, K, B, R, \
+                     cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, c->pn_res_dev + 1)
       switch (variant) {
         case 1: CG_NW(1); break;
         case 2: CG_NW(2); break;
@@ -732,6 +749,9 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     if ((rc = cg_hip_check(hipGetLastError(), "per-node kernels"))) return rc;
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
     En = c->pn_res_host[0];
+    if (c->pn_res_host[1] != 0)
+      return cg_fail(CG_ERANGE, "per-node output: a (node, rule band) segment or a band's fire "
+                                "lists exceed 2^30 events (narrow the time window)");
     if (En <= cap) break;
     // grow the output, reset the tickets the first launch consumed, rerun
     if ((rc = c->node_time.ensure(En)) || (rc = c->node_rule.ensure(En))) return rc;
