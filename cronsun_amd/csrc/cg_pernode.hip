@@ -337,11 +337,13 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 //     start mask M, and lane l's pair is prev + popcount(M & lanes <= l).
 // A block shared with the next window of the same segment is carried in
 // registers; only blocks at segment edges are stored partially.
-// V (diagnostic build only): 1 = no gather (synthetic values), 2 = no stores.
+// V (diagnostic build only): 1 = no gather (synthetic values), 2 = no stores,
+// 4 = no per-block placement (stores of zeros), 8 = no rule-index stores.
 #ifndef CG_NODE_BATCH
 #define CG_NODE_BATCH 4
 #endif
 constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
+constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 node-major
 
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
@@ -349,7 +351,7 @@ __global__ __launch_bounds__(256) void k_node_write(
     const int32_t* __restrict__ nt_rule, const int64_t* __restrict__ rule_off,
     const int64_t* __restrict__ times, int32_t N, int32_t K, int32_t B, int64_t R, int64_t cap,
     uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time, int32_t* __restrict__ out_rule,
-    int64_t* __restrict__ err) {
+    int64_t* __restrict__ err, int node_major) {
   __shared__ uint32_t marks_all[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* marks = marks_all[wave];
@@ -368,7 +370,10 @@ __global__ __launch_bounds__(256) void k_node_write(
   };
   for (int64_t t = take(); t < NK;) {
     const int64_t t_next = take();
-    const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
+    // task order: band-major (a band's fire lists shared in L2 by all nodes'
+    // segments) or node-major (a narrow write front: consecutive segments)
+    const int32_t k = node_major ? int32_t(t % K) : int32_t(t / N);
+    const int32_t n = node_major ? int32_t(t / K) : int32_t(t - int64_t(k) * N);
     const int64_t s = int64_t(n) * K + k;
     t = t_next;
     const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
@@ -440,7 +445,7 @@ __global__ __launch_bounds__(256) void k_node_write(
           const int32_t b = bq + 64 * u;
           gi[u] = -1;
           rvs[u] = 0;
-          if (b >= we) continue;
+          if (b >= we || (V & 4)) continue;
           const int32_t q = b + lane;
           int cb = cprev;  // the pair holding q = b, when b lies in this window
           if (b >= qw && cprev + 1 < nc && __builtin_amdgcn_readlane(dst, cprev + 1) == b) cb = cprev + 1;
@@ -486,7 +491,7 @@ __global__ __launch_bounds__(256) void k_node_write(
               asm volatile("" ::"v"(val), "v"(rv));
             } else if (q >= q_lo && q < q_hi) {
               ot[q] = val;
-              orl[q] = rv;
+              if (!(V & 8)) orl[q] = rv;
             }
             pq = -1;
           } else {
@@ -725,8 +730,12 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     const char* e = getenv("CG_NODE_BLOCKS_PER_CU");
     return e ? std::max(1, atoi(e)) : 8;
   }();
+  static const int node_major = [] {  // writer task order (see k_node_write)
+    const char* e = getenv("CG_NODE_ORDER");
+    return e ? atoi(e) : kNodeMajorDefault;
+  }();
 #else
-  constexpr int variant = 0, per_cu = 8;
+  constexpr int variant = 0, per_cu = 8, node_major = kNodeMajorDefault;
 #endif
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
   int64_t En = 0;
@@ -736,11 +745,14 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL(k_node_write<V>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
                      0, st, c->seg_pair.p, c->seg_pos.p, c->nt_rule.p, c->offsets.p, c->times.p, N, K, B, R, \
-                     cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, c->pn_res_dev + 1)
+                     cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, c->pn_res_dev + 1, node_major)
       switch (variant) {
         case 1: CG_NW(1); break;
         case 2: CG_NW(2); break;
         case 3: CG_NW(3); break;
+        case 4: CG_NW(4); break;
+        case 8: CG_NW(8); break;
+        case 12: CG_NW(12); break;
         default: CG_NW(0); break;
       }
 #undef CG_NW

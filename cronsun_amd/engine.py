@@ -159,6 +159,32 @@ class RulesIn:
                 a = np.zeros(1, dtype=self.DTYPES[f])
             setattr(self, f, a)
 
+    def slice_rules(self, lo, hi):
+        """The rules [lo, hi) as their own rule set (job-ID-range shard): the
+        same nodes and groups, the jobs of those rules renumbered from 0.  A
+        job's rules must not be split by the cut."""
+        if lo < 0 or hi > self.n_rules or lo > hi:
+            raise ValueError("rule range out of bounds")
+        if 0 < lo < self.n_rules and self.rule_job[lo - 1] == self.rule_job[lo]:
+            raise ValueError("the cut splits a job's rules")
+        if 0 < hi < self.n_rules and self.rule_job[hi - 1] == self.rule_job[hi]:
+            raise ValueError("the cut splits a job's rules")
+        rj = self.rule_job[lo:hi]
+        j0 = int(rj[0]) if hi > lo else 0
+        j1 = int(rj[-1]) + 1 if hi > lo else 0
+
+        def part(off, vals):
+            o = off[lo:hi + 1] - off[lo]
+            return o, vals[off[lo]:off[hi]]
+        nid_off, nids = part(self.nid_off, self.nids)
+        gid_off, gids = part(self.gid_off, self.gids)
+        ex_off, ex = part(self.ex_off, self.ex)
+        return RulesIn(self.n_nodes, self.n_groups, hi - lo, j1 - j0,
+                       group_off=self.group_off, group_nodes=self.group_nodes,
+                       group_exists=self.group_exists, rule_job=rj - j0, nid_off=nid_off, nids=nids,
+                       gid_off=gid_off, gids=gids, ex_off=ex_off, ex=ex,
+                       job_pause=self.job_pause[j0:j1])
+
     def to_c(self):
         s = _lib.cg_rules_in()
         s.n_nodes, s.n_groups, s.n_rules, s.n_jobs = (

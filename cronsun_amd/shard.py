@@ -17,6 +17,10 @@ with no data-path collective.  The only exchanges are small:
   gather_csr       the optional second collective: every rank's slice of the
                    rule-major CSR to rank 0 with grouped point-to-point
                    send/recv (variable sizes; xGMI: one link per peer)
+  gather_node_csr  the same for the per-node CSR (north_star's "gather the
+                   final per-node CSR"): every node's global list is the
+                   ranks' slices of it in job-ID order, as one process walking
+                   all jobs builds it (node/node.go:121-158 -> Job.Cmds)
 
 Works with torch.distributed over RCCL ("nccl", one process per MI355X) and
 over gloo on CPU (tests).
@@ -156,3 +160,64 @@ def gather_csr(local_offsets, local_times, dist, dst=0):
             times[int(ebase[g]):int(ebase[g + 1])] = local_times
         offsets[lo:lo + int(alls[g, 0]) + 1] = part + int(ebase[g])
     return offsets, times
+
+
+def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst=0):
+    """Gather the per-node (time, rule) CSR of job-ID-range shards on rank `dst`.
+
+    local_node_off: int64 tensor [N+1] (this rank's node offsets, from 0);
+    local_time int64 [E_g] and local_rule int32 [E_g] (rule indices local to
+    the rank's range, which starts at global rule `rule_base`), all on the
+    collective's device.  Returns (node_off [N+1], time [E], rule [E], global
+    rule indices) on `dst`, None elsewhere.
+
+    Sizes: one all-gather of the per-node counts (N int64 per rank, the
+    collective node_offsets uses).  Payload: one isend of each array per rank
+    into a staging buffer on `dst` (one xGMI link per peer, all in flight
+    together), then each rank's slice of node n is placed at
+    node_base[n] + sum_{g' < g} count[g'][n] by one index scatter per rank."""
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = local_time.device
+    N = local_node_off.numel() - 1
+    counts = (local_node_off[1:] - local_node_off[:-1]).to(torch.int64).contiguous()
+    allc = torch.zeros(world * N, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(allc, counts)
+    allc = allc.view(world, N)
+    sizes = allc.sum(dim=1).cpu().numpy()
+    grule = (local_rule.to(torch.int64) + int(rule_base)).to(torch.int32).contiguous()
+    if rank != dst:
+        ops = [dist.P2POp(dist.isend, local_time.contiguous(), dst), dist.P2POp(dist.isend, grule, dst)]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        return None
+    per_node = allc.sum(dim=0)
+    node_base = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+    node_base[1:] = torch.cumsum(per_node, dim=0)
+    E = int(node_base[-1].item())
+    out_time = torch.empty(E, dtype=torch.int64, device=dev)
+    out_rule = torch.empty(E, dtype=torch.int32, device=dev)
+    stage, ops = {}, []
+    for g in range(world):
+        if g == dst:
+            stage[g] = (local_time, grule)
+            continue
+        stage[g] = (torch.empty(int(sizes[g]), dtype=torch.int64, device=dev),
+                    torch.empty(int(sizes[g]), dtype=torch.int32, device=dev))
+        ops += [dist.P2POp(dist.irecv, stage[g][0], g), dist.P2POp(dist.irecv, stage[g][1], g)]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    before = torch.zeros(N, dtype=torch.int64, device=dev)
+    for g in range(world):
+        c = allc[g]
+        if int(sizes[g]) > 0:
+            src_start = torch.cumsum(c, dim=0) - c
+            delta = node_base[:-1] + before - src_start  # destination - source, per node
+            dest = torch.arange(int(sizes[g]), dtype=torch.int64, device=dev) + \
+                torch.repeat_interleave(delta, c)
+            out_time[dest] = stage[g][0]
+            out_rule[dest] = stage[g][1]
+        before += c
+        stage[g] = None
+    return node_base, out_time, out_rule

@@ -139,3 +139,64 @@ def test_event_balanced_ranges_gloo(tmp_path):
     assert max(ev) - min(ev) <= 2 * 16 * 28800, ev
     assert min(ev) > 0.5 * max(ev), ev
     assert int(rs[0]["w"].sum()) == int(off[-1])
+
+
+def _node_csr_oracle(rin, mode, specs, t0, t1):
+    """Per-node (time, rule) CSR of a rule set from the oracle: every node's
+    own filter over all rules (node.go:121-158 -> Job.Cmds) composed with the
+    Next loop; rules ascending within a node."""
+    arr = O.sched_array([O.parse(s)[0] for s in specs])
+    eo, et = O.expand_batch(arr, t0, t1, O.Loc("UTC"), threads=2)
+    roff, rules = O.node_rules(rin, mode, np.arange(rin.n_nodes), threads=2)
+    node_off = [0]
+    ts, rs = [], []
+    for n in range(rin.n_nodes):
+        t, r = O.node_list(eo, et, rules[roff[n]:roff[n + 1]])
+        ts.append(t)
+        rs.append(r)
+        node_off.append(node_off[-1] + len(t))
+    return (np.array(node_off, dtype=np.int64), np.concatenate(ts).astype(np.int64),
+            np.concatenate(rs).astype(np.int32))
+
+
+def _gather_worker(rank, world, port, outdir, mode):
+    import torch
+    import torch.distributed as dist
+    from cronsun_amd import synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rin = synth.multi_rule_jobs(160, seed=5)
+    specs = synth.spec_mix(rin.n_rules, seed=6, mix=synth.MIX_LIGHT)
+    # job-ID-range shards: cut at the job boundaries nearest to equal rule counts
+    starts = np.concatenate([[0], np.nonzero(np.diff(rin.rule_job))[0] + 1, [rin.n_rules]])
+    cuts = [int(starts[np.argmin(np.abs(starts - rin.n_rules * g // world))]) for g in range(world)]
+    cuts.append(rin.n_rules)
+    lo, hi = cuts[rank], cuts[rank + 1]
+    part = rin.slice_rules(lo, hi)
+    off, t, r = _node_csr_oracle(part, mode, specs[lo:hi], T0, T0 + DAY)
+    g = shard.gather_node_csr(torch.from_numpy(off), torch.from_numpy(t), torch.from_numpy(r), lo, dist)
+    if g is not None:
+        np.savez(os.path.join(outdir, f"g{rank}.npz"), node_off=g[0].numpy(), time=g[1].numpy(),
+                 rule=g[2].numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_gather_node_csr_gloo(tmp_path, mode):
+    """north_star's per-node CSR gather: job-ID-range shards, each with its
+    own per-node lists, gathered on rank 0 into exactly the per-node CSR of the
+    unsharded rule set (world_size 3, exclude modes none and cumulative)."""
+    import torch.multiprocessing as mp
+    from cronsun_amd import synth
+    world = 3
+    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
+    got = np.load(tmp_path / "g0.npz")
+    assert not (tmp_path / "g1.npz").exists()
+    rin = synth.multi_rule_jobs(160, seed=5)
+    specs = synth.spec_mix(rin.n_rules, seed=6, mix=synth.MIX_LIGHT)
+    exp = _node_csr_oracle(rin, mode, specs, T0, T0 + DAY)
+    assert np.array_equal(got["node_off"], exp[0])
+    assert np.array_equal(got["time"], exp[1])
+    assert np.array_equal(got["rule"], exp[2])
