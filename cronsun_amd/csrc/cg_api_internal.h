@@ -107,6 +107,7 @@ struct cg_ctx {
   // transpose, the (node, rule band) segments and the node CSR
   DBuf<int64_t> rn_off, node_off, node_time, nt_off, rs_off, seg_pair, seg_cnt, seg_pos;
   DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule, rs_hist;
+  DBuf<int32_t> seg_nrec, rec_rule, rec_dst, rec_dlt;  // per-call segment records
   DBuf<uint32_t> pn_tickets;
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
@@ -132,6 +133,7 @@ struct cg_ctx {
     seg_pair.release(); seg_cnt.release(); seg_pos.release(); rn_cnt.release(); rn_nodes.release();
     pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();
     rs_hist.release(); pn_tickets.release(); rules.release();
+    seg_nrec.release(); rec_rule.release(); rec_dst.release(); rec_dlt.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);
     pn_res_host = nullptr;
     pn_res_dev = nullptr;

@@ -16,7 +16,7 @@
 //   k_node_bounds        per-node pair offsets (lower bound per node)
 //   (cached per rule set and exclude mode up to here)
 //   k_seg_bounds         (node, rule band) segment bounds (cached per band width)
-//   k_seg_count -> scan  events per segment -> segment and node offsets
+//   k_seg_records -> scan  per segment: events, compact pair records -> offsets
 //   k_node_write         per segment, in band-major order: each node's copy of
 //                        its rules' fire times (whole 64-event blocks; pairs
 //                        placed by a wave prefix sum, blocks spanning pairs
@@ -260,39 +260,71 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
   seg_pair[t] = lo;
 }
 
-// Events per segment: sum over its pairs of the rule's fire count (rule-major
-// offsets of the expansion).  One wave per segment, band-major order so the
-// band's offsets stay in L2.  Block 0 also resets the writer's tickets.
-__global__ __launch_bounds__(256) void k_seg_count(const int64_t* __restrict__ seg_pair,
-                                                    const int32_t* __restrict__ nt_rule,
-                                                    const int64_t* __restrict__ rule_off, int32_t N,
-                                                    int32_t K, int64_t* __restrict__ seg_cnt,
-                                                    uint32_t* __restrict__ tickets) {
+// Segment records, one wave per segment in band-major order (a band's
+// offsets stay in L2): the segment's event count, and for each of its
+// non-empty pairs (in order, compacted to the front of the segment's pair
+// range) a record {rule, first event relative to the segment, band-relative
+// fire-list index minus that position}.  The writer then reads plain records
+// instead of chasing pair -> rule -> offsets per window.  Block 0 also resets
+// the writer's tickets; err[0] is set if a segment or a band outgrows the
+// writer's 32-bit positions.
+__global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__ seg_pair,
+                                                      const int32_t* __restrict__ nt_rule,
+                                                      const int64_t* __restrict__ rule_off, int32_t N,
+                                                      int32_t K, int32_t B, int64_t R,
+                                                      int64_t* __restrict__ seg_cnt,
+                                                      int32_t* __restrict__ seg_nrec,
+                                                      int32_t* __restrict__ rec_rule,
+                                                      int32_t* __restrict__ rec_dst,
+                                                      int32_t* __restrict__ rec_dlt,
+                                                      uint32_t* __restrict__ tickets,
+                                                      int64_t* __restrict__ err) {
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < kTicketGroups * kTicketStride; i += blockDim.x) tickets[i] = 0;
   const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
   const int64_t NK = int64_t(N) * K;
   const int64_t nw = int64_t(gridDim.x) * (blockDim.x >> 6);
   for (int64_t t = blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6); t < NK; t += nw) {
     const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
     const int64_t s = int64_t(n) * K + k;
     const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
-    int64_t acc = 0;
-    for (int64_t p = p0 + lane; p < p1; p += 64 * 4) {  // 4 pairs per lane in flight
-      int32_t r[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) r[u] = p + 64 * u < p1 ? nt_rule[p + 64 * u] : -1;
-      int64_t lo[4], hi[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        lo[u] = r[u] >= 0 ? rule_off[r[u]] : 0;
-        hi[u] = r[u] >= 0 ? rule_off[r[u] + 1] : 0;
+    const int64_t band_lo = rule_off[int64_t(k) * B];
+    const int64_t band_hi = rule_off[int64_t(k + 1) * B < R ? int64_t(k + 1) * B : R];
+    int64_t run = 0;  // events of the segment so far
+    int32_t nrec = 0;
+    for (int64_t pc = p0; pc < p1; pc += 64) {
+      const int64_t p = pc + lane;
+      int32_t r = 0;
+      int64_t a = 0, c = 0;
+      if (p < p1) {
+        r = nt_rule[p];
+        a = rule_off[r];
+        c = rule_off[r + 1] - a;
       }
-#pragma unroll
-      for (int u = 0; u < 4; u++) acc += hi[u] - lo[u];
+      int64_t incl = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+      }
+      const uint64_t NE = __ballot(c > 0);
+      if (c > 0) {
+        const int64_t d = run + incl - c;
+        const int64_t at = p0 + nrec + __popcll(NE & lt);
+        rec_rule[at] = r;
+        rec_dst[at] = int32_t(d);
+        rec_dlt[at] = int32_t((a - band_lo) - d);
+      }
+      const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(incl)), 63));
+      const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(incl) >> 32)), 63));
+      run += int64_t((uint64_t(hi) << 32) | lo);
+      nrec += __popcll(NE);
     }
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-    if (lane == 0) seg_cnt[s] = acc;
+    if (lane == 0) {
+      seg_cnt[s] = run;
+      seg_nrec[s] = nrec;
+      if (run > (int64_t(1) << 30) || band_hi - band_lo > (int64_t(1) << 30)) err[0] = 1;
+    }
   }
 }
 
@@ -302,10 +334,7 @@ __global__ void k_node_off_from_seg(const int64_t* __restrict__ seg_pos, int32_t
   const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
   if (n > N) return;
   node_off[n] = seg_pos[n * K];
-  if (n == N) {
-    res[0] = seg_pos[n * K];
-    res[1] = 0;  // the writer's error flag
-  }
+  if (n == N) res[0] = seg_pos[n * K];
 }
 
 __device__ __forceinline__ int64_t rl64n(int64_t v, int i) {
@@ -348,10 +377,11 @@ constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
-    const int32_t* __restrict__ nt_rule, const int64_t* __restrict__ rule_off,
-    const int64_t* __restrict__ times, int32_t N, int32_t K, int32_t B, int64_t R, int64_t cap,
-    uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time, int32_t* __restrict__ out_rule,
-    int64_t* __restrict__ err, int node_major) {
+    const int32_t* __restrict__ seg_nrec, const int32_t* __restrict__ rec_rule,
+    const int32_t* __restrict__ rec_dst, const int32_t* __restrict__ rec_dlt,
+    const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times, int32_t N, int32_t K,
+    int32_t B, int64_t cap, uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time,
+    int32_t* __restrict__ out_rule, int node_major) {
   __shared__ uint32_t marks_all[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* marks = marks_all[wave];
@@ -360,7 +390,6 @@ __global__ __launch_bounds__(256) void k_node_write(
   const int64_t NK = int64_t(N) * K;
   if (seg_pos[NK] > cap) return;  // output too small: the host grows it and relaunches
   const uint64_t le = (2ull << lane) - 1ull;  // lanes <= this one
-  const uint64_t lt = (1ull << lane) - 1ull;
   const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
   const int grp = int(blockIdx.x % unsigned(ng));
   auto take = [&]() -> int64_t {
@@ -368,72 +397,58 @@ __global__ __launch_bounds__(256) void k_node_write(
     if (lane == 0) t = atomicAdd(tickets + grp * kTicketStride, 1u);
     return grp + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
   };
-  for (int64_t t = take(); t < NK;) {
-    const int64_t t_next = take();
-    // task order: band-major (a band's fire lists shared in L2 by all nodes'
-    // segments) or node-major (a narrow write front: consecutive segments)
+  // a task's descriptor, loaded one task ahead by lanes 0..4 (vector loads:
+  // they neither wait on nor hold up the LDS counter)
+  auto desc = [&](int64_t t) -> int64_t {
+    if (t >= NK) return 0;
     const int32_t k = node_major ? int32_t(t % K) : int32_t(t / N);
     const int32_t n = node_major ? int32_t(t / K) : int32_t(t - int64_t(k) * N);
     const int64_t s = int64_t(n) * K + k;
-    t = t_next;
-    const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
-    const int64_t o0 = seg_pos[s], o1 = seg_pos[s + 1];
-    if (o0 == o1) continue;
-    // the band's fire lists are one contiguous range of the rule-major times
-    const int64_t band_lo = rule_off[int64_t(k) * B];
-    const int64_t band_hi = rule_off[int64_t(k + 1) * B < R ? int64_t(k + 1) * B : R];
-    if (o1 - o0 > (int64_t(1) << 30) || band_hi - band_lo > (int64_t(1) << 30)) {
-      if (lane == 0) err[0] = 1;  // 32-bit offsets below: the host reports CG_ERANGE
-      continue;
+    switch (lane) {
+      case 0: return seg_pair[s];
+      case 1: return seg_nrec[s];
+      case 2: return seg_pos[s];
+      case 3: return seg_pos[s + 1];
+      case 4: return rule_off[int64_t(k) * B];
+      default: return 0;
     }
+  };
+  int64_t t = take();
+  int64_t dsc = desc(t);
+  while (t < NK) {
+    const int64_t t_next = take();
+    const int64_t dsc_next = desc(t_next);
+    const int64_t p0 = rl64n(dsc, 0), o0 = rl64n(dsc, 2), o1 = rl64n(dsc, 3), band_lo = rl64n(dsc, 4);
+    const int32_t nrec = int32_t(rl64n(dsc, 1));
+    t = t_next;
+    dsc = dsc_next;
+    if (o0 == o1) continue;
     // segment-local 32-bit positions: q = output index - abase (abase 64-aligned)
     const int64_t abase = o0 & ~int64_t(63);
     const int32_t q_lo = int32_t(o0 - abase), q_hi = q_lo + int32_t(o1 - o0);
     const int64_t* __restrict__ tb = times + band_lo;
     int64_t* __restrict__ ot = out_time + abase;
     int32_t* __restrict__ orl = out_rule + abase;
-    int32_t pq = -1, prule = 0;  // a block carried into the next window
+    int32_t pq = -1, prule = 0;  // a block carried into the next chunk
     int64_t ptime = 0;
-    int32_t qw = q_lo;  // first q of the current window
-    // window pipeline: this window's rules and fire-list bounds are in
-    // registers; the next window's bounds and the one after's rules in flight
-    int32_t r_nx = 0, r_nx2 = 0;
-    int64_t a_nx = 0, z_nx = 0;
-    if (p0 + lane < p1) {
-      r_nx = nt_rule[p0 + lane];
-      a_nx = rule_off[r_nx];
-      z_nx = rule_off[r_nx + 1];
-    }
-    if (p0 + 64 + lane < p1) r_nx2 = nt_rule[p0 + 64 + lane];
-    for (int64_t pw = p0; pw < p1; pw += 64) {
-      const bool valid = pw + lane < p1;
-      const int32_t r = r_nx;
-      const int32_t c = valid ? int32_t(z_nx - a_nx) : 0;
-      const int32_t arel = int32_t(a_nx - band_lo);
-      if (pw + 64 + lane < p1) {
-        r_nx = r_nx2;
-        a_nx = rule_off[r_nx];
-        z_nx = rule_off[r_nx + 1];
+    // records in chunks of 64 (lane i: record i), the next chunk in flight
+    int32_t nx_r = 0, nx_d = 0, nx_l = 0, nx_end = q_hi;
+    auto fetch = [&](int32_t w) {
+      if (w + lane < nrec) {
+        nx_r = rec_rule[p0 + w + lane];
+        nx_d = rec_dst[p0 + w + lane] + q_lo;
+        nx_l = rec_dlt[p0 + w + lane] - q_lo;
       }
-      if (pw + 128 + lane < p1) r_nx2 = nt_rule[pw + 128 + lane];
-      int32_t incl = c;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-      }
-      const int32_t tot = __builtin_amdgcn_readlane(incl, 63);
-      if (tot == 0) continue;
-      // compact the non-empty pairs into lanes 0..nc-1 (a permutation)
-      const uint64_t NE = __ballot(c > 0);
-      const int nc = __popcll(NE);
-      const int ci = __popcll(NE & lt);
-      const int dstl = c > 0 ? ci : nc + (lane - ci);
-      const int32_t d0 = qw + incl - c;  // q of the pair's first event
-      const int32_t dst = __builtin_amdgcn_ds_permute(dstl << 2, d0);
-      const int32_t dlt = __builtin_amdgcn_ds_permute(dstl << 2, arel - d0);  // band index - q
-      const int32_t rr = __builtin_amdgcn_ds_permute(dstl << 2, r);
-      const int32_t we = qw + tot;  // window end (q)
-      int cprev = -1;  // compacted pair holding q = b - 1 (-1: before this window)
+      // the chunk ends where the next one's first record starts
+      nx_end = w + 64 < nrec ? rec_dst[p0 + w + 64] + q_lo : q_hi;
+    };
+    fetch(0);
+    for (int32_t w = 0; w < nrec; w += 64) {
+      const int32_t rr = nx_r, dst = nx_d, dlt = nx_l, we = nx_end;  // q of first event, band index - q
+      const int nc = nrec - w < 64 ? nrec - w : 64;
+      const int32_t qw = __builtin_amdgcn_readlane(dst, 0);
+      if (w + 64 < nrec) fetch(w + 64);
+      int cprev = -1;  // record holding q = b - 1 (-1: before this chunk)
       // blocks in batches: every block's lanes are placed first (LDS and
       // cross-lane work only), then the batch's gathers are issued together,
       // then stored
@@ -447,7 +462,7 @@ __global__ __launch_bounds__(256) void k_node_write(
           rvs[u] = 0;
           if (b >= we || (V & 4)) continue;
           const int32_t q = b + lane;
-          int cb = cprev;  // the pair holding q = b, when b lies in this window
+          int cb = cprev;  // the record holding q = b, when b lies in this chunk
           if (b >= qw && cprev + 1 < nc && __builtin_amdgcn_readlane(dst, cprev + 1) == b) cb = cprev + 1;
           const int32_t cb_end = cb >= 0 ? (cb + 1 < nc ? __builtin_amdgcn_readlane(dst, cb + 1) : we) : 0;
           if (b >= qw && cb >= 0 && cb_end >= b + 64) {  // inside one pair
@@ -482,7 +497,7 @@ __global__ __launch_bounds__(256) void k_node_write(
           const int32_t q = b + lane;
           int64_t val = vals[u];
           int32_t rv = rvs[u];
-          if (b == pq && q < qw) {  // lanes of the previous window
+          if (b == pq && q < qw) {  // lanes of the previous chunk
             val = ptime;
             rv = prule;
           }
@@ -501,7 +516,6 @@ __global__ __launch_bounds__(256) void k_node_write(
           }
         }
       }
-      qw = we;
     }
   }
 }
@@ -712,9 +726,15 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
                          hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pn_res_dev), c->pn_res_host, 0));
   }
+  if ((rc = c->seg_nrec.ensure(std::max<int64_t>(NK, 1))) ||
+      (rc = c->rec_rule.ensure(std::max<int64_t>(nnz, 1))) || (rc = c->rec_dst.ensure(std::max<int64_t>(nnz, 1))) ||
+      (rc = c->rec_dlt.ensure(std::max<int64_t>(nnz, 1))))
+    return rc;
+  c->pn_res_host[1] = 0;  // error flag (nothing of this ctx is in flight here)
   if (NK > 0)
-    hipLaunchKernelGGL(k_seg_count, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
-                       c->nt_rule.p, c->offsets.p, N, K, c->seg_cnt.p, c->pn_tickets.p);
+    hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
+                       c->nt_rule.p, c->offsets.p, N, K, B, R, c->seg_cnt.p, c->seg_nrec.p, c->rec_rule.p,
+                       c->rec_dst.p, c->rec_dlt.p, c->pn_tickets.p, c->pn_res_dev + 1);
   launch_scan64(c->seg_cnt.p, c->seg_pos.p, NK, c->scan_tmp.p, st);
   hipLaunchKernelGGL(k_node_off_from_seg, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
                      c->seg_pos.p, N, K, c->node_off.p, c->pn_res_dev);
@@ -744,8 +764,9 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL(k_node_write<V>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
-                     0, st, c->seg_pair.p, c->seg_pos.p, c->nt_rule.p, c->offsets.p, c->times.p, N, K, B, R, \
-                     cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, c->pn_res_dev + 1, node_major)
+                     0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->rec_rule.p, c->rec_dst.p,          \
+                     c->rec_dlt.p, c->offsets.p, c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p,     \
+                     c->node_rule.p, node_major)
       switch (variant) {
         case 1: CG_NW(1); break;
         case 2: CG_NW(2); break;

@@ -1,5 +1,7 @@
 """Does torch-ROCm accept __cuda_array_interface__ (zero-copy views of the
 engine's device buffers)?"""
+import os, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 from cronsun_amd import cron
 from cronsun_amd.engine import Engine
