@@ -373,6 +373,9 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 #endif
 constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
 constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 node-major
+#ifndef CG_NODE_FAST
+#define CG_NODE_FAST 1  // blocks inside one pair skip the mark/ballot placement
+#endif
 
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
@@ -382,7 +385,7 @@ __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times, int32_t N, int32_t K,
     int32_t B, int64_t cap, uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time,
     int32_t* __restrict__ out_rule, int node_major) {
-  __shared__ uint32_t marks_all[4][64];
+  __shared__ uint32_t marks_all[4][128];  // slots 64..127: the writes of lanes that mark nothing
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* marks = marks_all[wave];
   marks[lane] = 0u;
@@ -450,8 +453,8 @@ __global__ __launch_bounds__(256) void k_node_write(
       if (w + 64 < nrec) fetch(w + 64);
       int cprev = -1;  // record holding q = b - 1 (-1: before this chunk)
       // blocks in batches: every block's lanes are placed first (LDS and
-      // cross-lane work only), then the batch's gathers are issued together,
-      // then stored
+      // cross-lane work, no divergent branches), then the batch's gathers are
+      // issued together, then stored
       for (int32_t bq = qw & ~63; bq < we; bq += 64 * kNodeBatch) {
         int32_t gi[kNodeBatch];  // band index of this lane's fire (-1: none here)
         int32_t rvs[kNodeBatch];
@@ -462,6 +465,7 @@ __global__ __launch_bounds__(256) void k_node_write(
           rvs[u] = 0;
           if (b >= we || (V & 4)) continue;
           const int32_t q = b + lane;
+#if CG_NODE_FAST
           int cb = cprev;  // the record holding q = b, when b lies in this chunk
           if (b >= qw && cprev + 1 < nc && __builtin_amdgcn_readlane(dst, cprev + 1) == b) cb = cprev + 1;
           const int32_t cb_end = cb >= 0 ? (cb + 1 < nc ? __builtin_amdgcn_readlane(dst, cb + 1) : we) : 0;
@@ -469,27 +473,32 @@ __global__ __launch_bounds__(256) void k_node_write(
             gi[u] = q + __builtin_amdgcn_readlane(dlt, cb);
             rvs[u] = __builtin_amdgcn_readlane(rr, cb);
             cprev = cb;
-          } else {
-            tag++;
-            if (lane < nc && dst >= b && dst < b + 64) marks[dst - b] = tag;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            const uint64_t M = __ballot(marks[lane] == tag);
-            int own = cprev + __popcll(M & le);
-            own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
-            const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
-            const int32_t ro = __builtin_amdgcn_ds_bpermute(own << 2, rr);
-            if (q >= qw && q < we) {
-              gi[u] = q + dl;
-              rvs[u] = ro;
-            }
-            cprev = __builtin_amdgcn_readlane(own, 63);
+            continue;
           }
+#endif
+          // the records starting in this block mark their first lane (the
+          // others write a slot of their own past 64); lane l's record = prev +
+          // marks at <= l
+          tag++;
+          const bool mark = lane < nc && dst >= b && dst < b + 64;
+          marks[mark ? dst - b : 64 + lane] = tag;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const uint64_t M = __ballot(marks[lane] == tag);
+          int own = cprev + __popcll(M & le);
+          own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
+          const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
+          rvs[u] = __builtin_amdgcn_ds_bpermute(own << 2, rr);
+          gi[u] = (q >= qw && q < we) ? q + dl : -1;
+          cprev = __builtin_amdgcn_readlane(own, 63);
         }
         int64_t vals[kNodeBatch];
 #pragma unroll
-        for (int u = 0; u < kNodeBatch; u++) vals[u] = gi[u] < 0 ? 0 : ((V & 1) ? int64_t(gi[u]) : tb[gi[u]]);
+        for (int u = 0; u < kNodeBatch; u++) {
+          const int64_t v = (V & 1) ? int64_t(gi[u]) : tb[gi[u] < 0 ? 0 : gi[u]];
+          vals[u] = gi[u] < 0 ? 0 : v;
+        }
 #pragma unroll
         for (int u = 0; u < kNodeBatch; u++) {
           const int32_t b = bq + 64 * u;
@@ -497,14 +506,17 @@ __global__ __launch_bounds__(256) void k_node_write(
           const int32_t q = b + lane;
           int64_t val = vals[u];
           int32_t rv = rvs[u];
-          if (b == pq && q < qw) {  // lanes of the previous chunk
-            val = ptime;
-            rv = prule;
+          if (b == pq) {  // lanes of the previous chunk
+            val = q < qw ? ptime : val;
+            rv = q < qw ? prule : rv;
           }
           if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
             if (V & 2) {
               asm volatile("" ::"v"(val), "v"(rv));
-            } else if (q >= q_lo && q < q_hi) {
+            } else if (b >= q_lo && b + 64 <= q_hi) {  // interior block: whole stores
+              ot[q] = val;
+              if (!(V & 8)) orl[q] = rv;
+            } else if (q >= q_lo && q < q_hi) {  // a segment edge
               ot[q] = val;
               if (!(V & 8)) orl[q] = rv;
             }
