@@ -374,7 +374,7 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
 constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 node-major
 #ifndef CG_NODE_FAST
-#define CG_NODE_FAST 1  // blocks inside one pair skip the mark/ballot placement
+#define CG_NODE_FAST 0  // 1: blocks inside one pair skip the mark/ballot placement (A/B: ~2% slower)
 #endif
 
 template <int V>
