@@ -86,6 +86,9 @@ def main():
     ap.add_argument("--verify-sample", type=int, default=2000,
                     help="rules (rule-major) or nodes/250 (per-node) of the timed result checked "
                          "against the oracle after the timed region (0 = skip)")
+    ap.add_argument("--gather-node-csr", action="store_true",
+                    help="pernode/config3 at N > 1: every step also gathers the whole per-node CSR on "
+                         "rank 0 (shard.gather_node_csr; timed)")
     ap.add_argument("--diagnostic", action="store_true",
                     help="allow the diagnostic library / CG_WRITE_* CG_NODE_* switches (the line is "
                          "then marked diagnostic and is not a headline)")
@@ -135,15 +138,15 @@ def main():
         mix = synth.MIX_CONFIG2
         seed = 0x5EED + 5 + rank
     elif wl == "pernode":
-        R = args.rules or 1_000_000
+        R = args.rules or 1_000_000  # per GPU: the global set has R * world jobs
         H = args.horizon or 3600
         mix = synth.MIX_LIGHT
-        seed = 0x5EED + 3 + rank
+        seed = 0x5EED + 3
     elif wl == "config3":
         R = args.rules or 1_000_000
         H = args.horizon or 86400
         mix = synth.MIX_CONFIG2
-        seed = 0x5EED + 3 + rank
+        seed = 0x5EED + 3
     else:  # config4: 10M rules in total, job-ID-range shards balanced by events
         total = args.rules or 10_000_000
         R = total
@@ -189,7 +192,7 @@ def main():
 
         def spec_of(i):  # local rule i of this rank's range
             return base_specs[(shard_lo + i) % base_n]
-    elif wl == "config2":
+    elif wl in ("config2", "pernode", "config3"):
         # one global rule set of R * world rules in job-ID order, built from
         # R-rule blocks (block b: seed 0x5EED + b, so the N = 1 set is block 0);
         # rank g expands its job-ID range [g R, (g + 1) R)
@@ -220,7 +223,11 @@ def main():
     drules = None
     n_nodes = 10_000
     if pn:
-        rin = synth.rules_for_nodes(R, n_nodes=n_nodes, n_groups=500, seed=0x5EED + 3 + 1000 * rank)
+        # the global jobs x groups x nodes set (one rule per job), this rank's
+        # job-ID range of it (the same 500 groups and 10k nodes everywhere)
+        rin = synth.rules_for_nodes(R * world, n_nodes=n_nodes, n_groups=500, seed=0x5EED + 3)
+        if world > 1:
+            rin = rin.slice_rules(shard_info["lo"], shard_info["hi"])
         drules = eng.upload_rules(rin)
 
     def barrier():
@@ -256,7 +263,17 @@ def main():
                 kt_sum += np.array(eng.kernel_times())
                 nkt_sum += np.array(eng.node_kernel_times())
                 last.setdefault("first_nkt", eng.node_kernel_times())  # the uncached join
-                if world > 1:
+                if world > 1 and args.gather_node_csr:
+                    # north_star's second collective: the whole per-node CSR on
+                    # rank 0 (per-node counts all-gathered, then each rank's
+                    # slice to rank 0 over its own link)
+                    n_off, n_time, n_rule = eng.node_result_tensors(rin.n_nodes)
+                    g = shard.gather_node_csr(n_off.to(cdev), n_time.to(cdev), n_rule.to(cdev),
+                                              shard_info["lo"], dist)
+                    if g is not None:
+                        last["gathered_events"] = int(g[1].numel())
+                    del g
+                elif world > 1:
                     # per-node offsets of every rank's slice (RCCL allgather of N int64)
                     eng.node_counts_to_device(node_counts.data_ptr())
                     shard.node_offsets(node_counts.to(cdev), dist)
@@ -480,6 +497,8 @@ def main():
     if pn:
         out["kernel_ms"].update({"rule_node_join": nkt[0], "transpose": nkt[1], "node_write": nkt[2]})
         out["config"]["nnz_rule_node_pairs"] = last["nnz"]
+        if args.gather_node_csr and world > 1:
+            out["config"]["gathered_per_node_csr_on_rank0_events"] = last.get("gathered_events")
         out["config"]["windows"] = last["windows"]
         # the rule->node join + transpose depend only on the uploaded rule set and
         # exclude mode: computed on the first call (warmup), reused afterwards

@@ -399,6 +399,22 @@ class Engine:
         check(lib().cg_node_result_device(self._h, C.byref(o), C.byref(t), C.byref(r), C.byref(n)))
         return o.value, t.value, r.value, n.value
 
+    def node_result_tensors(self, n_nodes):
+        """The last per-node result as zero-copy torch views of the engine's
+        device buffers (node_off int64 [N+1], time int64 [E], rule int32 [E]),
+        valid until the next per-node call (__cuda_array_interface__)."""
+        import torch
+        o, t, r, n = self.node_result_device()
+
+        class _View:
+            def __init__(self, ptr, count, typestr):
+                self.__cuda_array_interface__ = {"shape": (count,), "typestr": typestr,
+                                                 "data": (ptr, False), "version": 3}
+        dev = torch.device("cuda", self.device)
+        return (torch.as_tensor(_View(o, n_nodes + 1, "<i8"), device=dev),
+                torch.as_tensor(_View(t, n, "<i8"), device=dev),
+                torch.as_tensor(_View(r, n, "<i4"), device=dev))
+
     def node_result(self, n_nodes, n_events):
         """Copy the last per-node result (node_off, time, rule) to host."""
         node_off = np.empty(n_nodes + 1, dtype=np.int64)
