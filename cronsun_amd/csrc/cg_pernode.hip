@@ -282,7 +282,6 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < kTicketGroups * kTicketStride; i += blockDim.x) tickets[i] = 0;
   const int lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
   const int64_t NK = int64_t(N) * K;
   const int64_t nw = int64_t(gridDim.x) * (blockDim.x >> 6);
   for (int64_t t = blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6); t < NK; t += nw) {
@@ -293,32 +292,54 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
     const int64_t band_hi = rule_off[int64_t(k + 1) * B < R ? int64_t(k + 1) * B : R];
     int64_t run = 0;  // events of the segment so far
     int32_t nrec = 0;
-    for (int64_t pc = p0; pc < p1; pc += 64) {
-      const int64_t p = pc + lane;
-      int32_t r = 0;
-      int64_t a = 0, c = 0;
-      if (p < p1) {
-        r = nt_rule[p];
-        a = rule_off[r];
-        c = rule_off[r + 1] - a;
+    // 256 pairs per round, 4 consecutive ones per lane: all their loads in
+    // flight together (most segments take one or two rounds)
+    for (int64_t pc = p0; pc < p1; pc += 256) {
+      const int64_t pb = pc + 4 * lane;
+      int32_t r[4];
+      int64_t a[4], c[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) r[u] = pb + u < p1 ? nt_rule[pb + u] : -1;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        a[u] = r[u] >= 0 ? rule_off[r[u]] : 0;
+        c[u] = r[u] >= 0 ? rule_off[r[u] + 1] : 0;
       }
-      int64_t incl = c;
+      int64_t lsum = 0;
+      int32_t lne = 0;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        c[u] -= a[u];
+        lsum += c[u];
+        lne += c[u] > 0;
+      }
+      // wave exclusive scans of the lane sums (events) and non-empty counts
+      int64_t incl = lsum;
+      int32_t inc_ne = lne;
       for (int o = 1; o < 64; o <<= 1) {
         const int64_t y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
+        const int32_t z = __shfl_up(inc_ne, o, 64);
+        if (lane >= o) {
+          incl += y;
+          inc_ne += z;
+        }
       }
-      const uint64_t NE = __ballot(c > 0);
-      if (c > 0) {
-        const int64_t d = run + incl - c;
-        const int64_t at = p0 + nrec + __popcll(NE & lt);
-        rec_rule[at] = r;
-        rec_dst[at] = int32_t(d);
-        rec_dlt[at] = int32_t((a - band_lo) - d);
+      int64_t d = run + incl - lsum;
+      int64_t at = p0 + nrec + (inc_ne - lne);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        if (c[u] > 0) {
+          rec_rule[at] = r[u];
+          rec_dst[at] = int32_t(d);
+          rec_dlt[at] = int32_t((a[u] - band_lo) - d);
+          at++;
+        }
+        d += c[u];
       }
       const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(incl)), 63));
       const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(incl) >> 32)), 63));
       run += int64_t((uint64_t(hi) << 32) | lo);
-      nrec += __popcll(NE);
+      nrec += __builtin_amdgcn_readlane(inc_ne, 63);
     }
     if (lane == 0) {
       seg_cnt[s] = run;
