@@ -80,6 +80,11 @@ def main():
     ap.add_argument("--window", type=int, default=0,
                     help="per-node output window in seconds (0 = the workload's; config3: 3600)")
     ap.add_argument("--exclude-mode", choices=["none", "rule", "cumulative"], default="none")
+    ap.add_argument("--zone", default="UTC",
+                    help="time zone of the expansion (UTC, or a TZif name under tests/golden/zoneinfo, "
+                         "e.g. America/New_York: the walk path near DST transitions)")
+    ap.add_argument("--t0", type=int, default=0,
+                    help="horizon start, unix seconds (0 = the workload's: 2026-01-05T00:00Z)")
     ap.add_argument("--cpu-sample", type=int, default=None,
                     help="rules in the CPU-baseline sample (0 = skip; default 40k, 1M for dispatch)")
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -153,13 +158,17 @@ def main():
         H = args.horizon or 7 * 86400
         mix = synth.MIX_LIGHT
         seed = 0x5EED + 4
-    t0 = synth.T0_2026
+    t0 = args.t0 or synth.T0_2026
     t1 = t0 + H
     pn = wl in ("pernode", "config3")
     W = args.window or (3600 if wl == "config3" else H)
     xmode = {"none": 0, "rule": 1, "cumulative": 2}[args.exclude_mode]
     eng = Engine(local)
-    utc = cron.UTC()
+    if args.zone == "UTC":
+        utc = cron.UTC()
+    else:  # the committed tzdata (the GPU box has no other zoneinfo guarantee)
+        with open(os.path.join(ROOT, "tests", "golden", "zoneinfo", args.zone), "rb") as f:
+            utc = cron.LoadLocationFromTZData(args.zone, f.read())
     log(f"[rank {rank}] {wl}: generating {R} rules")
     shard_info = None
     if wl == "config4":
@@ -343,10 +352,11 @@ def main():
         if pn:
             a_last = list(range(t0, t1, W))[-1]
             verify = verify_per_node(eng, spec_of, rin, xmode, a_last, min(a_last + W, t1), last["En_last"],
-                                     max(2, args.verify_sample // 250), seed=0x5EED + 77 + rank)
+                                     max(2, args.verify_sample // 250), seed=0x5EED + 77 + rank,
+                                     zone=args.zone)
         else:
             verify = verify_rule_major(eng, spec_of, R, t0, t1, E, args.verify_sample,
-                                       seed=0x5EED + 99 + rank)
+                                       seed=0x5EED + 99 + rank, zone=args.zone)
         verify["seconds"] = time.perf_counter() - tv
         verify["unwritten_after_poison"] = unwritten
         verify["verified"] = verify["verified"] and unwritten == 0
@@ -427,22 +437,22 @@ def main():
         metric = f"per-node fire events materialised/sec (config 3: 1M jobs × 10k nodes, {hz})"
         workload = (f"config 3: 1M jobs x 10k nodes (500 groups, GroupIDs/NodeIDs/ExcludeNodeIDs), "
                     f"{'config-2' if wl == 'config3' else 'light'} spec mix, {hz} horizon in "
-                    f"{nw} window(s) of {W}s, UTC, per GPU; exclude mode {args.exclude_mode}"
+                    f"{nw} window(s) of {W}s, {args.zone}, per GPU; exclude mode {args.exclude_mode}"
                     + (" (job.go:591-630)" if xmode == 0 else ""))
         traffic = pmc_traffic("pmc_traffic_pernode.json", kname, R, E) if wl == "pernode" else None
     else:
         algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
         kname, ksec = "k_write_cf", kt[3] / 1e3
         metric = METRIC
-        workload = ("config 2: 1M mixed cron rules x 24h horizon, UTC, per GPU (job-ID-range shards)"
-                    if wl == "config2" else
-                    "config 4: 10M rules x 7d horizon, light spec mix, UTC, job-ID-range shards over N GPUs")
+        workload = (f"config 2: 1M mixed cron rules x {H // 3600}h horizon, {args.zone}, per GPU "
+                    f"(job-ID-range shards)" if wl == "config2" else
+                    f"config 4: 10M rules x 7d horizon, light spec mix, {args.zone}, job-ID-range shards over N GPUs")
         traffic = pmc_traffic("pmc_traffic.json", kname, R, E) if wl == "config2" else None
     achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
 
     cpu = None
     if world == 1 and args.cpu_sample != 0 and wl == "config2":
-        cpu = cpu_baseline(specs, args.cpu_sample, t0, t1, args.cpu_threads)
+        cpu = cpu_baseline(specs, args.cpu_sample, t0, t1, args.cpu_threads, zone=args.zone)
 
     out = {
         "metric": metric,
@@ -462,7 +472,7 @@ def main():
             "rules_per_gpu": R,
             "horizon_s": H,
             "t0": t0,
-            "zone": "UTC",
+            "zone": args.zone,
             "events_per_gpu_step": E,
             "shard": shard_info or {"lo": 0, "hi": R},
             "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard totals / per-node counts)",
@@ -581,7 +591,7 @@ def _oracle_scheds(O, specs):
     return O.sched_array(out)
 
 
-def verify_rule_major(eng, spec_of, R, t0, t1, E, sample, seed):
+def verify_rule_major(eng, spec_of, R, t0, t1, E, sample, seed, zone="UTC"):
     """The last timed step's rule-major CSR against the oracle's Next loop on
     a seeded sample of rules (checker only; outside the timed region)."""
     import numpy as np
@@ -590,7 +600,7 @@ def verify_rule_major(eng, spec_of, R, t0, t1, E, sample, seed):
     off = np.empty(R + 1, dtype=np.int64)
     check(lib().cg_result_copy_offsets(eng._h, off.ctypes.data))
     idx = np.sort(np.random.default_rng(seed).choice(R, min(sample, R), replace=False))
-    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(i)) for i in idx]), t0, t1, O.Loc("UTC"),
+    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(i)) for i in idx]), t0, t1, O.Loc(zone),
                             threads=host_cpus()[0])
     bad = 0
     for k, i in enumerate(idx):
@@ -602,7 +612,7 @@ def verify_rule_major(eng, spec_of, R, t0, t1, E, sample, seed):
             "mismatched_rules": int(bad), "offsets_consistent": mono}
 
 
-def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed):
+def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed, zone="UTC"):
     """The last timed window's per-node lists against each sampled node's own
     filter over every rule (node.go:121-158 -> Job.Cmds) composed with the
     oracle's Next loop (checker only; outside the timed region)."""
@@ -615,7 +625,7 @@ def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed):
     nodes = np.sort(np.random.default_rng(seed).choice(rin.n_nodes, n_nodes_sample, replace=False))
     roff, rules = O.node_rules(rin, mode, nodes, threads=threads)
     union = np.unique(rules)
-    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(r)) for r in union]), a, b, O.Loc("UTC"),
+    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(r)) for r in union]), a, b, O.Loc(zone),
                             threads=threads)
     bad, ev = 0, 0
     for k, n in enumerate(nodes):
@@ -660,7 +670,7 @@ def cpu_dispatch(specs, t0):
                       f"({dt * 1e3:.1f} ms per wake: qsort by Next + Next for the due prefix)"}
 
 
-def cpu_baseline(specs, sample, t0, t1, threads):
+def cpu_baseline(specs, sample, t0, t1, threads, zone="UTC"):
     """The oracle's literal Next loop (reference semantics, port of
     spec.go:55-158 + Go time) on this host's CPUs: one pass of
     `t = Next(t)` until > T1 per rule, parallel over rules (the Go baseline's
@@ -670,7 +680,7 @@ def cpu_baseline(specs, sample, t0, t1, threads):
     O = _oracle()
     avail, cpuinfo = host_cpus()
     threads = threads or avail
-    loc = O.Loc("UTC")
+    loc = O.Loc(zone)
 
     def timed(sub):
         tp = time.perf_counter()
@@ -703,7 +713,7 @@ def cpu_baseline(specs, sample, t0, t1, threads):
     what = ("the whole workload" if len(sub) == n else
             f"every {stride}th rule ({len(sub)} of {n})")
     return {"value": ev / dt, "unit": "events/s", "cores": threads, "kind": "port",
-            "sample": f"{what} x {t1 - t0}s horizon, UTC ({ev} events, {dt:.2f}s for one pass of "
+            "sample": f"{what} x {t1 - t0}s horizon, {zone} ({ev} events, {dt:.2f}s for one pass of "
                       f"the Next loop on {threads} threads; parse excluded, +{parse_s:.2f}s parse)",
             "value_incl_parse": ev / (dt + parse_s), "cpu_model": cpu_model, **cpuinfo,
             "go_toolchain": "absent on the box image (oracle C port timed instead)"}
