@@ -302,6 +302,7 @@ int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* p
   pa->G = G;
   pa->nd = nd;
   pa->dtab_global = 0;
+  pa->flags = plan.flags;
   pa->t0 = t0;
   pa->t1 = t1;
   // long horizons: the day table (4 B per local day) stays in HBM and the
@@ -494,7 +495,9 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   // walked runs: WALK windows, or CF segments whose entry fire does not fully
   // match (only possible when the plan has zone transitions)
   const bool all_phases = c->phase_timing >= 2;
-  bool has_walk = c->plan.table.when.size() > 1;
+  // (a CF run is entered by the exact walk only after a WALK segment, or from
+  // T0 when a transition lies in the 40 days before it)
+  bool has_walk = (c->plan.flags & kPlanT0Walk) != 0;
   for (const Segment& sg : c->plan.segs) has_walk |= sg.kind != 0;
   int64_t E = 0;
   unsigned long long stuck = 0;

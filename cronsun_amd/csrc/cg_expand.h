@@ -200,8 +200,8 @@ CG_HD bool past_year_limit(const ZoneView& z, int64_t t, int64_t e, int32_t e_of
 }
 
 CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, int G,
-                      const uint32_t* dtab, int64_t t0, int64_t t1, int64_t* anchor_out,
-                      int32_t* count_out, uint32_t* dmask_out) {
+                      const uint32_t* dtab, int64_t t0, int64_t t1, uint32_t flags,
+                      int64_t* anchor_out, int32_t* count_out, uint32_t* dmask_out) {
   if (sp.kind == KIND_EVERY) {
     // ConstantDelaySchedule: T0 + k*D for k >= 1 (constantdelay.go:25-27),
     // one run per segment (k with T0 + kD in (a, b]; anchor = the time one
@@ -219,26 +219,35 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
   int64_t pos = t0;             // last fire so far (or T0)
   int64_t pending = INT64_MIN;  // Next(pos) if already computed
   bool done = false, ok = true;
+  // The walk from T0 (not a fire) may first reset back to the start of T0's
+  // month, day or hour; with a zone transition in the 40 days before T0 that
+  // reset can land across it, so Next(T0) then comes from the exact walk.
+  const bool t0_walk = (flags & kPlanT0Walk) != 0;
+  // A skipped local day ahead (kPlanFinalWalk): the reference's last Next,
+  // the one past T1, may never return; it is walked to its end.
+  const bool final_walk = (flags & kPlanFinalWalk) != 0;
+  bool final_known = false;  // that last Next has been walked to its end
   for (int s = 0; s < G; s++) {
     const Segment& sg = segs[s];
     int64_t anchor = 0, cnt = 0;
     uint32_t dm = 0;
-    if (!done && sg.kind == 0 && pending == INT64_MIN) {
-      // Next(pos) in closed form: pos is T0 inside this constant-offset span,
-      // or the last fire of the CF segment just before it (same span), so the
-      // walk from pos never leaves the span before its result
+    if (!done && sg.kind == 0 && pending == INT64_MIN && !(t0_walk && pos == t0)) {
+      // Next(pos) in closed form: pos is T0 (no transition in the 40 days
+      // before it) or the last fire of a CF segment before this one in the
+      // same span, so the walk from pos stays in the span until its result
       const int64_t b = sg.b < t1 ? sg.b : t1;
       dm = seg_daymask(sp, sg, dtab);
       const int64_t e = cf_first_after(c, sg, dm, pos > sg.a ? pos : sg.a);
       if (e <= b && past_year_limit(z, pos, e, sg.off)) {
         dm = 0;  // Next(pos) is the zero time: the reference loop stops here
         done = true;
+        final_known = true;
       } else if (e <= b) {
         cnt = 1 + cf_count(c, sg, dm, e, b);
         anchor = e;
         // the run's last fire starts the next segment's search (not needed
         // after the last segment: one closed-form seek saved per rule)
-        if (s + 1 < G) pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
+        if (s + 1 < G || final_walk) pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
       } else {
         dm = 0;  // no fire in this segment; the next one searches from its start
       }
@@ -254,7 +263,7 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
         anchor = e;
         // the run's last fire starts the next segment's search (not needed
         // after the last segment: one closed-form seek saved per rule)
-        if (s + 1 < G) pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
+        if (s + 1 < G || final_walk) pos = cnt > 1 ? cf_value(sg, cf_seek(c, sg, dm, e, cnt - 1)) : e;
       } else {
         // walked run: a WALK segment, or a CF segment entered by a fire the
         // closed form cannot continue from
@@ -263,7 +272,7 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
         for (;;) {
           if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;
           if (e == CG_NO_PROGRESS) { done = true; ok = false; break; }
-          if (e == CG_ZERO_TIME || e == CG_BEYOND) { done = true; break; }
+          if (e == CG_ZERO_TIME || e == CG_BEYOND) { done = true; final_known = e == CG_ZERO_TIME; break; }
           if (e > b) { pending = e; break; }
           cnt++;
           pos = e;
@@ -275,6 +284,10 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
     anchor_out[s] = anchor;
     count_out[s] = (int32_t)cnt;
     dmask_out[s] = dm;
+  }
+  if (final_walk && ok && !final_known) {
+    const int64_t e = next_exact(sp, z, pos, INT64_MAX);
+    if (e == CG_NO_PROGRESS || (e <= pos && e != CG_ZERO_TIME)) ok = false;
   }
   return ok;
 }

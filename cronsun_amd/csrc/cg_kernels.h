@@ -16,6 +16,7 @@ struct PlanArgs {
   const uint32_t* dtab;
   int32_t zn, G, nd;
   int32_t dtab_global;  // 1: the day table is read from HBM (too large to stage in LDS)
+  uint32_t flags;       // Plan::flags (kPlanT0Walk | kPlanFinalWalk)
   int64_t t0, t1;
 };
 

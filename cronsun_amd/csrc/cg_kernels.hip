@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, 
        r += int64_t(gridDim.x) * blockDim.x) {
     DSpec sp = load_spec(specs + r);
     const int64_t j0 = r * G;
-    if (!count_rule(sp, v.z, v.segs, G, v.dtab, p.t0, p.t1, run_anchor + j0, run_count + j0,
+    if (!count_rule(sp, v.z, v.segs, G, v.dtab, p.t0, p.t1, p.flags, run_anchor + j0, run_count + j0,
                     run_dmask + j0))
       atomicMin(stuck_rule, (unsigned long long)r);
   }

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cstdlib>
 #include <cstring>
 
 #include "cg_time.h"
@@ -373,18 +374,47 @@ ZoneTable build_table(const ZoneRules& z, int64_t lo, int64_t hi) {
 Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
   Plan plan;
   const int64_t kDay = 86400;
-  plan.table = build_table(z, t0 - 64 * kDay, t1 + 64 * kDay);
+  // the table reaches six years past T1: the reference's last Next (the one
+  // past T1) may walk up to five years on (spec.go:70-76)
+  plan.table = build_table(z, t0 - 64 * kDay, t1 + (6 * 366 + 64) * kDay);
   if (t1 <= t0) return plan;
-  // Inside (a, b] with a constant offset on [a - M, b + M], every lookup the
-  // Go walk between two consecutive fires makes (fields at visited instants,
-  // Date at local-seconds-as-UTC) sees that one offset, so Next there is the
-  // fixed-offset walk, i.e. the first matching local time.
-  const int64_t M = int64_t(plan.table.max_abs_off) + 3600;
-  plan.margin = M;
-  std::vector<std::pair<int64_t, int64_t>> win;  // (lo, hi] WALK windows
   for (size_t i = 1; i < plan.table.when.size(); i++) {
-    int64_t tau = plan.table.when[i];
-    int64_t lo = std::max(tau - M, t0), hi = std::min(tau + M, t1);
+    const int64_t tau = plan.table.when[i];
+    // the walk from T0 may reset back across a transition of the last 40 days
+    if (tau > t0 - 40 * kDay && tau <= t0) plan.flags |= kPlanT0Walk;
+    // a skipped local day (e.g. Pacific/Apia 2011-12-30): AddDate(0,0,1) can
+    // stall there, so the last Next must be walked to its end
+    if (tau > t0 && plan.table.off[i] - plan.table.off[i - 1] >= kDay) plan.flags |= kPlanFinalWalk;
+  }
+  // WALK windows.  Between two consecutive fires e < u the Go
+  // walk visits only instants in [e + 1, u]; it reads fields there (exact when
+  // the offset is the segment's) and calls Date for civil times whose
+  // fixed-offset instant X lies there.  With a single transition tau (o1 ->
+  // o2, d = o2 - o1) within A = max|off| + max|d| of X, Date(X + o(X)) = X
+  // except on the overlap of a backward transition (d < 0): after tau,
+  // [tau, tau + min(-o2, -d)) when o2 < 0 (Go resolves those civil times to
+  // the first pass); before tau, [tau - min(o1, -d), tau) when o1 > 0.  So a CF
+  // segment may run up to tau - 1 and resume after that bad set: the window
+  // around tau is (tau - 1 - before, tau + after], and the walk that crosses it
+  // (from the last fire before) is the exact walk.  Transitions closer than
+  // 2A share one window (a CF instant must see at most one of them).
+  int32_t max_d = 0;
+  for (size_t i = 2; i < plan.table.when.size(); i++)
+    max_d = std::max(max_d, std::abs(plan.table.off[i] - plan.table.off[i - 1]));
+  const int64_t A = int64_t(plan.table.max_abs_off) + max_d;
+  plan.margin = A;
+  std::vector<std::pair<int64_t, int64_t>> win;  // (lo, hi] WALK windows
+  int64_t prev_tau = INT64_MIN;
+  for (size_t i = 1; i < plan.table.when.size(); i++) {
+    const int64_t tau = plan.table.when[i];
+    const int64_t o1 = plan.table.off[i - 1], o2 = plan.table.off[i], d = o2 - o1;
+    const int64_t before = (d < 0 && o1 > 0) ? std::min(o1, -d) : 0;
+    const int64_t after = (d < 0 && o2 < 0) ? std::min(-o2, -d) : 0;
+    int64_t lo = tau - 1 - before - 2, hi = tau + after + 2;  // +-2 s: no off-by-one risk
+    if (prev_tau != INT64_MIN && tau - prev_tau <= 2 * A + 8) lo = std::min(lo, prev_tau);  // one window
+    prev_tau = tau;
+    lo = std::max(lo, t0);
+    hi = std::min(hi, t1);
     if (hi <= lo) continue;
     if (!win.empty() && lo <= win.back().second) win.back().second = std::max(win.back().second, hi);
     else win.push_back({lo, hi});

@@ -45,9 +45,11 @@ struct ZoneTable {
 };
 ZoneTable build_table(const ZoneRules& z, int64_t lo, int64_t hi);
 
-// Expansion plan for (T0, T1]: alternating closed-form (CF) spans, inside
-// which the offset is constant with a margin on both sides, and WALK spans
-// around zone transitions where Next is emulated step by step.
+// Expansion plan for (T0, T1]: closed-form (CF) spans of one offset, on which
+// every Date call of the Go walk returns its fixed-offset instant, and WALK
+// spans around zone transitions (at least the transition instant itself, plus
+// the overlap Go resolves to the other pass) where Next is emulated step by
+// step.  margin = A: transitions closer than 2A share one WALK span.
 struct Segment {
   int64_t a, b;    // (a, b] in UTC seconds
   int64_t base;    // UTC instant of local midnight of day0 (CF only)
@@ -57,11 +59,14 @@ struct Segment {
   int32_t ndays;   // local days spanned (CF only, <= 31)
   int32_t dt_off;  // offset into the day table (CF only)
 };
+constexpr uint32_t kPlanT0Walk = 1;     // Next(T0) by the exact walk
+constexpr uint32_t kPlanFinalWalk = 2;  // the Next past T1 walked to its end
 struct Plan {
   std::vector<Segment> segs;
   std::vector<uint32_t> dtab;  // per CF local day: month | dom << 4 | dow << 9
   ZoneTable table;
   int64_t margin = 0;
+  uint32_t flags = 0;  // kPlanT0Walk | kPlanFinalWalk (cg_expand.h)
 };
 Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1);
 

@@ -2,6 +2,8 @@
 // closed-form iteration + WALK re-walk, exactly what k_count/k_write_cf/
 // k_write_walk run) against the oracle's literal Next loop.  Test
 // infrastructure; the GPU tests check the kernels themselves.
+#include <algorithm>
+#include <cstdlib>
 #include <random>
 
 #include "../../cronsun_amd/csrc/cg_expand.h"
@@ -34,6 +36,9 @@ int main(int argc, char** argv) {
   const char* zone = argc > 1 ? argv[1] : "UTC";
   int nspec = argc > 2 ? atoi(argv[2]) : 400;
   const bool long_mode = argc > 4 && std::string(argv[4]) == "long";
+  // near mode: T0 at many offsets around transitions of 2011-2027 (just before,
+  // on, inside the overlap, hours and days after), 30-hour horizons
+  const bool near_mode = argc > 4 && std::string(argv[4]) == "near";
   ZoneRules zr;
   or_loc* ol = nullptr;
   load_zone(zone, &zr, &ol);
@@ -65,6 +70,21 @@ int main(int argc, char** argv) {
     hz.push_back({tt.when[i] - 43217, tt.when[i] + 43200});
     hz.push_back({tt.when[i] - 3 * 86400, tt.when[i] + 4 * 86400});
   }
+  if (near_mode) {
+    hz.clear();
+    ZoneTable nt = build_table(zr, 1293840000, 1830297600);
+    const size_t n = nt.when.size() > 1 ? nt.when.size() - 1 : 0;
+    const int64_t offs[] = {-7201, -3600, -2, -1, 0, 1, 2, 1799, 3599, 3600, 3601, 5400, 18000,
+                            18001, 72000, 90000, 3 * 86400, 35 * 86400 + 7};
+    std::vector<size_t> pick;
+    for (size_t k = 0; k < 6 && k < n; k++) pick.push_back(1 + (n > 6 ? k * (n - 1) / 5 : k));
+    size_t big = 0;  // and the largest jump (Pacific/Apia's skipped 2011-12-30)
+    for (size_t i = 1; i <= n; i++)
+      if (!big || std::abs(nt.off[i] - nt.off[i - 1]) > std::abs(nt.off[big] - nt.off[big - 1])) big = i;
+    if (big && std::find(pick.begin(), pick.end(), big) == pick.end()) pick.push_back(big);
+    for (size_t i : pick)
+      for (int64_t o : offs) hz.push_back({nt.when[i] + o, nt.when[i] + o + 30 * 3600});
+  }
   if (long_mode)  // three years from 2026; 2095-06-01 .. 2106-06-01 (Feb 29 gap over 2100)
     hz = {{1767571200 - 77, 1767571200 + 1096 * 86400}, {3957984000, 3957984000 + 4018 * 86400}};
   int bad = 0;
@@ -79,7 +99,7 @@ int main(int argc, char** argv) {
       std::vector<int32_t> cnt(G);
       std::vector<uint32_t> dm(G);
       std::vector<int64_t> got;
-      bool ok = G == 0 || count_rule(d, zv, plan.segs.data(), G, plan.dtab.data(), t0, t1, anc.data(), cnt.data(), dm.data());
+      bool ok = G == 0 || count_rule(d, zv, plan.segs.data(), G, plan.dtab.data(), t0, t1, plan.flags, anc.data(), cnt.data(), dm.data());
       for (int s = 0; s < G && ok; s++) {
         const Segment& sg = plan.segs[s];
         if (d.kind == KIND_EVERY) {
@@ -104,7 +124,7 @@ int main(int argc, char** argv) {
         }
       }
       int64_t n = or_expand(&scheds[r], t0, t1, ol, nullptr, 0);
-      if (n < 0) { if (ok) { if (bad++ < 10) printf("NOPROGRESS mismatch %s\n", names[r].c_str()); } continue; }
+      if (n < 0) { if (ok) { if (bad++ < 10) printf("NOPROGRESS mismatch %s (%lld,%lld] got %zu fires, G=%d\n", names[r].c_str(), (long long)t0, (long long)t1, got.size(), G); } continue; }
       std::vector<int64_t> exp(n);
       or_expand(&scheds[r], t0, t1, ol, exp.data(), n);
       total += n;

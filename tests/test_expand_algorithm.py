@@ -47,3 +47,17 @@ def test_host_algorithm_long_horizons(expand_host, zone):
                          text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     assert " 0 mismatches" in out.stdout
+
+
+@pytest.mark.parametrize("zone", ["America/New_York", "Europe/Dublin", "America/Havana", "Australia/Lord_Howe",
+                                  "Pacific/Chatham", "Pacific/Apia", "Africa/Casablanca", "America/Sao_Paulo"])
+def test_host_algorithm_near_transitions(expand_host, zone):
+    """T0 at 18 offsets around six transitions of 2011-2027 (just before, on,
+    inside a backward transition's overlap, hours and days after; Pacific/Apia's
+    skipped 2011-12-30 included): narrow WALK windows, Next(T0) by the exact
+    walk after a recent transition, and the reference's last Next past T1
+    walked to its end where a skipped day could stall it."""
+    out = subprocess.run([expand_host, zone, "150", "13", "near"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert " 0 mismatches" in out.stdout

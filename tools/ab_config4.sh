@@ -1,12 +1,19 @@
 #!/bin/bash
-# A/B of library variants on config 4 (10M x 7 d): tools/ab_config4.sh <tag> <lib-suffix>...
+# A/B of library variants (built with make OUT=../libcronsun_gpu_<suffix>.so):
+#   WL=config4 tools/ab_config4.sh <tag> <lib-suffix|base>...   (WL default config4)
+# Two interleaved rounds, so box drift shows as a spread, not as a difference.
 set -o pipefail
 OUT=gpurun_out/${1:-ab4}
 shift
+WL=${WL:-config4}
+STEPS=${STEPS:-3}
 mkdir -p "$OUT"
+for round in 1 2; do
 for v in "$@"; do
   [ "$v" = base ] && v=""
-  CRONSUN_GPU_LIB=$PWD/cronsun_amd/libcronsun_gpu${v:+_$v}.so timeout -k 10 400 python bench.py --workload config4 \
-    --steps 3 --warmup 1 --cpu-sample 0 > "$OUT/${v:-base}.json" 2> "$OUT/${v:-base}.err" || { tail -20 "$OUT/${v:-base}.err"; exit 1; }
-  python3 -c "import json; d=json.load(open('$OUT/${v:-base}.json')); print('%-8s config4 write_cf=%.3f ms step=%.3f ms' % ('${v:-base}', d['kernel_ms']['write_cf'], d['ms_per_step']))"
+  f="$OUT/${WL}_${v:-base}_$round"
+  CRONSUN_GPU_LIB=$PWD/cronsun_amd/libcronsun_gpu${v:+_$v}.so timeout -k 10 400 python bench.py --workload $WL \
+    --steps $STEPS --warmup 1 --cpu-sample 0 --verify-sample 200 > "$f.json" 2> "$f.err" || { tail -20 "$f.err"; exit 1; }
+  python3 -c "import json; d=json.load(open('$f.json')); k=d['kernel_ms']; print('%-8s %s round $round write_cf=%.3f node_write=%s step=%.3f ms verified=%s' % ('${v:-base}', '$WL', k['write_cf'], k.get('node_write'), d['ms_per_step'], d['verified']))"
+done
 done
