@@ -398,6 +398,9 @@ Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
   // around tau is (tau - 1 - before, tau + after], and the walk that crosses it
   // (from the last fire before) is the exact walk.  Transitions closer than
   // 2A share one window (a CF instant must see at most one of them).
+  // The overlap's bad set matters only where it holds a local hour start (see
+  // below): America/New_York's 01:00-02:00 second pass holds none past tau
+  // itself, Pacific/Chatham's 02:45-03:45 first pass holds 03:00.
   int32_t max_d = 0;
   for (size_t i = 2; i < plan.table.when.size(); i++)
     max_d = std::max(max_d, std::abs(plan.table.off[i] - plan.table.off[i - 1]));
@@ -408,8 +411,18 @@ Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
   for (size_t i = 1; i < plan.table.when.size(); i++) {
     const int64_t tau = plan.table.when[i];
     const int64_t o1 = plan.table.off[i - 1], o2 = plan.table.off[i], d = o2 - o1;
-    const int64_t before = (d < 0 && o1 > 0) ? std::min(o1, -d) : 0;
-    const int64_t after = (d < 0 && o2 < 0) ? std::min(-o2, -d) : 0;
+    int64_t before = (d < 0 && o1 > 0) ? std::min(o1, -d) : 0;
+    int64_t after = (d < 0 && o2 < 0) ? std::min(-o2, -d) : 0;
+    // Between two fires of a segment, Go's walk calls Date only for local
+    // hour starts (its resets land on the instant after the previous fire,
+    // which starts the unit that changed; AddDate steps go from midnights to
+    // midnights or month starts).  A bad set with no local hour start on the
+    // segment's side of the +-2 s margin is never reached: no window for it.
+    auto hour_start_at_or_after = [](int64_t x, int64_t o) {  // first instant >= x with local h:00:00
+      return floordiv64(x + o + 3599, 3600) * 3600 - o;
+    };
+    if (after > 0 && hour_start_at_or_after(tau + 3, o2) >= tau + after) after = 0;
+    if (before > 0 && floordiv64(tau - 3 + o1, 3600) * 3600 - o1 < tau - before) before = 0;
     int64_t lo = tau - 1 - before - 2, hi = tau + after + 2;  // +-2 s: no off-by-one risk
     if (prev_tau != INT64_MIN && tau - prev_tau <= 2 * A + 8) lo = std::min(lo, prev_tau);  // one window
     prev_tau = tau;
