@@ -234,3 +234,34 @@ def test_output_growth_and_reuse():
     t0 = synth.T0_2026
     for scheds, t1 in ((small, t0 + DAY), (big, t0 + 2 * DAY), (small, t0 + DAY), (big, t0 + DAY)):
         check_same(eng, scheds, "UTC", t0, t1)
+
+
+@pytest.mark.parametrize("t0", [1772910000, 1793469600], ids=["ny-spring", "ny-fall"])
+def test_config2_scale_dst_day(eng, t0):
+    """Config 2 at full size in America/New_York over the 24 h centred on the
+    2026 spring-forward / fall-back (the walk path: the transition's WALK
+    window, its crossing walks, the fall-back overlap), bit-exact on a seeded
+    sample that includes every every-second rule."""
+    n = 1_000_000
+    specs = synth.spec_mix(n, seed=0x5EED)
+    arr, status = cron.parse_batch(specs)
+    assert (status == 0).all()
+    sp = eng.upload_c(arr, n)
+    t1 = t0 + DAY
+    E = eng.expand_device(sp, product_zone("America/New_York"), t0, t1)
+    off = np.empty(n + 1, dtype=np.int64)
+    from cronsun_amd._lib import check, lib
+    check(lib().cg_result_copy_offsets(eng._h, off.ctypes.data))
+    assert off[0] == 0 and off[-1] == E and (np.diff(off) >= 0).all()
+    times = eng.copy_times(0, E)
+    assert ((times > t0) & (times <= t1)).all()
+    steps = np.nonzero(np.diff(times) <= 0)[0] + 1
+    assert np.isin(steps, off[1:-1]).all()
+    rng = np.random.default_rng(t0 & 0xFFFF)
+    heavy = [i for i in range(n) if specs[i] == "* * * * * *"][:200]
+    idx = np.unique(np.concatenate([rng.choice(n, 3000, replace=False), np.array(heavy, dtype=np.int64)]))
+    sample = [cron.Parse(specs[i]) for i in idx]
+    eo, et = oracle_csr(sample, "America/New_York", t0, t1, [specs[i] for i in idx])
+    for k, i in enumerate(idx):
+        assert np.array_equal(times[off[i]:off[i + 1]], et[eo[k]:eo[k + 1]]), specs[i]
+    sp.free()
