@@ -449,7 +449,7 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   if (all_phases) (void)hipEventRecord(c->ev[0], c->st);
   launch_count(s->d, R, pa, c->run_anchor.p, c->run_count.p, c->run_dmask.p, c->stuck.p, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[1], c->st);
-  if (map_cap > 0 && (rc = c->block_run.ensure(map_cap / kSuper + 2 + kTicketWords + 8))) return rc;
+  if (map_cap > 0 && (rc = c->block_run.ensure(slice_map_words(map_cap)))) return rc;
   launch_scan_runs(c->run_count.p, c->run_off.p, R, int32_t(G), c->scan_tmp.p, c->offsets.p, c->res_dev,
                    c->stuck.p, map_cap > 0 ? c->block_run.p : nullptr, map_cap, c->st);
   if (all_phases) (void)hipEventRecord(c->ev[2], c->st);
@@ -503,7 +503,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   unsigned long long stuck = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(c->times.cap);
-    if ((rc = c->block_run.ensure(cap / kSuper + 2 + kTicketWords + 8))) return rc;
+    if ((rc = c->block_run.ensure(slice_map_words(cap)))) return rc;
     if (all_phases) (void)hipEventRecord(c->ev[3], c->st);
     if (!(cap0 > 0 && cap == cap0))
       launch_chunk_map(c->run_off.p, nruns, cap, c->block_run.p, c->st);

@@ -25,17 +25,12 @@ struct PlanArgs {
 constexpr int kMaxSegments = 1024;
 constexpr size_t kPlanLdsBytes = 60 * 1024;
 
-// closed-form writer: 4 waves per block; waves take kSuper-event output slices
+// closed-form writer: 4 waves per block; waves take output slices by ticket
 constexpr int kWriteWaves = 4;
 #ifndef CG_WRITE_BPC
 #define CG_WRITE_BPC 4
 #endif
 constexpr int kWriteBlocksPerCU = CG_WRITE_BPC;  // persistent grid: blocks of 4 waves per CU
-#ifndef CG_SUPER
-#define CG_SUPER 2048
-#endif
-constexpr int kSuper = CG_SUPER;  // events per writer slice (multiple of 64)
-static_assert(kSuper % 64 == 0, "writer slices are whole 64-event blocks");
 // writer slice tickets: one u32 counter per group of blocks, 128 B apart
 #ifndef CG_TICKET_GROUPS
 #define CG_TICKET_GROUPS 32
@@ -43,6 +38,27 @@ static_assert(kSuper % 64 == 0, "writer slices are whole 64-event blocks");
 constexpr int kTicketGroups = CG_TICKET_GROUPS;
 constexpr int kTicketStride = 32;                                  // u32 words
 constexpr int kTicketWords = kTicketGroups * kTicketStride / 2;    // int64 words
+// Events per writer slice, chosen per call from the output capacity (host and
+// kernels derive it from the same cap): 2048 (a 16-KB write front per wave)
+// below 2^31 events, 16384 above (fewer slices, tickets and map entries).
+// A/B on one box (profiles/r02_ab_slices.json): config 2 (0.67 G events)
+// 0.99-1.01 ms at 2048 vs 1.10 ms at 16384; config 4 (18.2 G) 25.9 ms vs 24.2.
+#ifndef CG_SUPER_SHIFT_SMALL
+#define CG_SUPER_SHIFT_SMALL 11
+#endif
+#ifndef CG_SUPER_SHIFT_LARGE
+#define CG_SUPER_SHIFT_LARGE 14
+#endif
+static_assert(CG_SUPER_SHIFT_SMALL >= 6 && CG_SUPER_SHIFT_LARGE >= 6, "slices are whole 64-event blocks");
+__host__ __device__ inline int super_shift(int64_t cap) {
+  return cap >= (int64_t(1) << 31) ? CG_SUPER_SHIFT_LARGE : CG_SUPER_SHIFT_SMALL;
+}
+// slice-map entries for an output capacity: the map, 2 sentinels, the ticket
+// counters and 8 debug words
+inline int64_t slice_map_words(int64_t cap) {
+  return (cap >> super_shift(cap)) + 2 + kTicketWords + 8;
+}
+
 
 size_t plan_lds_bytes(const PlanArgs& p);
 
@@ -102,7 +118,7 @@ void launch_scan_runs(const int32_t* run_count, int64_t* run_off, int64_t R, int
                       int64_t* offsets, int64_t* res, unsigned long long* stuck,
                       int64_t* chunk_run, int64_t cap, hipStream_t st);
 
-// chunk_run needs cap / kSuper + 2 + kTicketWords + 8 entries (slice map, the
+// chunk_run needs slice_map_words(cap) entries (slice map, the
 // writer's slice tickets, 8 diagnostic counters); both read E = run_off[nruns]
 // on the device (no host sync) and do nothing when E > cap
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,

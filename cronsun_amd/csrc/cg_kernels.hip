@@ -6,7 +6,7 @@
 //                or the walked count inside WALK windows -> run records
 //   k_scan_*     exclusive scan of run counts -> run offsets (int64); the
 //                last pass also writes the rule-major CSR offsets
-//   k_chunk_map  first run touched by each kSuper-event output slice
+//   k_chunk_map  first run touched by each output slice (super_shift(cap))
 //   k_write_cf   persistent, output-parallel: each wave walks its slices;
 //                long runs are written wave-cooperatively (64 consecutive
 //                fires per store instruction, mixed-radix digits + lane rank
@@ -464,7 +464,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const T* __restrict
     if (idx < n) out[idx + 1] = run;
   }
   if (tail.offsets) {
-    const int64_t last_sup = tail.cap / kSuper;  // map entries 0 .. last_sup + 1
+    const int sh = super_shift(tail.cap);
+    const int64_t sup = int64_t(1) << sh;
+    const int64_t last_sup = tail.cap >> sh;  // map entries 0 .. last_sup + 1
     if (tail.chunk_run && blockIdx.x == 0)
       for (int i = threadIdx.x; i < kTicketWords + 8; i += kScanThreads)
         tail.chunk_run[last_sup + 2 + i] = 0;
@@ -476,9 +478,9 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const T* __restrict
         tail.offsets[(idx + 1) / tail.G] = r;
       if (tail.chunk_run && idx < n && v[i] > 0) {
         // slices whose first event lies in this (non-empty) run: the largest
-        // j with run_off[j] <= c*kSuper, as k_chunk_map's search finds it
+        // j with run_off[j] <= c*sup, as k_chunk_map's search finds it
         const int64_t lo = r - v[i];
-        for (int64_t c = (lo + kSuper - 1) / kSuper; c * kSuper < r && c <= last_sup; c++)
+        for (int64_t c = (lo + sup - 1) >> sh; (c << sh) < r && c <= last_sup; c++)
           tail.chunk_run[c] = idx;
       }
       r -= v[i];
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan_apply(const T* __restrict
       tail.res[0] = run;  // = out[n]: the thread's values past n - 1 are zeros
       tail.res[1] = int64_t(*tail.stuck);
       *tail.stuck = ~0ull;
-      const int64_t nsup = (run + kSuper - 1) / kSuper;
+      const int64_t nsup = (run + sup - 1) >> sh;
       if (tail.chunk_run && nsup <= last_sup + 1) tail.chunk_run[nsup] = n - 1;
     }
   }
@@ -504,20 +506,22 @@ __device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, i
   return lo;
 }
 
-// first run touched by each kSuper-event output slice; E is read on the device
+// first run touched by each output slice (2^super_shift(cap) events); E is read on the device
 // so the launch needs no host sync (grid sized by capacity, extra threads exit)
-// (chunk_run holds cap / kSuper + 2 + kTicketWords entries: the map, then the
+// (chunk_run holds slice_map_words(cap) entries: the map, then the
 // writer's slice ticket counters, reset here)
 __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, int64_t cap,
                             int64_t* __restrict__ chunk_run) {
+  const int sh = super_shift(cap);
+  const int64_t sup = int64_t(1) << sh;
   if (blockIdx.x == 0)
-    for (int i = threadIdx.x; i < kTicketWords + 8; i += blockDim.x) chunk_run[cap / kSuper + 2 + i] = 0;
+    for (int i = threadIdx.x; i < kTicketWords + 8; i += blockDim.x) chunk_run[(cap >> sh) + 2 + i] = 0;
   const int64_t E = run_off[nruns];
   if (E > cap) return;
-  const int64_t nsup = (E + kSuper - 1) / kSuper;
+  const int64_t nsup = (E + sup - 1) >> sh;
   for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c <= nsup;
        c += int64_t(gridDim.x) * blockDim.x)
-    chunk_run[c] = c == nsup ? nruns - 1 : search_run(run_off, 0, nruns - 1, c * int64_t(kSuper));
+    chunk_run[c] = c == nsup ? nruns - 1 : search_run(run_off, 0, nruns - 1, c << sh);
 }
 
 
@@ -832,7 +836,7 @@ __device__ void coop_every(const WinRun& w, int64_t roff, int64_t p0, int64_t p1
   drive<V, false>([&]() { return t; }, [&]() { t += st; }, p0, p1, pd, times);
 }
 
-// Persistent closed-form writer.  Waves work independently on kSuper-event
+// Persistent closed-form writer.  Waves work independently on 2^super_shift(cap)-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
 // consecutive runs (one coalesced round of loads, staged in its LDS slice;
 // only the runs the slice can touch are loaded) and walks its slice run by
@@ -861,7 +865,9 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   WinRun* win = win_all[wave];
   const int64_t E = run_off[nruns];
   if (E > cap) return;  // output buffer too small: host grows it and relaunches
-  const int64_t nsup = (E + kSuper - 1) / kSuper;
+  const int sh = super_shift(cap);
+  const int64_t sup = int64_t(1) << sh;
+  const int64_t nsup = (E + sup - 1) >> sh;
   int64_t woff = INT64_MAX;  // this lane's window run: offset, count
   int32_t wcnt = 0;
   int64_t jend = nruns;  // runs the current slice can touch: [.., jend)
@@ -898,7 +904,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
   const int grp = int(blockIdx.x % unsigned(ng));
   unsigned int* ticket =
-      reinterpret_cast<unsigned int*>(chunk_run + cap / kSuper + 2) + grp * kTicketStride;
+      reinterpret_cast<unsigned int*>(chunk_run + (cap >> sh) + 2) + grp * kTicketStride;
   int64_t static_next = int64_t(blockIdx.x) * kWriteWaves + wave;
   auto take = [&]() -> int64_t {
     if (V & 16) {  // diagnostic: static grid-stride split
@@ -916,8 +922,8 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   const uint64_t k_start = clk();
   for (int64_t c = take(); c < nsup;) {
     const int64_t c_next = take();
-    int64_t pos = c * kSuper;  // multiple of 64: every store below is a whole 512 B block
-    const int64_t S1 = E - pos < kSuper ? E : pos + kSuper;
+    int64_t pos = c << sh;  // multiple of 64: every store below is a whole 512 B block
+    const int64_t S1 = E - pos < sup ? E : pos + sup;
     uint64_t t_a = clk();
     if (V & 64) {  // diagnostic: plain fill of the slice (with bit 3: + the skeleton's reads)
       for (int64_t b = pos + lane; b < S1; b += 64) put<V>(times + b, b);
@@ -984,7 +990,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   if (V & 32) {
     st_all = clk() - k_start;
     unsigned long long* dbg =
-        reinterpret_cast<unsigned long long*>(chunk_run + cap / kSuper + 2 + kTicketWords);
+        reinterpret_cast<unsigned long long*>(chunk_run + (cap >> sh) + 2 + kTicketWords);
     if (lane == 0) {
       atomicAdd(dbg + 0, st_all);
       atomicAdd(dbg + 1, st_win);
@@ -998,7 +1004,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   }
 }
 
-// diagnostic store ceiling (CG_WRITE_PROBE): fill the kSuper slices of the
+// diagnostic store ceiling (CG_WRITE_PROBE): fill the writer's slices of the
 // output with W*8-byte-per-lane stores, 64 lanes contiguous
 template <int W>
 __global__ __launch_bounds__(kWriteWaves * 64) void k_fill_probe(const int64_t* __restrict__ run_off,
@@ -1007,11 +1013,12 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_fill_probe(const int64_t* 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t E = run_off[nruns];
   if (E > cap) return;
+  const int64_t kSup = int64_t(1) << super_shift(cap);
   if (W == 6 || W == 7) {  // per-wave streams with a pause (s_sleep) after every 24 stores
-    const int64_t nsup = (E + kSuper - 1) / kSuper;
+    const int64_t nsup = (E + kSup - 1) / kSup;
     const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
     for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
-      const int64_t p0 = c * kSuper, p1 = E - p0 < kSuper ? E : p0 + kSuper;
+      const int64_t p0 = c * kSup, p1 = E - p0 < kSup ? E : p0 + kSup;
       int k = 0;
       for (int64_t b = p0 + lane; b < p1; b += 64) {
         times[b] = b;
@@ -1025,17 +1032,17 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_fill_probe(const int64_t* 
     return;
   }
   if (W == 4) {  // block-wide streams: the 4 waves interleave 512 B pieces of one slice
-    const int64_t nsup = (E + kSuper - 1) / kSuper;
+    const int64_t nsup = (E + kSup - 1) / kSup;
     for (int64_t c = blockIdx.x; c < nsup; c += gridDim.x) {
-      const int64_t p0 = c * kSuper, p1 = E - p0 < kSuper ? E : p0 + kSuper;
+      const int64_t p0 = c * kSup, p1 = E - p0 < kSup ? E : p0 + kSup;
       for (int64_t b = p0 + wave * 64 + lane; b < p1; b += 64 * kWriteWaves) times[b] = b;
     }
     return;
   }
-  const int64_t nsup = (E + kSuper - 1) / kSuper;
+  const int64_t nsup = (E + kSup - 1) / kSup;
   const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
   for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
-    const int64_t p0 = c * kSuper + (W == 3 ? 8 : 0), p1 = E - c * kSuper < kSuper ? E : c * kSuper + kSuper;
+    const int64_t p0 = c * kSup + (W == 3 ? 8 : 0), p1 = E - c * kSup < kSup ? E : c * kSup + kSup;
     for (int64_t b = p0 + lane * (W == 3 ? 1 : W); b < p1; b += 64 * (W == 3 ? 1 : W)) {
       if (W == 2 && b + 1 < p1) {
         longlong2 v;
@@ -1280,7 +1287,7 @@ void launch_scan_runs(const int32_t* run_count, int64_t* run_off, int64_t R, int
 
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
                       hipStream_t st) {
-  int64_t max_sup = cap / kSuper + 1;
+  int64_t max_sup = (cap >> super_shift(cap)) + 1;
   hipLaunchKernelGGL(k_chunk_map, dim3(grid_for(max_sup + 1, 256, 4096)), dim3(256), 0, st,
                      run_off, nruns, cap, chunk_run);
 }
@@ -1360,7 +1367,7 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
 #undef CG_WCF
   if (variant & 32) {
     unsigned long long d[8];
-    (void)hipMemcpyAsync(d, chunk_run + cap / kSuper + 2 + kTicketWords, sizeof d,
+    (void)hipMemcpyAsync(d, chunk_run + (cap >> super_shift(cap)) + 2 + kTicketWords, sizeof d,
                          hipMemcpyDeviceToHost, st);
     (void)hipStreamSynchronize(st);
     fprintf(stderr,
