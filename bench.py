@@ -94,6 +94,9 @@ def main():
     ap.add_argument("--gather-node-csr", action="store_true",
                     help="pernode/config3 at N > 1: every step also gathers the whole per-node CSR on "
                          "rank 0 (shard.gather_node_csr; timed)")
+    ap.add_argument("--time-order", action="store_true",
+                    help="pernode/config3: every window's per-node lists are also reordered by (time, "
+                         "rule) on the device (cg_node_result_order_by_time; timed)")
     ap.add_argument("--diagnostic", action="store_true",
                     help="allow the diagnostic library / CG_WRITE_* CG_NODE_* switches (the line is "
                          "then marked diagnostic and is not a headline)")
@@ -271,6 +274,8 @@ def main():
                 last["En_last"] = En_w
                 kt_sum += np.array(eng.kernel_times())
                 nkt_sum += np.array(eng.node_kernel_times())
+                if args.time_order:
+                    last["order_ms"] = last.get("order_ms", 0.0) + eng.node_order_by_time()
                 last.setdefault("first_nkt", eng.node_kernel_times())  # the uncached join
                 if world > 1 and args.gather_node_csr:
                     # north_star's second collective: the whole per-node CSR on
@@ -325,6 +330,7 @@ def main():
     wake["due"] = wake["wakes"] = 0
     wake["wall"] = []
     step_wall = []
+    last["order_ms"] = 0.0
     for _ in range(args.steps):
         ts = time.perf_counter()
         E = step()
@@ -353,7 +359,7 @@ def main():
             a_last = list(range(t0, t1, W))[-1]
             verify = verify_per_node(eng, spec_of, rin, xmode, a_last, min(a_last + W, t1), last["En_last"],
                                      max(2, args.verify_sample // 250), seed=0x5EED + 77 + rank,
-                                     zone=args.zone)
+                                     zone=args.zone, time_order=args.time_order)
         else:
             verify = verify_rule_major(eng, spec_of, R, t0, t1, E, args.verify_sample,
                                        seed=0x5EED + 99 + rank, zone=args.zone)
@@ -506,6 +512,9 @@ def main():
         out["end_to_end_rank0"] = e2e
     if pn:
         out["kernel_ms"].update({"rule_node_join": nkt[0], "transpose": nkt[1], "node_write": nkt[2]})
+        if args.time_order:  # (time, rule) reorder of every node's list, per step
+            out["kernel_ms"]["time_order"] = last["order_ms"] / args.steps
+            out["config"]["per_node_order"] = "(time, rule) within every node (cron.go:64-79 byTime)"
         out["config"]["nnz_rule_node_pairs"] = last["nnz"]
         if args.gather_node_csr and world > 1:
             out["config"]["gathered_per_node_csr_on_rank0_events"] = last.get("gathered_events")
@@ -612,7 +621,7 @@ def verify_rule_major(eng, spec_of, R, t0, t1, E, sample, seed, zone="UTC"):
             "mismatched_rules": int(bad), "offsets_consistent": mono}
 
 
-def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed, zone="UTC"):
+def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed, zone="UTC", time_order=False):
     """The last timed window's per-node lists against each sampled node's own
     filter over every rule (node.go:121-158 -> Job.Cmds) composed with the
     oracle's Next loop (checker only; outside the timed region)."""
@@ -631,6 +640,9 @@ def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed, zon
     for k, n in enumerate(nodes):
         pos = np.searchsorted(union, rules[roff[k]:roff[k + 1]])
         exp_t, exp_p = O.node_list(eo, et, pos)
+        if time_order:  # (time, rule) order: pos ascends with the rule index
+            o = np.lexsort((exp_p, exp_t))
+            exp_t, exp_p = exp_t[o], exp_p[o]
         got_t, got_r = eng.node_copy_range(node_off[n], node_off[n + 1] - node_off[n])
         ev += len(exp_t)
         bad += not (np.array_equal(got_t, exp_t) and np.array_equal(got_r, union[exp_p]))

@@ -74,8 +74,9 @@ struct cg_ctx {
   // ms: [0..5] expansion phases (count, scan, map, write_cf, write_walk,
   // offsets), [6..8] per-node phases (rule->node join, transpose + per-node
   // offsets, k_node_write) of the last per-node call, [9..11] dispatcher
-  // wake (scan, due compaction, advance) of the last cg_dispatcher_fire
-  float kt[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // wake (scan, due compaction, advance) of the last cg_dispatcher_fire, [12]
+  // the time-order pass of the last cg_node_result_order_by_time
+  float kt[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   // expansion phase timing: 2 = an event between every phase (kt[0..5]);
   // 1 = events around k_write_cf only (kt[3]; the others read -1).  Each
   // event recorded between two kernels costs 6-12 us of idle GPU on this
@@ -109,6 +110,11 @@ struct cg_ctx {
   DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule, rs_hist;
   DBuf<int32_t> seg_nrec, rec_rule, rec_dst, rec_dlt;  // per-call segment records
   DBuf<uint32_t> pn_tickets;
+  // time-order pass (cg_node_order.hip): node-aligned tiles, per-pass
+  // histograms/offsets, and the second buffers of the ping-pong
+  DBuf<int32_t> ts_cnt, ts_tile_node, ts_hist, node_rule2;
+  DBuf<int64_t> ts_base, ts_off, node_time2;
+  int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
   int64_t* pn_res_host = nullptr;  // mapped pinned: per-node event total of the last call
@@ -134,6 +140,8 @@ struct cg_ctx {
     pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();
     rs_hist.release(); pn_tickets.release(); rules.release();
     seg_nrec.release(); rec_rule.release(); rec_dst.release(); rec_dlt.release();
+    ts_cnt.release(); ts_tile_node.release(); ts_hist.release(); node_rule2.release();
+    ts_base.release(); ts_off.release(); node_time2.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);
     pn_res_host = nullptr;
     pn_res_dev = nullptr;

@@ -377,16 +377,17 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 // Per-node lists, one (node, band) segment per wave task, tasks taken by
 // ticket in band-major order (every node's segment of band 0, then band 1, ...)
 // so the band's rule-major fire lists are read from L2 by all of them.  A
-// wave walks its segment's pairs 64 at a time: lane i loads pair i's rule,
-// the rule's fire-list start and count (rule-major offsets), a wave prefix
-// sum places the pairs, and the non-empty ones are compacted into lanes
-// 0..nc-1 (ds_permute).  The output is filled in aligned 64-event blocks:
-//   - inside one pair: one uniform shift, a coalesced 512-B gather;
-//   - across pairs: each pair starting in the block marks its first lane in a
-//     per-wave LDS row (tagged, no clearing), a ballot of the marks gives the
-//     start mask M, and lane l's pair is prev + popcount(M & lanes <= l).
-// A block shared with the next window of the same segment is carried in
-// registers; only blocks at segment edges are stored partially.
+// wave reads its segment's pair records (k_seg_records: rule, first position,
+// band-relative list index) 64 at a time, lane i holding record i, the next
+// chunk in flight.  The output is filled in aligned 64-event blocks, a batch
+// of kNodeBatch blocks at a time, each block placed on its own: the records
+// starting in it mark their first lane in the block's LDS row (tagged, no
+// clearing); lane l's record = (records starting before the block, one
+// ballot over the sorted starts) - 1 + popcount(marks at lanes <= l); its
+// list index and rule come from that record's lane (ds_bpermute).  The
+// batch's gathers are issued together, then its stores.  A block shared with
+// the next chunk of the same segment is carried in registers; only blocks at
+// segment edges are stored partially.
 // V (diagnostic build only): 1 = no gather (synthetic values), 2 = no stores,
 // 4 = no per-block placement (stores of zeros), 8 = no rule-index stores.
 #ifndef CG_NODE_BATCH
@@ -394,9 +395,6 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 #endif
 constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
 constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 node-major
-#ifndef CG_NODE_FAST
-#define CG_NODE_FAST 0  // 1: blocks inside one pair skip the mark/ballot placement (A/B: ~2% slower)
-#endif
 
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
@@ -406,10 +404,12 @@ __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times, int32_t N, int32_t K,
     int32_t B, int64_t cap, uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time,
     int32_t* __restrict__ out_rule, int node_major) {
-  __shared__ uint32_t marks_all[4][128];  // slots 64..127: the writes of lanes that mark nothing
+  // per wave, one 128-slot row per block of a batch (slots 64..127: the
+  // writes of lanes that mark nothing); tags only grow, so no clearing
+  __shared__ uint32_t marks_all[4][kNodeBatch * 128];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* marks = marks_all[wave];
-  marks[lane] = 0u;
+  for (int u = 0; u < kNodeBatch; u++) marks[u * 128 + lane] = 0u;
   uint32_t tag = 0;
   const int64_t NK = int64_t(N) * K;
   if (seg_pos[NK] > cap) return;  // output too small: the host grows it and relaunches
@@ -472,11 +472,25 @@ __global__ __launch_bounds__(256) void k_node_write(
       const int nc = nrec - w < 64 ? nrec - w : 64;
       const int32_t qw = __builtin_amdgcn_readlane(dst, 0);
       if (w + 64 < nrec) fetch(w + 64);
-      int cprev = -1;  // record holding q = b - 1 (-1: before this chunk)
-      // blocks in batches: every block's lanes are placed first (LDS and
-      // cross-lane work, no divergent branches), then the batch's gathers are
-      // issued together, then stored
+      const bool live = lane < nc;
+      // blocks in batches, each placed on its own: the records starting in
+      // block u mark their first lane in LDS row u (the others write a slot of
+      // their own past 64), one wave barrier for the batch; lane l's record =
+      // (records starting before the block: a ballot, the records are sorted)
+      // - 1 + (marks at lanes <= l).  No block waits on the one before it.
       for (int32_t bq = qw & ~63; bq < we; bq += 64 * kNodeBatch) {
+        tag++;
+        if (!(V & 4)) {
+#pragma unroll
+          for (int u = 0; u < kNodeBatch; u++) {
+            const int32_t b = bq + 64 * u;
+            const bool mark = live && dst >= b && dst < b + 64;
+            marks[u * 128 + (mark ? dst - b : 64 + lane)] = tag;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         int32_t gi[kNodeBatch];  // band index of this lane's fire (-1: none here)
         int32_t rvs[kNodeBatch];
 #pragma unroll
@@ -486,33 +500,13 @@ __global__ __launch_bounds__(256) void k_node_write(
           rvs[u] = 0;
           if (b >= we || (V & 4)) continue;
           const int32_t q = b + lane;
-#if CG_NODE_FAST
-          int cb = cprev;  // the record holding q = b, when b lies in this chunk
-          if (b >= qw && cprev + 1 < nc && __builtin_amdgcn_readlane(dst, cprev + 1) == b) cb = cprev + 1;
-          const int32_t cb_end = cb >= 0 ? (cb + 1 < nc ? __builtin_amdgcn_readlane(dst, cb + 1) : we) : 0;
-          if (b >= qw && cb >= 0 && cb_end >= b + 64) {  // inside one pair
-            gi[u] = q + __builtin_amdgcn_readlane(dlt, cb);
-            rvs[u] = __builtin_amdgcn_readlane(rr, cb);
-            cprev = cb;
-            continue;
-          }
-#endif
-          // the records starting in this block mark their first lane (the
-          // others write a slot of their own past 64); lane l's record = prev +
-          // marks at <= l
-          tag++;
-          const bool mark = lane < nc && dst >= b && dst < b + 64;
-          marks[mark ? dst - b : 64 + lane] = tag;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          const uint64_t M = __ballot(marks[lane] == tag);
-          int own = cprev + __popcll(M & le);
+          const uint64_t M = __ballot(marks[u * 128 + lane] == tag);
+          const int before = __popcll(__ballot(live && dst < b));
+          int own = before - 1 + __popcll(M & le);
           own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
           const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
           rvs[u] = __builtin_amdgcn_ds_bpermute(own << 2, rr);
           gi[u] = (q >= qw && q < we) ? q + dl : -1;
-          cprev = __builtin_amdgcn_readlane(own, 63);
         }
         int64_t vals[kNodeBatch];
 #pragma unroll
@@ -830,6 +824,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_E = En;
   c->pn_nnz = nnz;
   c->pn_N = N;
+  c->pn_t0 = t0;
+  c->pn_t1 = t1;
   c->pn_cache_serial = in.serial;
   c->pn_cache_mode = mode;
   *n_events = En;

@@ -432,6 +432,15 @@ class Engine:
                                               rule.ctypes.data))
         return time[:count], rule[:count]
 
+    def node_order_by_time(self):
+        """Reorder every node's list of the last per-node result by (time,
+        rule) in device memory (cg_node_result_order_by_time; the byTime order
+        of Cron.run, cron.go:64-79,220).  Returns the pass's ms."""
+        check(lib().cg_node_result_order_by_time(self._h))
+        buf = (C.c_float * 13)()
+        lib().cg_last_kernel_times(self._h, buf, 13)
+        return buf[12]
+
     def node_counts_to_device(self, d_ptr):
         check(lib().cg_node_counts_to_device(self._h, C.c_void_p(d_ptr)))
 

@@ -349,6 +349,13 @@ int cg_expand_per_node_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone*
 /* device pointers of the last per-node result */
 int cg_node_result_device(cg_ctx* ctx, const int64_t** d_node_off, const int64_t** d_time,
                           const int32_t** d_rule, int64_t* n_events);
+/* Reorder every node's list of the last per-node result by (time, rule), in
+ * device memory: the order the node's scheduler keeps its entries in
+ * (Cron.run's sort.Sort(byTime), node/cron/cron.go:64-79,220; equal times in
+ * ascending rule order, one of the orders that unstable sort may give).
+ * Later cg_node_result_* calls see the ordered lists; the node offsets are
+ * unchanged.  Time of the pass: cg_last_kernel_times [12]. */
+int cg_node_result_order_by_time(cg_ctx* ctx);
 /* copy the last per-node result to host buffers (node_off [N+1]; time/rule
  * [n_events], cap = their capacity); any pointer may be NULL */
 int cg_node_result_copy(cg_ctx* ctx, int64_t* node_off, int64_t* time, int32_t* rule, int64_t cap);

@@ -141,3 +141,38 @@ def test_transpose_cache_keyed_by_rule_set_and_mode(eng):
         assert all(np.array_equal(x, y) for x, y in zip(got, exp)), (name, mode, w)
         if w == 1:  # the host-array path in between re-uploads its own rule set
             eng.expand_per_node(sps[name], None, a, a + 3600, rin, mode)
+
+
+@pytest.mark.parametrize("zone,t0,hours", [("UTC", synth.T0_2026 + 64 * DAY, 1), ("UTC", synth.T0_2026, 25),
+                                           ("America/New_York", 1772953200 - 12 * 3600, 24)])
+def test_per_node_time_ordered_vs_oracle(eng, zone, t0, hours):
+    """cg_node_result_order_by_time: every node's list in (time, rule) order
+    -- the byTime order of Cron.run (cron.go:64-79,220) with equal times in
+    rule order -- from the oracle's per-node lists, for 2 and 3 radix passes
+    (1 h: 12-bit time offsets; 24-25 h: 17 bits); node offsets unchanged."""
+    rin = synth.multi_rule_jobs(300, seed=23)
+    specs = synth.spec_mix(rin.n_rules, seed=6, mix=synth.MIX_CONFIG2)
+    scheds = [cron.Parse(s) for s in specs]
+    t1 = t0 + hours * 3600
+    node_off, time, rule = eng.expand_per_node(scheds, product_zone(zone), t0, t1, rin, _lib.EXCLUDE_NONE)
+    ms = eng.node_order_by_time()
+    assert ms >= 0
+    off2, time2, rule2 = eng.node_result(rin.n_nodes, len(time))
+    assert np.array_equal(off2, node_off)
+    arr = O.sched_array(oracle_parse_all(specs))
+    eo, et = O.expand_batch(arr, t0, t1, oracle_zone(zone))
+    rn = oracle_rule_nodes(rin, _lib.EXCLUDE_NONE)
+    per_node = [[] for _ in range(rin.n_nodes)]
+    for r in range(rin.n_rules):
+        for n in rn[r]:
+            per_node[n].append(r)
+    checked = 0
+    for n in range(rin.n_nodes):
+        exp_t, exp_r = O.node_list(eo, et, per_node[n]) if per_node[n] else (np.zeros(0, np.int64),
+                                                                            np.zeros(0, np.int32))
+        order = np.lexsort((exp_r, exp_t))
+        a, b = node_off[n], node_off[n + 1]
+        assert np.array_equal(time2[a:b], exp_t[order]), n
+        assert np.array_equal(rule2[a:b], exp_r[order]), n
+        checked += b - a
+    assert checked == len(time) > 1000
