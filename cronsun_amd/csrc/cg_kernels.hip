@@ -896,15 +896,17 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
     __syncwarp();
   };
   // Slices are handed out dynamically (the cost per slice varies with the
-  // spec mix; a static split leaves a long tail).  One ticket counter per
-  // XCD-sized group of blocks (blocks go round-robin over the 8 XCDs): group x
-  // owns slices x, x + ng, x + 2 ng, ..., so the counters' atomics spread over
-  // 8 addresses.  Tickets are taken one slice ahead so the atomic's latency
+  // spec mix; a static split leaves a long tail).  kTicketGroups counters,
+  // 128 B apart, one per group of blocks (blocks go round-robin over the
+  // groups): group g's counter hands out slices g, g + ng, g + 2 ng, ..., so
+  // the atomics spread over ng addresses.  A wave whose group has run out
+  // moves on to the next group's counter (no group's tail waits on its own
+  // waves alone).  Tickets are taken one slice ahead so the atomic's latency
   // hides under the current slice.
   const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
   const int grp = int(blockIdx.x % unsigned(ng));
-  unsigned int* ticket =
-      reinterpret_cast<unsigned int*>(chunk_run + (cap >> sh) + 2) + grp * kTicketStride;
+  unsigned int* tickets = reinterpret_cast<unsigned int*>(chunk_run + (cap >> sh) + 2);
+  int cur = grp, hops = 0;  // the group whose slices this wave takes, groups left behind
   int64_t static_next = int64_t(blockIdx.x) * kWriteWaves + wave;
   auto take = [&]() -> int64_t {
     if (V & 16) {  // diagnostic: static grid-stride split
@@ -912,9 +914,13 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       static_next += int64_t(gridDim.x) * kWriteWaves;
       return t;
     }
-    unsigned int t = 0;
-    if (lane == 0) t = atomicAdd(ticket, 1u);
-    return grp + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
+    for (;;) {
+      unsigned int t = 0;
+      if (lane == 0) t = atomicAdd(tickets + cur * kTicketStride, 1u);
+      const int64_t c = cur + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
+      if (c < nsup || ++hops >= ng) return c;
+      cur = cur + 1 == ng ? 0 : cur + 1;
+    }
   };
   // V & 32 (diagnostic): per-phase shader-clock totals and counts
   uint64_t st_win = 0, st_long = 0, st_all = 0, n_win = 0, n_long = 0, st_mix = 0, n_mix = 0;
@@ -1235,11 +1241,14 @@ void launch_dispatch_min(const int64_t* next, int64_t n, DispatchState* st, hipS
   hipLaunchKernelGGL(k_dispatch_min, dim3(grid_for(n, 256 * 8, 1024)), dim3(256), 0, s, next, n, st);
 }
 
+#ifndef CG_COUNT_MAX_BLOCKS
+#define CG_COUNT_MAX_BLOCKS 4096  // k_count grid cap (rules beyond it loop grid-stride)
+#endif
 void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run_anchor,
                   int32_t* run_count, uint32_t* run_dmask, unsigned long long* stuck_rule,
                   hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(k_count, dim3(grid_for(R, 256, 256 * 16)), dim3(256), plan_lds_bytes(p), st,
+  hipLaunchKernelGGL(k_count, dim3(grid_for(R, 256, CG_COUNT_MAX_BLOCKS)), dim3(256), plan_lds_bytes(p), st,
                      specs, R, p, run_anchor, run_count, run_dmask, stuck_rule);
 }
 

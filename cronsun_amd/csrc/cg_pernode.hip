@@ -394,6 +394,21 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 #define CG_NODE_BATCH 4
 #endif
 constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
+#ifndef CG_NODE_STORE_SC1
+#define CG_NODE_STORE_SC1 1
+#endif
+// Output stores.  Plain stores keep the written line in the XCD's L2, so the
+// 10 GB write stream keeps evicting the band's rule-major times that the
+// gathers want from L2; relaxed agent-scope atomic stores are plain vector
+// stores with sc1, which leave L2 (MI355X_MICROARCH.md: stores of each flavour).
+template <class T>
+__device__ __forceinline__ void out_store(T* p, T v) {
+#if CG_NODE_STORE_SC1
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
 constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 node-major
 
 template <int V>
@@ -478,7 +493,7 @@ __global__ __launch_bounds__(256) void k_node_write(
       // their own past 64), one wave barrier for the batch; lane l's record =
       // (records starting before the block: a ballot, the records are sorted)
       // - 1 + (marks at lanes <= l).  No block waits on the one before it.
-      for (int32_t bq = qw & ~63; bq < we; bq += 64 * kNodeBatch) {
+      auto place = [&](int32_t bq, int32_t (&gi)[kNodeBatch], int32_t (&rvs)[kNodeBatch]) {
         tag++;
         if (!(V & 4)) {
 #pragma unroll
@@ -491,12 +506,10 @@ __global__ __launch_bounds__(256) void k_node_write(
           __builtin_amdgcn_wave_barrier();
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
-        int32_t gi[kNodeBatch];  // band index of this lane's fire (-1: none here)
-        int32_t rvs[kNodeBatch];
 #pragma unroll
         for (int u = 0; u < kNodeBatch; u++) {
           const int32_t b = bq + 64 * u;
-          gi[u] = -1;
+          gi[u] = -1;  // band index of this lane's fire (-1: none here)
           rvs[u] = 0;
           if (b >= we || (V & 4)) continue;
           const int32_t q = b + lane;
@@ -508,18 +521,19 @@ __global__ __launch_bounds__(256) void k_node_write(
           rvs[u] = __builtin_amdgcn_ds_bpermute(own << 2, rr);
           gi[u] = (q >= qw && q < we) ? q + dl : -1;
         }
-        int64_t vals[kNodeBatch];
+      };
+      auto gather = [&](const int32_t (&gi)[kNodeBatch], int64_t (&vals)[kNodeBatch]) {
 #pragma unroll
-        for (int u = 0; u < kNodeBatch; u++) {
-          const int64_t v = (V & 1) ? int64_t(gi[u]) : tb[gi[u] < 0 ? 0 : gi[u]];
-          vals[u] = gi[u] < 0 ? 0 : v;
-        }
+        for (int u = 0; u < kNodeBatch; u++) vals[u] = (V & 1) ? int64_t(gi[u]) : tb[gi[u] < 0 ? 0 : gi[u]];
+      };
+      auto store = [&](int32_t bq, const int32_t (&gi)[kNodeBatch], const int64_t (&vals)[kNodeBatch],
+                       const int32_t (&rvs)[kNodeBatch]) {
 #pragma unroll
         for (int u = 0; u < kNodeBatch; u++) {
           const int32_t b = bq + 64 * u;
           if (b >= we) break;
           const int32_t q = b + lane;
-          int64_t val = vals[u];
+          int64_t val = gi[u] < 0 ? 0 : vals[u];
           int32_t rv = rvs[u];
           if (b == pq) {  // lanes of the previous chunk
             val = q < qw ? ptime : val;
@@ -529,11 +543,11 @@ __global__ __launch_bounds__(256) void k_node_write(
             if (V & 2) {
               asm volatile("" ::"v"(val), "v"(rv));
             } else if (b >= q_lo && b + 64 <= q_hi) {  // interior block: whole stores
-              ot[q] = val;
-              if (!(V & 8)) orl[q] = rv;
+              out_store(ot + q, val);
+              if (!(V & 8)) out_store(orl + q, rv);
             } else if (q >= q_lo && q < q_hi) {  // a segment edge
-              ot[q] = val;
-              if (!(V & 8)) orl[q] = rv;
+              out_store(ot + q, val);
+              if (!(V & 8)) out_store(orl + q, rv);
             }
             pq = -1;
           } else {
@@ -542,9 +556,43 @@ __global__ __launch_bounds__(256) void k_node_write(
             prule = rv;
           }
         }
+      };
+      // Software-pipelined over two register sets: batch k + 1 is placed and
+      // its gathers issued before batch k's stores.  Vector-memory returns are
+      // counted in issue order, so waiting for gathers issued after a batch of
+      // stores would also wait for those stores' write acknowledgements.
+      constexpr int32_t kStep = 64 * kNodeBatch;
+      int32_t giA[kNodeBatch], rvA[kNodeBatch], giB[kNodeBatch], rvB[kNodeBatch];
+      int64_t vA[kNodeBatch], vB[kNodeBatch];
+      int32_t bq = qw & ~63;
+      place(bq, giA, rvA);
+      gather(giA, vA);
+      for (;;) {
+        if (bq + kStep < we) {
+          place(bq + kStep, giB, rvB);
+          gather(giB, vB);
+        }
+        store(bq, giA, vA, rvA);
+        bq += kStep;
+        if (bq >= we) break;
+        if (bq + kStep < we) {
+          place(bq + kStep, giA, rvA);
+          gather(giA, vA);
+        }
+        store(bq, giB, vB, rvB);
+        bq += kStep;
+        if (bq >= we) break;
       }
     }
   }
+}
+
+// persistent k_node_write grid: as many 4-wave blocks per CU as its register
+// and LDS use let run at once (no block of the grid waits for a slot)
+int node_write_blocks_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_node_write<0>, 256, 0) != hipSuccess || n < 1) n = 4;
+  return std::min(n, 8);
 }
 
 int gridn(int64_t n, int threads, int cap) {
@@ -775,14 +823,15 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   }();
   static const int per_cu = [] {  // persistent grid: blocks of 4 waves per CU
     const char* e = getenv("CG_NODE_BLOCKS_PER_CU");
-    return e ? std::max(1, atoi(e)) : 8;
+    return e ? std::max(1, atoi(e)) : node_write_blocks_per_cu();
   }();
   static const int node_major = [] {  // writer task order (see k_node_write)
     const char* e = getenv("CG_NODE_ORDER");
     return e ? atoi(e) : kNodeMajorDefault;
   }();
 #else
-  constexpr int variant = 0, per_cu = 8, node_major = kNodeMajorDefault;
+  constexpr int variant = 0, node_major = kNodeMajorDefault;
+  static const int per_cu = node_write_blocks_per_cu();
 #endif
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
   int64_t En = 0;

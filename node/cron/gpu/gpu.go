@@ -306,8 +306,10 @@ func (j *Jobset) Schedules() []cron.Schedule { return j.scheds }
 // ExpandPerNode is every node's loadJobs -> Job.Cmds filter
 // (node/node.go:121-158, job.go:591-614) plus its Cron entries' Next loop over
 // (t0, t1], for all nodes at once: node ID -> (rule, time) events, rule-major
-// inside a node (rules ascending, times ascending within a rule).
-func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, mode int) (map[string][]Fire, error) {
+// inside a node (rules ascending, times ascending within a rule), or with
+// byTime set in the order a node's Cron keeps its entries (sort.Sort(byTime),
+// cron.go:64-79: times ascending, equal times in rule order).
+func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, mode int, byTime bool) (map[string][]Fire, error) {
 	var rin C.cg_rules_in
 	if rc := C.cg_jobset_rules(j.js, &rin); rc != 0 {
 		return nil, lastErr(rc)
@@ -321,6 +323,11 @@ func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, 
 	if rc := C.cg_expand_per_node(e.ctx, sp.s, z.z, C.int64_t(t0.Unix()), C.int64_t(t1.Unix()), &rin,
 		C.int(mode), &out); rc != 0 {
 		return nil, lastErr(rc)
+	}
+	if byTime {
+		if rc := C.cg_node_result_order_by_time(e.ctx); rc != 0 {
+			return nil, lastErr(rc)
+		}
 	}
 	tm, rl := make([]int64, int64(out.n_events)), make([]int32, int64(out.n_events))
 	if len(tm) > 0 {

@@ -220,6 +220,14 @@ int main(int argc, char** argv) {
     for (int64_t k = node_off[n]; k < node_off[n + 1]; k++) printf(" %d:%lld", nr[k], (long long)nt[k]);
     printf("\n");
   }
+  /* the same lists in the node scheduler's byTime order (cron.go:64-79) */
+  CHECK(cg_node_result_order_by_time(ctx));
+  CHECK(cg_node_result_copy(ctx, NULL, nt, nr, nc.n_events));
+  for (int n = 0; n < rules.n_nodes; n++) {
+    printf("O %s", cg_jobset_node_id(js, n));
+    for (int64_t k = node_off[n]; k < node_off[n + 1]; k++) printf(" %d:%lld", nr[k], (long long)nt[k]);
+    printf("\n");
+  }
   free(nt);
   free(nr);
 
