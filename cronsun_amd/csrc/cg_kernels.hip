@@ -899,14 +899,18 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   // spec mix; a static split leaves a long tail).  kTicketGroups counters,
   // 128 B apart, one per group of blocks (blocks go round-robin over the
   // groups): group g's counter hands out slices g, g + ng, g + 2 ng, ..., so
-  // the atomics spread over ng addresses.  A wave whose group has run out
-  // moves on to the next group's counter (no group's tail waits on its own
-  // waves alone).  Tickets are taken one slice ahead so the atomic's latency
+  // the atomics spread over ng addresses.  With large slices a wave whose
+  // group has run out moves on to the next group's counter (no group's tail
+  // waits on its own waves alone).  Tickets are taken one slice ahead so the atomic's latency
   // hides under the current slice.
   const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
   const int grp = int(blockIdx.x % unsigned(ng));
   unsigned int* tickets = reinterpret_cast<unsigned int*>(chunk_run + (cap >> sh) + 2);
   int cur = grp, hops = 0;  // the group whose slices this wave takes, groups left behind
+  // (same-box A/B, profiles/r02_ab_steal.json: config 4 with 16384-event
+  // slices 23.7 vs 24.5 ms; config 2 with 2048-event slices 1.03 vs 0.99 ms:
+  // moving on only pays with the large slices)
+  const bool steal = sh == CG_SUPER_SHIFT_LARGE;
   int64_t static_next = int64_t(blockIdx.x) * kWriteWaves + wave;
   auto take = [&]() -> int64_t {
     if (V & 16) {  // diagnostic: static grid-stride split
@@ -918,7 +922,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       unsigned int t = 0;
       if (lane == 0) t = atomicAdd(tickets + cur * kTicketStride, 1u);
       const int64_t c = cur + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
-      if (c < nsup || ++hops >= ng) return c;
+      if (c < nsup || !steal || ++hops >= ng) return c;
       cur = cur + 1 == ng ? 0 : cur + 1;
     }
   };
