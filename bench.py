@@ -94,6 +94,12 @@ def main():
     ap.add_argument("--gather-node-csr", action="store_true",
                     help="pernode/config3 at N > 1: every step also gathers the whole per-node CSR on "
                          "rank 0 (shard.gather_node_csr; timed)")
+    ap.add_argument("--sync", action="store_true",
+                    help="config2/config4: synchronous steps (cg_expand_device: every step ends with a "
+                         "stream sync) instead of the pipelined cg_expand_device_async")
+    ap.add_argument("--tick", type=int, default=0,
+                    help="config2/config4: advance T0 (and T1) by this many seconds every step, as a "
+                         "scheduler's consecutive windows (0 = the same window every step)")
     ap.add_argument("--time-order", action="store_true",
                     help="pernode/config3: every window's per-node lists are also reordered by (time, "
                          "rule) on the device (cg_node_result_order_by_time; timed)")
@@ -293,9 +299,27 @@ def main():
                     shard.node_offsets(node_counts.to(cdev), dist)
             last.update(nnz=nnz, kt=kt_sum, nkt=nkt_sum, windows=len(range(t0, t1, W)))
             return En
-        E = eng.expand_device(sp, utc, t0, t1)
+        off_t = args.tick * last.get("step_no", 0)
+        last["step_no"] = last.get("step_no", 0) + 1
+        last["window"] = (t0 + off_t, t1 + off_t)
+        if pipelined:
+            # enqueued; the pipeline's results and errors come with expand_wait
+            eng.expand_async(sp, utc, t0 + off_t, t1 + off_t)
+            return None
+        E = eng.expand_device(sp, utc, t0 + off_t, t1 + off_t)
         if world > 1:
             # global CSR offsets of the job-ID-range shards (RCCL allgather)
+            mine = torch.tensor([E], dtype=torch.int64, device=cdev)
+            dist.all_gather_into_tensor(tot, mine)
+        return E
+
+    def finish():
+        """End of a run of steps: drain the pipeline (pipelined mode); at N > 1
+        one allgather of the ranks' totals gives the shards' global offsets."""
+        if not pipelined:
+            return None
+        E = eng.expand_wait()
+        if world > 1:
             mine = torch.tensor([E], dtype=torch.int64, device=cdev)
             dist.all_gather_into_tensor(tot, mine)
         return E
@@ -304,11 +328,16 @@ def main():
     # between every phase leaves the GPU idle for several us per event.  The
     # other phases are timed afterwards, outside the timed region.
     lean = not pn and wl != "dispatch"
+    pipelined = lean and not args.sync
     if lean:
         eng.set_phase_timing(1)
+    if pipelined:  # a synchronous call sizes the output for the pipelined ones
+        eng.expand_device(sp, utc, t0, t1 + args.tick * (args.warmup + args.steps + 8))
     for _ in range(args.warmup):
         E = step()
-    log(f"[rank {rank}] warmup done: {E} events/step")
+    if pipelined:
+        E = finish()
+    log(f"[rank {rank}] warmup done: {E} events/step ({'pipelined' if pipelined else 'synchronous'} steps)")
     if not pn and wl != "dispatch":
         _, d_times, _ = eng.result_device()
         log(f"[rank {rank}] times buffer at {d_times:#x} ({d_times % (1 << 21):#x} past a 2 MiB boundary)")
@@ -338,9 +367,13 @@ def main():
         if pn:
             kts.append(last["kt"])
             nkts.append(last["nkt"])
-        else:
+        elif not pipelined:
             kts.append(eng.kernel_times())
             nkts.append(eng.dispatch_kernel_times() if wl == "dispatch" else eng.node_kernel_times())
+    if pipelined:  # inside the timed region: every step's work is done and checked
+        E = finish()
+        kts.append(eng.kernel_times())  # [3] = mean k_write_cf time of the timed steps
+        nkts.append(eng.node_kernel_times())
     t_loop = time.perf_counter() - start
     torch.cuda.synchronize()
     barrier()
@@ -361,7 +394,8 @@ def main():
                                      max(2, args.verify_sample // 250), seed=0x5EED + 77 + rank,
                                      zone=args.zone, time_order=args.time_order)
         else:
-            verify = verify_rule_major(eng, spec_of, R, t0, t1, E, args.verify_sample,
+            wa, wb = last.get("window", (t0, t1))  # the last timed step's window
+            verify = verify_rule_major(eng, spec_of, R, wa, wb, E, args.verify_sample,
                                        seed=0x5EED + 99 + rank, zone=args.zone)
         verify["seconds"] = time.perf_counter() - tv
         verify["unwritten_after_poison"] = unwritten
@@ -376,8 +410,8 @@ def main():
         # per-phase breakdown of a few untimed steps (events between phases)
         eng.set_phase_timing(2)
         phases = []
-        for _ in range(3):
-            step()
+        for _ in range(3):  # synchronous calls: one per step, events between all phases
+            eng.expand_device(sp, utc, t0, t1)
             phases.append(eng.kernel_times())
         eng.set_phase_timing(1)
         ph = np.mean(np.array(phases), axis=0)
@@ -408,13 +442,19 @@ def main():
         sp2.free()
         del host_times, host_off
 
+    step_events = E * args.steps
+    if args.tick and not pn and wl != "dispatch":
+        # moving windows: every timed step's own total, counted afterwards
+        # (outside the timed region) with the count pass alone
+        step_events = sum(int(eng.count(sp, utc, t0 + args.tick * i, t1 + args.tick * i).sum())
+                          for i in range(args.warmup, args.warmup + args.steps))
     el = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-    ev = torch.tensor([E], dtype=torch.int64, device=cdev)
+    ev = torch.tensor([step_events], dtype=torch.int64, device=cdev)
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(ev, op=dist.ReduceOp.SUM)
     elapsed = float(el.item())
-    total_events = int(ev.item())
+    total_events = int(ev.item())  # events of all timed steps, all ranks
 
     kt = np.mean(np.array(kts), axis=0)    # count, scan, map, write_cf, write_walk, offsets (ms)
     nkt = np.mean(np.array(nkts), axis=0)  # join, transpose, node write (ms)
@@ -462,7 +502,7 @@ def main():
 
     out = {
         "metric": metric,
-        "value": total_events * args.steps / elapsed,
+        "value": total_events / elapsed,
         "unit": "events/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -478,12 +518,16 @@ def main():
             "rules_per_gpu": R,
             "horizon_s": H,
             "t0": t0,
+            "tick_s": args.tick,
             "zone": args.zone,
             "events_per_gpu_step": E,
             "shard": shard_info or {"lo": 0, "hi": R},
             "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard totals / per-node counts)",
         },
         "hbm_gbps_step": algo_bytes * world / (elapsed / args.steps) / 1e9,
+        "steps_mode": ("pipelined (cg_expand_device_async: count/scan of a step overlap the previous "
+                       "step's write; one cg_expand_wait at the end of the timed steps)" if pipelined else
+                       "synchronous (one call and stream sync per step)") if lean else "synchronous",
         "kernel_ms": {"count": kt[0], "scan": kt[1], "block_map": kt[2], "write_cf": kt[3],
                       "write_walk": kt[4], "offsets": kt[5],
                       "timing": "write_cf: HIP events around it in the timed steps; the other "

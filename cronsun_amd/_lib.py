@@ -125,6 +125,8 @@ def _declare(L):
         "cg_expand": ([vp, vp, vp, i64, i64, P(cg_csr)], C.c_int),
         "cg_count": ([vp, vp, vp, i64, i64, vp, P(i64)], C.c_int),
         "cg_expand_device": ([vp, vp, vp, i64, i64, P(i64)], C.c_int),
+        "cg_expand_device_async": ([vp, vp, vp, i64, i64], C.c_int),
+        "cg_expand_wait": ([vp, P(i64)], C.c_int),
         "cg_result_device": ([vp, P(vp), P(vp), P(i64)], C.c_int),
         "cg_result_copy_times": ([vp, i64, i64, vp], C.c_int),
         "cg_result_copy_offsets": ([vp, vp], C.c_int),

@@ -145,6 +145,7 @@ void cg_destroy(cg_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->st);
+  if (c->st_cs) (void)hipStreamSynchronize(c->st_cs);
   c->free_all();
   for (auto& e : c->ev) (void)hipEventDestroy(e);
   for (auto& e : c->pev) (void)hipEventDestroy(e);
@@ -268,39 +269,38 @@ void cg_specs_free(cg_specs* s) {
 }  // extern "C"
 
 // ----------------------------------------------------------- plan upload
-int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* pa) {
-  const int32_t zn = int32_t(plan.table.when.size());
+// one packed upload: when | off | segs | dtab
+PlanLayout plan_layout(const Plan& plan) {
+  PlanLayout L;
+  const size_t zn = plan.table.when.size(), G = plan.segs.size(), nd = plan.dtab.size();
+  L.o_when = 0;
+  L.o_off = L.o_when + zn * 8;
+  L.o_seg = (L.o_off + zn * 4 + 15) / 16 * 16;
+  L.o_dt = L.o_seg + G * sizeof(Segment);
+  L.bytes = L.o_dt + nd * 4 + 16;
+  return L;
+}
+
+void plan_pack(const Plan& plan, const PlanLayout& L, char* h) {
+  std::memset(h, 0, L.bytes);
+  std::memcpy(h + L.o_when, plan.table.when.data(), plan.table.when.size() * 8);
+  std::memcpy(h + L.o_off, plan.table.off.data(), plan.table.off.size() * 4);
+  if (!plan.segs.empty()) std::memcpy(h + L.o_seg, plan.segs.data(), plan.segs.size() * sizeof(Segment));
+  if (!plan.dtab.empty()) std::memcpy(h + L.o_dt, plan.dtab.data(), plan.dtab.size() * 4);
+}
+
+int plan_args(const Plan& plan, const PlanLayout& L, char* base, int64_t t0, int64_t t1, PlanArgs* pa) {
   const int32_t G = int32_t(plan.segs.size());
-  const int32_t nd = int32_t(plan.dtab.size());
   if (G > kMaxSegments)
     return cg_fail(CG_ERANGE, "plan has more than " + std::to_string(kMaxSegments) +
                                   " segments (horizon too long for this zone)");
-  // plan_dev is shared by every entry point: whatever it held is gone, so the
-  // expansion's plan cache must not be trusted after this (expand re-validates)
-  c->plan_valid = false;
-  // one packed upload: when | off | segs | dtab
-  size_t o_when = 0, o_off = o_when + size_t(zn) * 8;
-  size_t o_seg = (o_off + size_t(zn) * 4 + 15) / 16 * 16;
-  size_t o_dt = o_seg + size_t(G) * sizeof(Segment);
-  size_t bytes = o_dt + size_t(nd) * 4 + 16;
-  std::vector<char>& h = c->plan_host;
-  h.assign(bytes, 0);
-  std::memcpy(h.data() + o_when, plan.table.when.data(), size_t(zn) * 8);
-  std::memcpy(h.data() + o_off, plan.table.off.data(), size_t(zn) * 4);
-  if (G) std::memcpy(h.data() + o_seg, plan.segs.data(), size_t(G) * sizeof(Segment));
-  if (nd) std::memcpy(h.data() + o_dt, plan.dtab.data(), size_t(nd) * 4);
-  int rc = c->plan_dev.ensure(bytes);
-  if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(c->plan_dev.p, h.data(), bytes, hipMemcpyHostToDevice, c->st));
-  HIPCHK(hipStreamSynchronize(c->st));  // h is reused by the next call
-  char* base = c->plan_dev.p;
-  pa->zwhen = reinterpret_cast<const int64_t*>(base + o_when);
-  pa->zoff = reinterpret_cast<const int32_t*>(base + o_off);
-  pa->segs = reinterpret_cast<const Segment*>(base + o_seg);
-  pa->dtab = reinterpret_cast<const uint32_t*>(base + o_dt);
-  pa->zn = zn;
+  pa->zwhen = reinterpret_cast<const int64_t*>(base + L.o_when);
+  pa->zoff = reinterpret_cast<const int32_t*>(base + L.o_off);
+  pa->segs = reinterpret_cast<const Segment*>(base + L.o_seg);
+  pa->dtab = reinterpret_cast<const uint32_t*>(base + L.o_dt);
+  pa->zn = int32_t(plan.table.when.size());
   pa->G = G;
-  pa->nd = nd;
+  pa->nd = int32_t(plan.dtab.size());
   pa->dtab_global = 0;
   pa->flags = plan.flags;
   pa->t0 = t0;
@@ -311,6 +311,24 @@ int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* p
   if (plan_lds_bytes(*pa) > kPlanLdsBytes)
     return cg_fail(CG_ERANGE, "zone table too large for LDS staging (narrow the time range)");
   return CG_OK;
+}
+
+int upload_plan(cg_ctx* c, const Plan& plan, int64_t t0, int64_t t1, PlanArgs* pa) {
+  if (plan.segs.size() > size_t(kMaxSegments))
+    return cg_fail(CG_ERANGE, "plan has more than " + std::to_string(kMaxSegments) +
+                                  " segments (horizon too long for this zone)");
+  // plan_dev is shared by every entry point: whatever it held is gone, so the
+  // expansion's plan cache must not be trusted after this (expand re-validates)
+  c->plan_valid = false;
+  const PlanLayout L = plan_layout(plan);
+  std::vector<char>& h = c->plan_host;
+  h.assign(L.bytes, 0);
+  plan_pack(plan, L, h.data());
+  int rc = c->plan_dev.ensure(L.bytes);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(c->plan_dev.p, h.data(), L.bytes, hipMemcpyHostToDevice, c->st));
+  HIPCHK(hipStreamSynchronize(c->st));  // h is reused by the next call
+  return plan_args(plan, L, c->plan_dev.p, t0, t1, pa);
 }
 
 extern "C" {
@@ -398,6 +416,9 @@ int cg_lock_ttl_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int6
 static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
                        bool* empty, int64_t map_cap = 0) {
   // no readable result until this call succeeds (the accessors check last_R/E)
+  int rc0 = async_drain(c);
+  if (rc0) return rc0;
+  c->as_last = -1;
   c->last_R = 0;
   c->last_E = 0;
   HIPCHK(hipSetDevice(c->device));
@@ -596,7 +617,7 @@ int cg_expand(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_
 
 int cg_result_device(cg_ctx* c, const int64_t** d_off, const int64_t** d_times, int64_t* n) {
   if (!c) return cg_fail(CG_EINVAL, "cg_result_device: null");
-  if (d_off) *d_off = c->offsets.p;
+  if (d_off) *d_off = c->as_last >= 0 ? c->as[c->as_last].offsets.p : c->offsets.p;
   if (d_times) *d_times = c->times.p;
   if (n) *n = c->last_E;
   return CG_OK;
@@ -618,7 +639,8 @@ int cg_result_copy_offsets(cg_ctx* c, int64_t* host) {
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
-  HIPCHK(hipMemcpy(host, c->offsets.p, (c->last_R + 1) * 8, hipMemcpyDeviceToHost));
+  const int64_t* off = c->as_last >= 0 ? c->as[c->as_last].offsets.p : c->offsets.p;
+  HIPCHK(hipMemcpy(host, off, (c->last_R + 1) * 8, hipMemcpyDeviceToHost));
   return CG_OK;
 }
 

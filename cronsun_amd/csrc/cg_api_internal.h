@@ -64,6 +64,41 @@ struct RulesStore {
   }
 };
 
+// One run set of the pipelined expansion (cg_expand_device_async): what the
+// count/scan of a call writes and its writer reads, so the count/scan of call
+// k (on the ctx's second stream) can run while the writer of call k-1 does.
+struct AsyncSet {
+  DBuf<int64_t> run_anchor, run_off, offsets, block_run;
+  DBuf<int32_t> run_count;
+  DBuf<uint32_t> run_dmask;
+  DBuf<char> scan_tmp, plan_dev;
+  DBuf<unsigned long long> stuck;
+  int64_t* res_host = nullptr;  // {E, stuck rule}: mapped pinned, written by the scan
+  int64_t* res_dev = nullptr;
+  char* plan_pin = nullptr;  // pinned staging of the plan upload
+  size_t plan_pin_cap = 0;
+  cg::Plan plan;
+  cg::PlanArgs pa{};
+  bool plan_valid = false;
+  uint64_t plan_zone = 0;
+  int64_t plan_t0 = 0, plan_t1 = 0;
+  hipEvent_t written = nullptr, w0 = nullptr, w1 = nullptr;  // writer done; writer start/end
+  bool pending = false;  // a call on this set whose record has not been checked
+  bool armed = false;    // stuck flag holds ~0 (set once; every scan re-arms it)
+  int64_t R = 0, cap = 0;
+  void release() {
+    run_anchor.release(); run_off.release(); offsets.release(); block_run.release();
+    run_count.release(); run_dmask.release(); scan_tmp.release(); plan_dev.release(); stuck.release();
+    if (res_host) (void)hipHostFree(res_host);
+    if (plan_pin) (void)hipHostFree(plan_pin);
+    res_host = res_dev = nullptr;
+    plan_pin = nullptr;
+    plan_pin_cap = 0;
+    for (hipEvent_t* e : {&written, &w0, &w1})
+      if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+  }
+};
+
 struct cg_ctx {
   int device = 0;
   int write_blocks = 1024;  // persistent k_write_cf grid (set from the CU count)
@@ -104,6 +139,18 @@ struct cg_ctx {
   int64_t* res_dev = nullptr;      // res_host's device address
   int64_t last_E = 0, last_R = 0, last_G = 0;
 
+  // pipelined expansion (cg_async.cpp): two run sets used in turn, count +
+  // scan on st_cs, writers on st; as_last = set of the last async result
+  // (-1: the last result came from the synchronous path)
+  AsyncSet as[2];
+  int as_next = 0, as_last = -1;
+  hipStream_t st_cs = nullptr;
+  hipEvent_t cs_done[2] = {};
+  int async_rc = 0;  // first error of the calls since the last cg_expand_wait
+  std::string async_msg;
+  double wr_ms_sum = 0;  // writer (k_write_cf) time of the checked async calls
+  int wr_n = 0;
+
   // per-node buffers: the rule->node join (rule-major pairs), its node-major
   // transpose, the (node, rule band) segments and the node CSR
   DBuf<int64_t> rn_off, node_off, node_time, nt_off, rs_off, seg_pair, seg_cnt, seg_pos;
@@ -127,6 +174,11 @@ struct cg_ctx {
   int32_t pn_B = 0, pn_K = 0;  // rules per band, bands of the cached segment bounds (0: none)
 
   void free_all() {
+    for (AsyncSet& a : as) a.release();
+    for (hipEvent_t& e : cs_done)
+      if (e) (void)hipEventDestroy(e), e = nullptr;
+    if (st_cs) (void)hipStreamDestroy(st_cs);
+    st_cs = nullptr;
     plan_dev.release();
     run_anchor.release(); run_off.release(); offsets.release(); times.release();
     block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
@@ -168,5 +220,15 @@ struct cg_specs {
 // cg_schedule -> packed 32-byte device spec (validates @every delays)
 int pack_spec(const cg_schedule& s, cg::DSpec* d);
 int upload_plan(cg_ctx* c, const cg::Plan& plan, int64_t t0, int64_t t1, cg::PlanArgs* pa);
+struct PlanLayout {
+  size_t o_when, o_off, o_seg, o_dt, bytes;
+};
+PlanLayout plan_layout(const cg::Plan& plan);
+void plan_pack(const cg::Plan& plan, const PlanLayout& L, char* dst);
+int plan_args(const cg::Plan& plan, const PlanLayout& L, char* dev_base, int64_t t0, int64_t t1,
+              cg::PlanArgs* pa);
 int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
                          int64_t* n_events);
+// finish and check every pending cg_expand_device_async call (cg_async.cpp);
+// their errors are reported by the next cg_expand_wait
+int async_drain(cg_ctx* c);

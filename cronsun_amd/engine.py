@@ -305,6 +305,18 @@ class Engine:
                                      C.byref(n)))
         return n.value
 
+    def expand_async(self, specs, loc, t0, t1):
+        """Enqueue a pipelined expansion (cg_expand_device_async): returns at
+        once; results and errors come with expand_wait()."""
+        check(lib().cg_expand_device_async(self._h, specs._h, self._loc(loc).handle, int(t0), int(t1)))
+
+    def expand_wait(self):
+        """Wait for the async expansions since the last wait; the event total of
+        the last one (its result is then the engine's current result)."""
+        n = C.c_int64()
+        check(lib().cg_expand_wait(self._h, C.byref(n)))
+        return n.value
+
     def result_device(self):
         off, times, n = C.c_void_p(), C.c_void_p(), C.c_int64()
         check(lib().cg_result_device(self._h, C.byref(off), C.byref(times), C.byref(n)))

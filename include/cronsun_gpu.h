@@ -264,6 +264,21 @@ int cg_expand(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0, 
  * multi-GPU drivers that keep results in HBM. */
 int cg_expand_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
                      int64_t t1, int64_t* n_events);
+/* Pipelined variant for back-to-back calls (a scheduler's tick loop over
+ * consecutive windows, cron.go:212-215 per tick): enqueues the expansion and
+ * returns without waiting.  The count/scan of a call overlap the previous
+ * call's output write; each call's plan is staged without a stream sync, so
+ * T0 may move every call.  Needs the output capacity left by an earlier
+ * cg_expand_device large enough for every call's result: a call that would
+ * exceed it writes nothing and cg_expand_wait returns CG_ECAPACITY.  Results
+ * and errors are known only after cg_expand_wait, which waits for every
+ * call issued since the last wait, returns the first error among them (a
+ * rule whose reference loop never ends: CG_ERANGE, as cg_expand_device), and
+ * sets *n_events of the last call, whose result the accessors below then
+ * read.  cg_last_kernel_times [3] = the mean write time of those calls. */
+int cg_expand_device_async(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
+                           int64_t t1);
+int cg_expand_wait(cg_ctx* ctx, int64_t* n_events);
 /* device pointers of the last device-resident result */
 int cg_result_device(cg_ctx* ctx, const int64_t** d_offsets, const int64_t** d_times,
                      int64_t* n_events);

@@ -265,3 +265,56 @@ def test_config2_scale_dst_day(eng, t0):
     for k, i in enumerate(idx):
         assert np.array_equal(times[off[i]:off[i + 1]], et[eo[k]:eo[k + 1]]), specs[i]
     sp.free()
+
+
+def test_async_pipeline(eng):
+    """cg_expand_device_async / cg_expand_wait: a scheduler's consecutive
+    windows (T0 moving every call, America/New_York over the 2026
+    spring-forward) pipelined; the last call's result equals the synchronous
+    expansion of its window and the oracle; an oversized result is reported
+    as CG_ECAPACITY, a never-ending reference loop as CG_ERANGE (Pacific/Apia
+    over the skipped 2011-12-30), each at the wait."""
+    from cronsun_amd.engine import Engine
+    specs = synth.spec_mix(20_000, seed=11)
+    arr, status = cron.parse_batch(specs)
+    assert (status == 0).all()
+    e2 = Engine(0)
+    sp = e2.upload_c(arr, len(specs))
+    ny = product_zone("America/New_York")
+    t0 = 1772953200 - 30 * 3600
+    e2.expand_device(sp, ny, t0, t0 + 3 * DAY)  # sizes the output for the windows below
+    wins = [(t0 + 6 * 3600 * i, t0 + 6 * 3600 * i + DAY) for i in range(7)]
+    for a, b in wins:
+        e2.expand_async(sp, ny, a, b)
+    E = e2.expand_wait()
+    off = np.empty(len(specs) + 1, dtype=np.int64)
+    from cronsun_amd._lib import check, lib
+    check(lib().cg_result_copy_offsets(e2._h, off.ctypes.data))
+    times = e2.copy_times(0, E)
+    a, b = wins[-1]
+    E_sync = e2.expand_device(sp, ny, a, b)
+    off_s = np.empty_like(off)
+    check(lib().cg_result_copy_offsets(e2._h, off_s.ctypes.data))
+    assert E == E_sync and np.array_equal(off, off_s)
+    assert np.array_equal(times, e2.copy_times(0, E_sync))
+    idx = np.arange(0, len(specs), 7)
+    eo, et = oracle_csr([cron.Parse(specs[i]) for i in idx], "America/New_York", a, b, [specs[i] for i in idx])
+    for k, i in enumerate(idx):
+        assert np.array_equal(times[off[i]:off[i + 1]], et[eo[k]:eo[k + 1]]), specs[i]
+    # capacity: a window far larger than the output sized above
+    e2.expand_async(sp, ny, t0, t0 + 30 * DAY)
+    with pytest.raises(_lib.CgError) as err:
+        e2.expand_wait()
+    assert err.value.code == _lib.CG_ECAPACITY
+    sp.free()
+    # a rule whose reference loop never ends, among ordinary ones
+    stuck = [cron.Parse(s) for s in ["0 0 12 * * *", "0 0 9 * * Sat", "@daily"]]
+    sp2 = e2.upload(stuck)
+    apia = product_zone("Pacific/Apia")
+    e2.expand_device(sp2, apia, 1325030400 - 10 * DAY, 1325030400 - 5 * DAY)
+    e2.expand_async(sp2, apia, 1325030400 - 10 * DAY, 1325030400 - 5 * DAY)
+    e2.expand_async(sp2, apia, 1325030400, 1325030400 + 5 * DAY)
+    with pytest.raises(_lib.CgError) as err:
+        e2.expand_wait()
+    assert err.value.code == _lib.CG_ERANGE and "rule 1:" in err.value.msg
+    e2.close()
