@@ -429,7 +429,8 @@ def main():
         te = time.perf_counter()
         sp2 = eng.upload_c(arr, R)
         t_h2d = time.perf_counter() - te
-        E2 = eng.expand_device(sp2, utc, t0, t1)
+        wa, wb = last.get("window", (t0, t1))  # the last timed step's window (E events)
+        E2 = eng.expand_device(sp2, utc, wa, wb)
         t_exp = time.perf_counter() - te - t_h2d
         _check(_cglib().cg_result_copy_offsets(eng._h, host_off.data_ptr()))
         _check(_cglib().cg_result_copy_times(eng._h, 0, E2, host_times.data_ptr()))
