@@ -289,7 +289,8 @@ int cg_result_copy_offsets(cg_ctx* ctx, int64_t* host_offsets /* [R+1] */);
 /* Per-kernel device time of the last expansion (ms, HIP events on the ctx
  * stream): [0] count, [1] scan, [2] block map, [3] write (closed form),
  * [4] write (walk), [5] offsets; of the last per-node call: [6] rule->node
- * join, [7] transpose + per-node offsets, [8] per-node write; of the last
+ * join, [7] transpose (when the join is rebuilt) + segment records + per-node
+ * offsets, [8] per-node write; [12] the last time-order pass; of the last
  * dispatcher wake: [9] scan, [10] due compaction, [11] advance.  n = entries
  * written. */
 int cg_last_kernel_times(cg_ctx* ctx, float* ms, int n);
