@@ -518,8 +518,7 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
   const bool all_phases = c->phase_timing >= 2;
   // (a CF run is entered by the exact walk only after a WALK segment, or from
   // T0 when a transition lies in the 40 days before it)
-  bool has_walk = (c->plan.flags & kPlanT0Walk) != 0;
-  for (const Segment& sg : c->plan.segs) has_walk |= sg.kind != 0;
+  const bool has_walk = (c->plan.flags & (kPlanT0Walk | kPlanWalkSegs)) != 0;
   int64_t E = 0;
   unsigned long long stuck = 0;
   for (int attempt = 0; attempt < 2; attempt++) {

@@ -146,8 +146,7 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   HIPCHK(hipEventRecord(c->cs_done[k], c->st_cs));
   // the writer after the previous call's writer, once this call's scan is done
   HIPCHK(hipStreamWaitEvent(c->st, c->cs_done[k], 0));
-  bool has_walk = (a.plan.flags & kPlanT0Walk) != 0;
-  for (const Segment& sg : a.plan.segs) has_walk |= sg.kind != 0;
+  const bool has_walk = (a.plan.flags & (kPlanT0Walk | kPlanWalkSegs)) != 0;
   (void)hipEventRecord(a.w0, c->st);
   launch_write_cf(s->d, pa, a.run_anchor.p, a.run_count.p, a.run_dmask.p, a.run_off.p, nruns, a.block_run.p, cap,
                   c->times.p, c->write_blocks, c->st);

@@ -199,6 +199,10 @@ CG_HD bool past_year_limit(const ZoneView& z, int64_t t, int64_t e, int32_t e_of
   return ye > y0 + 5;
 }
 
+// kWalk = false: a plan with no WALK segment and no flags (e.g. UTC, or a
+// zone far from its transitions): every run is closed form, no exact walk is
+// reachable, and the kernel drops next_exact (and its registers).
+template <bool kWalk = true>
 CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, int G,
                       const uint32_t* dtab, int64_t t0, int64_t t1, uint32_t flags,
                       int64_t* anchor_out, int32_t* count_out, uint32_t* dmask_out) {
@@ -253,7 +257,8 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
       }
     } else if (!done) {
       const int64_t b = sg.b < t1 ? sg.b : t1;
-      int64_t e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
+      int64_t e = CG_BEYOND;
+      if constexpr (kWalk) e = pending != INT64_MIN ? pending : next_exact(sp, z, pos, t1);
       pending = INT64_MIN;
       if (e <= pos && e != CG_ZERO_TIME) e = CG_NO_PROGRESS;  // backwards: the loop cycles
       if (sg.kind == 0 && e != CG_NO_PROGRESS && e != CG_ZERO_TIME && e != CG_BEYOND &&
@@ -276,7 +281,7 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
           if (e > b) { pending = e; break; }
           cnt++;
           pos = e;
-          e = next_exact(sp, z, pos, t1);
+          if constexpr (kWalk) e = next_exact(sp, z, pos, t1);
         }
         if (cnt == 0) dm = 0;
       }
@@ -285,7 +290,7 @@ CG_HD bool count_rule(const DSpec& sp, const ZoneView& z, const Segment* segs, i
     count_out[s] = (int32_t)cnt;
     dmask_out[s] = dm;
   }
-  if (final_walk && ok && !final_known) {
+  if (kWalk && final_walk && ok && !final_known) {
     const int64_t e = next_exact(sp, z, pos, INT64_MAX);
     if (e == CG_NO_PROGRESS || (e <= pos && e != CG_ZERO_TIME)) ok = false;
   }

@@ -330,6 +330,7 @@ __global__ __launch_bounds__(256) void k_dispatch_min(const int64_t* __restrict_
   }
 }
 
+template <bool kWalk>
 __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, int64_t R,
                                                 PlanArgs p, int64_t* __restrict__ run_anchor,
                                                 int32_t* __restrict__ run_count,
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, 
        r += int64_t(gridDim.x) * blockDim.x) {
     DSpec sp = load_spec(specs + r);
     const int64_t j0 = r * G;
-    if (!count_rule(sp, v.z, v.segs, G, v.dtab, p.t0, p.t1, p.flags, run_anchor + j0, run_count + j0,
+    if (!count_rule<kWalk>(sp, v.z, v.segs, G, v.dtab, p.t0, p.t1, p.flags, run_anchor + j0, run_count + j0,
                     run_dmask + j0))
       atomicMin(stuck_rule, (unsigned long long)r);
   }
@@ -1252,8 +1253,14 @@ void launch_count(const DSpec* specs, int64_t R, const PlanArgs& p, int64_t* run
                   int32_t* run_count, uint32_t* run_dmask, unsigned long long* stuck_rule,
                   hipStream_t st) {
   if (R <= 0) return;
-  hipLaunchKernelGGL(k_count, dim3(grid_for(R, 256, CG_COUNT_MAX_BLOCKS)), dim3(256), plan_lds_bytes(p), st,
-                     specs, R, p, run_anchor, run_count, run_dmask, stuck_rule);
+  // the plan's walked parts (flags: WALK segments, an exact Next from T0, a
+  // final walk); without them k_count needs no exact walk
+  if (p.flags != 0)
+    hipLaunchKernelGGL(k_count<true>, dim3(grid_for(R, 256, CG_COUNT_MAX_BLOCKS)), dim3(256), plan_lds_bytes(p), st,
+                       specs, R, p, run_anchor, run_count, run_dmask, stuck_rule);
+  else
+    hipLaunchKernelGGL(k_count<false>, dim3(grid_for(R, 256, CG_COUNT_MAX_BLOCKS)), dim3(256), plan_lds_bytes(p),
+                       st, specs, R, p, run_anchor, run_count, run_dmask, stuck_rule);
 }
 
 size_t scan_temp_bytes(int64_t n) {

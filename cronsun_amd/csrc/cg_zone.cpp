@@ -465,6 +465,8 @@ Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
     cur = w.second;
   }
   if (cur < t1) add_cf(cur, t1);
+  for (const Segment& sg : plan.segs)
+    if (sg.kind != 0) plan.flags |= kPlanWalkSegs;
   return plan;
 }
 

@@ -61,12 +61,13 @@ struct Segment {
 };
 constexpr uint32_t kPlanT0Walk = 1;     // Next(T0) by the exact walk
 constexpr uint32_t kPlanFinalWalk = 2;  // the Next past T1 walked to its end
+constexpr uint32_t kPlanWalkSegs = 4;   // the plan has WALK segments
 struct Plan {
   std::vector<Segment> segs;
   std::vector<uint32_t> dtab;  // per CF local day: month | dom << 4 | dow << 9
   ZoneTable table;
   int64_t margin = 0;
-  uint32_t flags = 0;  // kPlanT0Walk | kPlanFinalWalk (cg_expand.h)
+  uint32_t flags = 0;  // kPlanT0Walk | kPlanFinalWalk | kPlanWalkSegs
 };
 Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1);
 

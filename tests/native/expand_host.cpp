@@ -100,6 +100,16 @@ int main(int argc, char** argv) {
       std::vector<uint32_t> dm(G);
       std::vector<int64_t> got;
       bool ok = G == 0 || count_rule(d, zv, plan.segs.data(), G, plan.dtab.data(), t0, t1, plan.flags, anc.data(), cnt.data(), dm.data());
+      if (G > 0 && plan.flags == 0) {  // the kernel's no-walk specialisation must agree exactly
+        std::vector<int64_t> anc2(G);
+        std::vector<int32_t> cnt2(G);
+        std::vector<uint32_t> dm2(G);
+        const bool ok2 = count_rule<false>(d, zv, plan.segs.data(), G, plan.dtab.data(), t0, t1, plan.flags,
+                                           anc2.data(), cnt2.data(), dm2.data());
+        if (ok2 != ok || anc2 != anc || cnt2 != cnt || dm2 != dm) {
+          if (bad++ < 10) printf("NOWALK mismatch %s\n", names[r].c_str());
+        }
+      }
       for (int s = 0; s < G && ok; s++) {
         const Segment& sg = plan.segs[s];
         if (d.kind == KIND_EVERY) {
