@@ -351,7 +351,10 @@ __global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, 
 
 // ---- scan: int32 counts -> int64 exclusive offsets -----------------------
 constexpr int kScanThreads = 256;
-constexpr int kScanPerThread = 16;
+#ifndef CG_SCAN_PER_THREAD
+#define CG_SCAN_PER_THREAD 4  // A/B (profiles/r02_ab_scan.json): config 2 scan 32 -> 21.5 us at 4 (16 items: 245 blocks, < 1 wave per SIMD)
+#endif
+constexpr int kScanPerThread = CG_SCAN_PER_THREAD;
 constexpr int kScanTile = kScanThreads * kScanPerThread;
 constexpr int64_t kScanFuseTiles = 1024;  // up to 4M elements: carries summed per block
 
