@@ -750,9 +750,12 @@ int transpose_locked(cg_ctx* c, int64_t nnz, int32_t N) {
 // Rules per band: the band's rule-major fire lists (E_band * 8 B) should sit
 // in one XCD's 4 MiB L2 beside the write stream; a power of two, so the
 // cached segment bounds stay valid across windows of similar volume.
+#ifndef CG_BAND_BYTES
+#define CG_BAND_BYTES (1536 * 1024)
+#endif
 int32_t band_rules(int64_t R, int64_t E) {
   const double per_rule = double(std::max<int64_t>(E, 1)) * 8.0 / double(std::max<int64_t>(R, 1));
-  int64_t B = int64_t(1.5 * 1024 * 1024 / per_rule);
+  int64_t B = int64_t(double(CG_BAND_BYTES) / per_rule);
   int64_t p = 1024;
   while (p < B && p < R) p <<= 1;
   return int32_t(std::max<int64_t>(p, 1024));
