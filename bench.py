@@ -74,7 +74,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["config2", "pernode", "config3", "config4", "dispatch"], default="config2")
+    ap.add_argument("--workload", choices=["config2", "pernode", "config3", "config4", "dispatch", "parse"],
+                    default="config2")
     ap.add_argument("--rules", type=int, default=0, help="rules per GPU (0 = the workload's)")
     ap.add_argument("--horizon", type=int, default=0, help="seconds (0 = the workload's)")
     ap.add_argument("--window", type=int, default=0,
@@ -108,6 +109,9 @@ def main():
                          "then marked diagnostic and is not a headline)")
     args = ap.parse_args()
 
+    if args.workload == "parse":  # host-only: no GPU, no ranks
+        print(json.dumps(parse_line(args)), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -614,6 +618,50 @@ def dispatch_line(args, R, world, elapsed, wake, nkt, build_info, cpu):
                   "tests/test_gpu_dispatch.py, not in the bench",
         "library": {"build_info": build_info},
     }
+
+
+def parse_line(args):
+    """the batch parser (cg_parse_batch: parser.go:78-377
+    restated in C++, Go's error texts) over 10M spec strings of the config-2
+    mix on the host's CPUs; beside it the oracle's parser (the same semantics,
+    one spec per call) on one thread."""
+    import ctypes as C
+    import numpy as np
+    from cronsun_amd import _lib, synth
+    n_total = args.rules or 10_000_000
+    base = synth.spec_mix(1_000_000, seed=0x5EED)
+    enc = [s.encode() for s in base]
+    reps = (n_total + len(enc) - 1) // len(enc)
+    enc = (enc * reps)[:n_total]
+    bufs = (C.c_char_p * n_total)(*enc)
+    lens = np.array([len(b) for b in enc], dtype=np.uint64)
+    out = (_lib.cg_schedule * n_total)()
+    status = np.zeros(n_total, dtype=np.int32)
+    threads, cpuinfo = host_cpus()
+    times = []
+    for _ in range(max(1, args.warmup) + max(1, args.steps)):
+        t = time.perf_counter()
+        _lib.check(_lib.lib().cg_parse_batch(_lib.PARSE_DEFAULT, C.cast(bufs, C.c_void_p), lens.ctypes.data,
+                                             n_total, C.cast(out, C.c_void_p), status.ctypes.data, threads))
+        times.append(time.perf_counter() - t)
+    assert (status == 0).all()
+    dt = float(np.median(times[max(1, args.warmup):]))
+    O = _oracle()
+    sample = base[:200_000]
+    t = time.perf_counter()
+    for s in sample:
+        O.parse(s)
+    dto = time.perf_counter() - t
+    return {"metric": "cron specs parsed/sec (host batch parser, 10M config-2 specs)",
+            "value": n_total / dt, "unit": "specs/s", "n_gpus": 0, "steps": max(1, args.steps),
+            "warmup": max(1, args.warmup), "ms_per_step": dt * 1e3, "higher_is_better": True,
+            "scaling": "none", "vs_baseline": None, "dtype": "bytes", "data": "synthetic config-2 mix",
+            "config": {"workload": "parse: 10M spec strings (the 1M config-2 mix repeated), "
+                                   "cg_parse_batch, default options (parser.go:171-183)",
+                       "threads": threads, **cpuinfo},
+            "cpu_baseline": {"value": len(sample) / dto, "unit": "specs/s", "cores": 1, "kind": "port",
+                             "sample": f"the oracle's parser over the first {len(sample)} specs, one "
+                                       f"call per spec through ctypes ({dto:.2f} s)"}}
 
 
 def host_cpus():
