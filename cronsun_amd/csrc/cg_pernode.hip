@@ -260,6 +260,11 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
   seg_pair[t] = lo;
 }
 
+#ifndef CG_SEG_PAIRS_PER_LANE
+#define CG_SEG_PAIRS_PER_LANE 4
+#endif
+constexpr int kSegPairsPerLane = CG_SEG_PAIRS_PER_LANE;
+
 // Segment records, one wave per segment in band-major order (a band's
 // offsets stay in L2): the segment's event count, and for each of its
 // non-empty pairs (in order, compacted to the front of the segment's pair
@@ -292,23 +297,24 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
     const int64_t band_hi = rule_off[int64_t(k + 1) * B < R ? int64_t(k + 1) * B : R];
     int64_t run = 0;  // events of the segment so far
     int32_t nrec = 0;
-    // 256 pairs per round, 4 consecutive ones per lane: all their loads in
-    // flight together (most segments take one or two rounds)
-    for (int64_t pc = p0; pc < p1; pc += 256) {
-      const int64_t pb = pc + 4 * lane;
-      int32_t r[4];
-      int64_t a[4], c[4];
+    // 64*P pairs per round, P consecutive ones per lane: all their loads in
+    // flight together (a segment holds ~300 pairs at config 3's shape)
+    constexpr int P = kSegPairsPerLane;
+    for (int64_t pc = p0; pc < p1; pc += 64 * P) {
+      const int64_t pb = pc + P * lane;
+      int32_t r[P];
+      int64_t a[P], c[P];
 #pragma unroll
-      for (int u = 0; u < 4; u++) r[u] = pb + u < p1 ? nt_rule[pb + u] : -1;
+      for (int u = 0; u < P; u++) r[u] = pb + u < p1 ? nt_rule[pb + u] : -1;
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < P; u++) {
         a[u] = r[u] >= 0 ? rule_off[r[u]] : 0;
         c[u] = r[u] >= 0 ? rule_off[r[u] + 1] : 0;
       }
       int64_t lsum = 0;
       int32_t lne = 0;
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < P; u++) {
         c[u] -= a[u];
         lsum += c[u];
         lne += c[u] > 0;
@@ -327,7 +333,7 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
       int64_t d = run + incl - lsum;
       int64_t at = p0 + nrec + (inc_ne - lne);
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < P; u++) {
         if (c[u] > 0) {
           rec_rule[at] = r[u];
           rec_dst[at] = int32_t(d);
@@ -394,6 +400,10 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 #define CG_NODE_BATCH 4
 #endif
 constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
+#ifndef CG_NODE_DEPTH
+#define CG_NODE_DEPTH 2
+#endif
+constexpr int kNodeDepth = CG_NODE_DEPTH;  // batches in flight (register sets)
 #ifndef CG_NODE_STORE_SC1
 #define CG_NODE_STORE_SC1 1
 #endif
@@ -557,31 +567,37 @@ __global__ __launch_bounds__(256) void k_node_write(
           }
         }
       };
-      // Software-pipelined over two register sets: batch k + 1 is placed and
-      // its gathers issued before batch k's stores.  Vector-memory returns are
-      // counted in issue order, so waiting for gathers issued after a batch of
-      // stores would also wait for those stores' write acknowledgements.
+      // Software-pipelined over kNodeDepth register sets: batches k + 1 ..
+      // k + depth - 1 are placed and their gathers issued before batch k's
+      // stores.  Vector-memory returns are counted in issue order, so waiting
+      // for gathers issued after a batch of stores would also wait for those
+      // stores' write acknowledgements.
       constexpr int32_t kStep = 64 * kNodeBatch;
-      int32_t giA[kNodeBatch], rvA[kNodeBatch], giB[kNodeBatch], rvB[kNodeBatch];
-      int64_t vA[kNodeBatch], vB[kNodeBatch];
+      constexpr int D = kNodeDepth;
+      int32_t gi[D][kNodeBatch], rv[D][kNodeBatch];
+      int64_t v[D][kNodeBatch];
       int32_t bq = qw & ~63;
-      place(bq, giA, rvA);
-      gather(giA, vA);
-      for (;;) {
-        if (bq + kStep < we) {
-          place(bq + kStep, giB, rvB);
-          gather(giB, vB);
+#pragma unroll
+      for (int s = 0; s + 1 < D; s++)
+        if (bq + s * kStep < we) {
+          place(bq + s * kStep, gi[s], rv[s]);
+          gather(gi[s], v[s]);
         }
-        store(bq, giA, vA, rvA);
-        bq += kStep;
-        if (bq >= we) break;
-        if (bq + kStep < we) {
-          place(bq + kStep, giA, rvA);
-          gather(giA, vA);
+      for (bool more = true; more;) {
+#pragma unroll
+        for (int s = 0; s < D; s++) {  // set s holds the batch at bq
+          const int nx = (s + D - 1) % D;
+          if (bq + (D - 1) * kStep < we) {
+            place(bq + (D - 1) * kStep, gi[nx], rv[nx]);
+            gather(gi[nx], v[nx]);
+          }
+          store(bq, gi[s], v[s], rv[s]);
+          bq += kStep;
+          if (bq >= we) {
+            more = false;
+            break;
+          }
         }
-        store(bq, giB, vB, rvB);
-        bq += kStep;
-        if (bq >= we) break;
       }
     }
   }

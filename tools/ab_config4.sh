@@ -14,6 +14,6 @@ for v in "$@"; do
   f="$OUT/${WL}_${v:-base}_$round"
   CRONSUN_GPU_LIB=$PWD/cronsun_amd/libcronsun_gpu${v:+_$v}.so timeout -k 10 400 python bench.py --workload $WL \
     --steps $STEPS --warmup 1 --cpu-sample 0 --verify-sample 200 > "$f.json" 2> "$f.err" || { tail -20 "$f.err"; exit 1; }
-  python3 -c "import json; d=json.load(open('$f.json')); k=d['kernel_ms']; print('%-8s %s round $round count=%.4f scan=%.4f write_cf=%.3f node_write=%s step=%.4f ms verified=%s' % ('${v:-base}', '$WL', k['count'], k['scan'], k['write_cf'], k.get('node_write'), d['ms_per_step'], d['verified']))"
+  python3 -c "import json; d=json.load(open('$f.json')); k=d['kernel_ms']; print('%-8s %s round $round count=%.4f scan=%.4f write_cf=%.3f node_write=%s segs=%s step=%.4f ms verified=%s' % ('${v:-base}', '$WL', k['count'], k['scan'], k['write_cf'], k.get('node_write'), k.get('segments_and_offsets'), d['ms_per_step'], d['verified']))"
 done
 done
