@@ -502,6 +502,9 @@ def main():
     achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
 
     cpu = None
+    if world == 1 and args.cpu_sample != 0 and pn:
+        a_last = list(range(t0, t1, W))[-1]
+        cpu = cpu_baseline_per_node(spec_of, rin, xmode, a_last, min(a_last + W, t1), args.zone)
     if world == 1 and args.cpu_sample != 0 and wl == "config2":
         cpu = cpu_baseline(specs, args.cpu_sample, t0, t1, args.cpu_threads, zone=args.zone)
 
@@ -776,6 +779,33 @@ def cpu_dispatch(specs, t0):
     return {"value": len(scheds) / dt, "unit": "entries/s", "cores": 1, "kind": "port",
             "sample": f"{len(scheds)} entries of the same mix, {wakes} steady-state wakes "
                       f"({dt * 1e3:.1f} ms per wake: qsort by Next + Next for the due prefix)"}
+
+
+def cpu_baseline_per_node(spec_of, rin, mode, a, b, zone, n_nodes=24, seed=0x5EED + 55):
+    """The reference's per-node work on the host (oracle port, all host CPUs):
+    every node filters all jobs (node.go:121-158 -> Job.Cmds) and runs the
+    Next loop of its rules over the window, then lists its (time, rule)
+    events -- timed on a seeded sample of nodes, events/s over the sample."""
+    import numpy as np
+    O = _oracle()
+    threads, cpuinfo = host_cpus()
+    loc = O.Loc(zone)
+    nodes = np.sort(np.random.default_rng(seed).choice(rin.n_nodes, n_nodes, replace=False))
+    ts = time.perf_counter()
+    roff, rules = O.node_rules(rin, mode, nodes, threads=threads)
+    t_filter = time.perf_counter() - ts
+    events = 0
+    for k in range(len(nodes)):
+        rs = rules[roff[k]:roff[k + 1]]
+        eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(r)) for r in rs]), a, b, loc, threads=threads)
+        O.node_list(eo, et, np.arange(len(rs)))
+        events += int(eo[-1])
+    dt = time.perf_counter() - ts
+    return {"value": events / dt, "unit": "node events/s", "cores": threads, "kind": "port",
+            "sample": f"{len(nodes)} nodes of {rin.n_nodes}: each filters all {rin.n_rules} rules "
+                      f"({t_filter:.2f} s for the sample) then expands its rules over ({a}, {b}] and lists "
+                      f"its events ({events} node events, {dt:.2f} s; parse of the rules' specs included)",
+            **cpuinfo}
 
 
 def cpu_baseline(specs, sample, t0, t1, threads, zone="UTC"):
