@@ -318,3 +318,29 @@ def test_async_pipeline(eng):
         e2.expand_wait()
     assert err.value.code == _lib.CG_ERANGE and "rule 1:" in err.value.msg
     e2.close()
+
+
+@pytest.mark.parametrize("zone", ["America/New_York", "America/Havana", "Australia/Lord_Howe",
+                                  "Pacific/Chatham", "Pacific/Apia", "Europe/Dublin"])
+def test_starts_near_transitions(eng, zone):
+    """T0 just before, on, inside the overlap of, and hours / a day after zone
+    transitions of 2011-2027 (Pacific/Apia's skipped 2011-12-30 included):
+    the narrowed WALK windows, Next(T0) by the exact walk after a recent
+    transition, and the last Next walked to its end before a skipped day --
+    the kernels against the oracle (the host check in tests/native covers
+    more starts)."""
+    from test_zone import _table
+    z = product_zone(zone)
+    when, off = _table(z, 1293840000, 1830297600)
+    idx = list(range(1, len(when), max(1, (len(when) - 1) // 3)))[:3]
+    big = 1 + int(np.argmax(np.abs(np.diff(off))))
+    if big not in idx:
+        idx.append(big)
+    rng = np.random.default_rng(zlib.crc32(("near" + zone).encode()))
+    specs = [random_spec(rng) for _ in range(150)] + ["0 30 2 * * *", "0 0 0 * * *", "0 0 9 * * Sat",
+                                                      "0 0 1 * * *", "0 */15 * * * *"]
+    scheds = [cron.Parse(s) for s in specs]
+    for i in idx:
+        tau = int(when[i])
+        for o in (-3600, -1, 0, 1, 3599, 3601, 18001, 90000):
+            check_same(eng, scheds, zone, tau + o, tau + o + 30 * 3600, specs)
