@@ -20,6 +20,21 @@ int cg_hip_check(hipError_t e, const char* what);
   } while (0)
 
 // Grow-only device buffer (grows by 1.25x so repeated calls settle).
+// per-node writer record of one non-empty (node, rule) pair of a segment
+// (cg_pernode.hip, k_seg_records): rule, first position in the segment, and
+// x, st -- fire at position p = t0 + x + p * st (a progression rule), or
+// band-relative fire-list index = x + p when st == 0
+// per rule of a per-node window (k_rule_info): fire count, band-relative
+// index of the first fire, and {first - t0, stride} of a progression (st 0:
+// not one)
+struct alignas(16) RuleInfo {
+  int32_t cnt, off, first, st;
+};
+
+struct alignas(16) PairRec {
+  int32_t rule, dst, x, st;
+};
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
@@ -155,7 +170,9 @@ struct cg_ctx {
   // transpose, the (node, rule band) segments and the node CSR
   DBuf<int64_t> rn_off, node_off, node_time, nt_off, rs_off, seg_pair, seg_cnt, seg_pos;
   DBuf<int32_t> rn_cnt, rn_nodes, pair_node, pair_rule, node_rule, nt_rule, rs_hist;
-  DBuf<int32_t> seg_nrec, rec_rule, rec_dst, rec_dlt;  // per-call segment records
+  DBuf<int32_t> seg_nrec;
+  DBuf<PairRec> recs;  // per-call segment records (k_seg_records)
+  DBuf<RuleInfo> rule_info;  // per-call, per rule (k_rule_info)
   DBuf<uint32_t> pn_tickets;
   // time-order pass (cg_node_order.hip): node-aligned tiles, per-pass
   // histograms/offsets, and the second buffers of the ping-pong
@@ -191,7 +208,8 @@ struct cg_ctx {
     seg_pair.release(); seg_cnt.release(); seg_pos.release(); rn_cnt.release(); rn_nodes.release();
     pair_node.release(); pair_rule.release(); node_rule.release(); nt_rule.release();
     rs_hist.release(); pn_tickets.release(); rules.release();
-    seg_nrec.release(); rec_rule.release(); rec_dst.release(); rec_dlt.release();
+    seg_nrec.release(); recs.release();
+    rule_info.release();
     ts_cnt.release(); ts_tile_node.release(); ts_hist.release(); node_rule2.release();
     ts_base.release(); ts_off.release(); node_time2.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);

@@ -260,6 +260,63 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
   seg_pair[t] = lo;
 }
 
+// Per rule of the window's rule-major CSR, one 16-byte RuleInfo: its fire
+// count, the band-relative index of its first fire, and whether its fires
+// form an arithmetic progression {first fire - t0, stride} (stride 0: they do
+// not, or it does not fit 32 bits).  In a 1-h window nearly every rule's
+// fires are one (`0 */5 * * * *`, `@every`, `*/10 * * * * *`, any rule with
+// <= 2 fires: 95 % of config 3's events), and the per-node writer computes
+// those fires instead of gathering them.  k_seg_records then reads one
+// 16-byte word per pair instead of three scattered ones.  One block per 256
+// rules: lanes take the block's events in turn, find their rule by a binary
+// search over the block's offsets in LDS and clear the rule's flag on a step
+// that differs from its first one.
+#ifndef CG_NODE_AP
+#define CG_NODE_AP 1
+#endif
+constexpr int kApRules = 256;
+__global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ rule_off,
+                                                    const int64_t* __restrict__ times, int64_t R, int64_t t0,
+                                                    int32_t B, RuleInfo* __restrict__ info) {
+  __shared__ int64_t off[kApRules + 1];
+  __shared__ int64_t step[kApRules];
+  __shared__ int32_t ok[kApRules];
+  const int64_t r0 = int64_t(blockIdx.x) * kApRules;
+  const int nr = int(R - r0 < kApRules ? R - r0 : kApRules);
+  const int tid = threadIdx.x;
+  const int64_t band_lo = rule_off[(r0 / B) * B];  // B is a multiple of kApRules
+  int64_t first = 0, cnt = 0;
+  if (tid < nr) {
+    const int64_t a = rule_off[r0 + tid];
+    cnt = rule_off[r0 + tid + 1] - a;
+    first = cnt > 0 ? times[a] : 0;
+    off[tid] = a;
+    step[tid] = cnt > 1 ? times[a + 1] - first : 1;
+    ok[tid] = CG_NODE_AP;
+  }
+  if (tid == 0) off[nr] = rule_off[r0 + nr];
+  __syncthreads();
+  const int64_t e_end = off[nr];
+  for (int64_t e = off[0] + tid; e + 1 < e_end; e += blockDim.x) {
+    int lo = 0, hi = nr - 1;  // the last rule whose list starts at or before e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (off[mid] <= e) lo = mid;
+      else hi = mid - 1;
+    }
+    if (e + 1 < off[lo + 1] && times[e + 1] - times[e] != step[lo]) ok[lo] = 0;
+  }
+  __syncthreads();
+  if (tid < nr) {
+    const int64_t rel = first - t0, s = step[tid];
+    const bool prog = cnt > 0 && ok[tid] && rel >= 0 && rel <= INT32_MAX && s > 0 && s <= INT32_MAX;
+    // counts and band-relative indices are < 2^30 (k_seg_records checks the
+    // band span and fails the call otherwise)
+    info[r0 + tid] = RuleInfo{int32_t(cnt), int32_t(off[tid] - band_lo), prog ? int32_t(rel) : 0,
+                              prog ? int32_t(s) : 0};
+  }
+}
+
 #ifndef CG_SEG_PAIRS_PER_LANE
 #define CG_SEG_PAIRS_PER_LANE 4
 #endif
@@ -268,20 +325,21 @@ constexpr int kSegPairsPerLane = CG_SEG_PAIRS_PER_LANE;
 // Segment records, one wave per segment in band-major order (a band's
 // offsets stay in L2): the segment's event count, and for each of its
 // non-empty pairs (in order, compacted to the front of the segment's pair
-// range) a record {rule, first event relative to the segment, band-relative
-// fire-list index minus that position}.  The writer then reads plain records
-// instead of chasing pair -> rule -> offsets per window.  Block 0 also resets
-// the writer's tickets; err[0] is set if a segment or a band outgrows the
-// writer's 32-bit positions.
+// range) a record {rule, first event relative to the segment, x, stride}:
+// for a progression rule (k_rule_info) x = first fire - t0 - position * stride,
+// so its fire at segment position p is t0 + x + p * stride; otherwise stride
+// is 0 and x = band-relative fire-list index minus the position.  The writer
+// then reads plain records instead of chasing pair -> rule -> offsets per
+// window.  Block 0 also resets the writer's tickets; err[0] is set if a
+// segment or a band outgrows the writer's 32-bit positions.
 __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__ seg_pair,
                                                       const int32_t* __restrict__ nt_rule,
-                                                      const int64_t* __restrict__ rule_off, int32_t N,
+                                                      const int64_t* __restrict__ rule_off,
+                                                      const RuleInfo* __restrict__ info, int32_t N,
                                                       int32_t K, int32_t B, int64_t R,
                                                       int64_t* __restrict__ seg_cnt,
                                                       int32_t* __restrict__ seg_nrec,
-                                                      int32_t* __restrict__ rec_rule,
-                                                      int32_t* __restrict__ rec_dst,
-                                                      int32_t* __restrict__ rec_dlt,
+                                                      PairRec* __restrict__ recs,
                                                       uint32_t* __restrict__ tickets,
                                                       int64_t* __restrict__ err) {
   if (blockIdx.x == 0)
@@ -303,21 +361,17 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
     for (int64_t pc = p0; pc < p1; pc += 64 * P) {
       const int64_t pb = pc + P * lane;
       int32_t r[P];
-      int64_t a[P], c[P];
+      RuleInfo g[P];
 #pragma unroll
       for (int u = 0; u < P; u++) r[u] = pb + u < p1 ? nt_rule[pb + u] : -1;
 #pragma unroll
-      for (int u = 0; u < P; u++) {
-        a[u] = r[u] >= 0 ? rule_off[r[u]] : 0;
-        c[u] = r[u] >= 0 ? rule_off[r[u] + 1] : 0;
-      }
+      for (int u = 0; u < P; u++) g[u] = r[u] >= 0 ? info[r[u]] : RuleInfo{0, 0, 0, 0};
       int64_t lsum = 0;
       int32_t lne = 0;
 #pragma unroll
       for (int u = 0; u < P; u++) {
-        c[u] -= a[u];
-        lsum += c[u];
-        lne += c[u] > 0;
+        lsum += g[u].cnt;
+        lne += g[u].cnt > 0;
       }
       // wave exclusive scans of the lane sums (events) and non-empty counts
       int64_t incl = lsum;
@@ -334,13 +388,13 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
       int64_t at = p0 + nrec + (inc_ne - lne);
 #pragma unroll
       for (int u = 0; u < P; u++) {
-        if (c[u] > 0) {
-          rec_rule[at] = r[u];
-          rec_dst[at] = int32_t(d);
-          rec_dlt[at] = int32_t((a[u] - band_lo) - d);
+        if (g[u].cnt > 0) {
+          const int64_t x = int64_t(g[u].first) - d * g[u].st;
+          const bool prog = g[u].st != 0 && x >= INT32_MIN && x <= INT32_MAX;
+          recs[at] = PairRec{r[u], int32_t(d), int32_t(prog ? x : int64_t(g[u].off) - d), prog ? g[u].st : 0};
           at++;
         }
-        d += c[u];
+        d += g[u].cnt;
       }
       const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(incl)), 63));
       const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(incl) >> 32)), 63));
@@ -404,28 +458,42 @@ constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight
 #define CG_NODE_DEPTH 2
 #endif
 constexpr int kNodeDepth = CG_NODE_DEPTH;  // batches in flight (register sets)
-#ifndef CG_NODE_STORE_SC1
-#define CG_NODE_STORE_SC1 1
+#ifndef CG_NODE_CONFINE
+#define CG_NODE_CONFINE 1
 #endif
-// Output stores.  Plain stores keep the written line in the XCD's L2, so the
-// 10 GB write stream keeps evicting the band's rule-major times that the
-// gathers want from L2; relaxed agent-scope atomic stores are plain vector
-// stores with sc1, which leave L2 (MI355X_MICROARCH.md: stores of each flavour).
+constexpr bool kNodeConfine = CG_NODE_CONFINE;  // gathers waited for in their own branch
+#ifndef CG_NODE_RUNS
+#define CG_NODE_RUNS 1
+#endif
+constexpr bool kNodeRuns = CG_NODE_RUNS;  // blocks owned by one record stored straight from it
+#ifndef CG_NODE_STORE
+#define CG_NODE_STORE 2
+#endif
+// Output stores: 0 plain, 1 sc1 (relaxed agent-scope atomic stores), 2 nt.
+// Plain stores keep the written lines in the XCD's L2; nt (streaming) stores
+// were the fastest on one box (pernode writer 2.36 ms vs 2.60 sc1, 2.71
+// plain, profiles/r02_ab_node_store.json): the writer waits for its own
+// stores whenever it needs a load, and streaming stores retire soonest.
 template <class T>
 __device__ __forceinline__ void out_store(T* p, T v) {
-#if CG_NODE_STORE_SC1
+#if CG_NODE_STORE == 2
+  __builtin_nontemporal_store(v, p);
+#elif CG_NODE_STORE == 1
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #else
   *p = v;
 #endif
 }
+#ifndef CG_NODE_UNIFORM
+#define CG_NODE_UNIFORM 1
+#endif
+constexpr bool kNodeUniform = CG_NODE_UNIFORM;  // readlane path for batches without inner record starts
 constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 node-major
 
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
-    const int32_t* __restrict__ seg_nrec, const int32_t* __restrict__ rec_rule,
-    const int32_t* __restrict__ rec_dst, const int32_t* __restrict__ rec_dlt,
+    const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, int64_t t0,
     const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times, int32_t N, int32_t K,
     int32_t B, int64_t cap, uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time,
     int32_t* __restrict__ out_rule, int node_major) {
@@ -481,19 +549,19 @@ __global__ __launch_bounds__(256) void k_node_write(
     int32_t pq = -1, prule = 0;  // a block carried into the next chunk
     int64_t ptime = 0;
     // records in chunks of 64 (lane i: record i), the next chunk in flight
-    int32_t nx_r = 0, nx_d = 0, nx_l = 0, nx_end = q_hi;
+    // (an unconditional load at a clamped index: a load under a branch is
+    // waited for at the branch's end, so the prefetch would not stay in flight)
+    PairRec nx;
+    int32_t nx_end = q_hi;
     auto fetch = [&](int32_t w) {
-      if (w + lane < nrec) {
-        nx_r = rec_rule[p0 + w + lane];
-        nx_d = rec_dst[p0 + w + lane] + q_lo;
-        nx_l = rec_dlt[p0 + w + lane] - q_lo;
-      }
+      nx = recs[p0 + (w + lane < nrec ? w + lane : nrec - 1)];
       // the chunk ends where the next one's first record starts
-      nx_end = w + 64 < nrec ? rec_dst[p0 + w + 64] + q_lo : q_hi;
+      nx_end = w + 64 < nrec ? recs[p0 + w + 64].dst + q_lo : q_hi;
     };
     fetch(0);
     for (int32_t w = 0; w < nrec; w += 64) {
-      const int32_t rr = nx_r, dst = nx_d, dlt = nx_l, we = nx_end;  // q of first event, band index - q
+      // q of first event; x and stride of the record (k_seg_records)
+      const int32_t rr = nx.rule, dst = nx.dst + q_lo, dlt = nx.x, sst = nx.st, we = nx_end;
       const int nc = nrec - w < 64 ? nrec - w : 64;
       const int32_t qw = __builtin_amdgcn_readlane(dst, 0);
       if (w + 64 < nrec) fetch(w + 64);
@@ -503,9 +571,17 @@ __global__ __launch_bounds__(256) void k_node_write(
       // their own past 64), one wave barrier for the batch; lane l's record =
       // (records starting before the block: a ballot, the records are sorted)
       // - 1 + (marks at lanes <= l).  No block waits on the one before it.
-      auto place = [&](int32_t bq, int32_t (&gi)[kNodeBatch], int32_t (&rvs)[kNodeBatch]) {
+      // A lane of a progression record computes its fire here; the others
+      // get a gather index (gi >= 0) and are filled by gather().
+      auto place = [&](int32_t bq, int32_t (&gi)[kNodeBatch], int32_t (&rvs)[kNodeBatch],
+                       int64_t (&vals)[kNodeBatch]) {
         tag++;
-        if (!(V & 4)) {
+        // No record starting strictly inside a block of the batch (a long
+        // run, e.g. an every-second rule's 3600 fires): every block has one
+        // owner for all its lanes, read with readlane -- no marks, no barrier.
+        const bool uni = kNodeUniform && !(V & 4) &&
+                         __ballot(live && dst > bq && dst < bq + 64 * kNodeBatch && (dst & 63) != 0) == 0;
+        if (!(V & 4) && !uni) {
 #pragma unroll
           for (int u = 0; u < kNodeBatch; u++) {
             const int32_t b = bq + 64 * u;
@@ -519,22 +595,36 @@ __global__ __launch_bounds__(256) void k_node_write(
 #pragma unroll
         for (int u = 0; u < kNodeBatch; u++) {
           const int32_t b = bq + 64 * u;
-          gi[u] = -1;  // band index of this lane's fire (-1: none here)
+          gi[u] = -1;  // band index of this lane's fire (-1: none to gather)
           rvs[u] = 0;
+          vals[u] = 0;
           if (b >= we || (V & 4)) continue;
           const int32_t q = b + lane;
-          const uint64_t M = __ballot(marks[u * 128 + lane] == tag);
-          const int before = __popcll(__ballot(live && dst < b));
-          int own = before - 1 + __popcll(M & le);
-          own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
-          const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
-          rvs[u] = __builtin_amdgcn_ds_bpermute(own << 2, rr);
-          gi[u] = (q >= qw && q < we) ? q + dl : -1;
+          int32_t dl, sv;
+          if (uni) {
+            int own = __popcll(__ballot(live && dst <= b)) - 1;
+            own = own < 0 ? 0 : own;
+            dl = __builtin_amdgcn_readlane(dlt, own);
+            sv = __builtin_amdgcn_readlane(sst, own);
+            rvs[u] = __builtin_amdgcn_readlane(rr, own);
+          } else {
+            const uint64_t M = __ballot(marks[u * 128 + lane] == tag);
+            const int before = __popcll(__ballot(live && dst < b));
+            int own = before - 1 + __popcll(M & le);
+            own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
+            dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
+            sv = __builtin_amdgcn_ds_bpermute(own << 2, sst);
+            rvs[u] = __builtin_amdgcn_ds_bpermute(own << 2, rr);
+          }
+          const bool in = q >= qw && q < we;
+          gi[u] = in && sv == 0 ? q + dl - q_lo : -1;
+          vals[u] = in && sv != 0 ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
         }
       };
       auto gather = [&](const int32_t (&gi)[kNodeBatch], int64_t (&vals)[kNodeBatch]) {
 #pragma unroll
-        for (int u = 0; u < kNodeBatch; u++) vals[u] = (V & 1) ? int64_t(gi[u]) : tb[gi[u] < 0 ? 0 : gi[u]];
+        for (int u = 0; u < kNodeBatch; u++)
+          if (gi[u] >= 0) vals[u] = (V & 1) ? int64_t(gi[u]) : tb[gi[u]];
       };
       auto store = [&](int32_t bq, const int32_t (&gi)[kNodeBatch], const int64_t (&vals)[kNodeBatch],
                        const int32_t (&rvs)[kNodeBatch]) {
@@ -543,7 +633,7 @@ __global__ __launch_bounds__(256) void k_node_write(
           const int32_t b = bq + 64 * u;
           if (b >= we) break;
           const int32_t q = b + lane;
-          int64_t val = gi[u] < 0 ? 0 : vals[u];
+          int64_t val = vals[u];
           int32_t rv = rvs[u];
           if (b == pq) {  // lanes of the previous chunk
             val = q < qw ? ptime : val;
@@ -573,6 +663,109 @@ __global__ __launch_bounds__(256) void k_node_write(
       // for gathers issued after a batch of stores would also wait for those
       // stores' write acknowledgements.
       constexpr int32_t kStep = 64 * kNodeBatch;
+      if (kNodeRuns && V == 0) {
+        // Runs.  A block that one record owns entirely (no record starts
+        // inside it) is stored straight from that record: a progression's
+        // fires are t0 + x + p * stride, so a run of such blocks costs two
+        // stores and an add per block.  Blocks where records start, and the
+        // chunk's first and last blocks (shared with the neighbouring chunk
+        // or at the segment's edges), go through one(): LDS start marks,
+        // bpermute of the lane's record, the carry and the edge stores.
+        auto one = [&](int32_t b) {
+          tag++;
+          const bool mark = live && dst >= b && dst < b + 64;
+          marks[mark ? dst - b : 64 + lane] = tag;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const int32_t q = b + lane;
+          const uint64_t M = __ballot(marks[lane] == tag);
+          const int before = __popcll(__ballot(live && dst < b));
+          int own = before - 1 + __popcll(M & le);
+          own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
+          const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
+          const int32_t sv = __builtin_amdgcn_ds_bpermute(own << 2, sst);
+          int32_t rv = __builtin_amdgcn_ds_bpermute(own << 2, rr);
+          const bool in = q >= qw && q < we;
+          int64_t val = in && sv != 0 ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
+          const int32_t gi = in && sv == 0 ? q + dl - q_lo : -1;
+          if (__ballot(gi >= 0)) {  // waited for here, not after the branch
+            if (gi >= 0) val = tb[gi];
+            asm volatile("" : "+v"(val));
+          }
+          if (b == pq) {  // lanes of the previous chunk
+            val = q < qw ? ptime : val;
+            rv = q < qw ? prule : rv;
+          }
+          if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
+            if (b >= q_lo && b + 64 <= q_hi) {
+              out_store(ot + q, val);
+              out_store(orl + q, rv);
+            } else if (q >= q_lo && q < q_hi) {  // a segment edge
+              out_store(ot + q, val);
+              out_store(orl + q, rv);
+            }
+            pq = -1;
+          } else {  // carried into the next chunk
+            pq = b;
+            ptime = val;
+            prule = rv;
+          }
+        };
+        const int32_t b0 = qw & ~63, bl = we & ~63;
+        if (qw & 63) one(b0);
+        for (int32_t b = (qw + 63) & ~63; b < bl;) {
+          const int o = __popcll(__ballot(live && dst <= b)) - 1;  // owner of lane 0 (dst[0] = qw <= b)
+          const int32_t e = o + 1 < nc ? __builtin_amdgcn_readlane(dst, o + 1) : we;
+          if (e < b + 64) {  // a record starts inside
+            one(b);
+            b += 64;
+            continue;
+          }
+          const int32_t bend = (e & ~63) < bl ? (e & ~63) : bl;  // blocks [b, bend) all o's
+          const int32_t dl = __builtin_amdgcn_readlane(dlt, o), sv = __builtin_amdgcn_readlane(sst, o);
+          const int32_t rv = __builtin_amdgcn_readlane(rr, o);
+          if (sv != 0) {
+            int64_t val = t0 + int64_t(dl) + int64_t(b + lane - q_lo) * sv;
+            const int64_t step = int64_t(64) * sv;
+            for (; b < bend; b += 64, val += step) {
+              out_store(ot + b + lane, val);
+              out_store(orl + b + lane, rv);
+            }
+          } else {
+            for (; b < bend; b += 64) {
+              int64_t val = tb[b + lane + dl - q_lo];
+              asm volatile("" : "+v"(val));
+              out_store(ot + b + lane, val);
+              out_store(orl + b + lane, rv);
+            }
+          }
+        }
+        if ((we & 63) && (bl != b0 || !(qw & 63))) one(bl);
+        continue;
+      }
+      if (kNodeConfine) {
+        // Fires of progression records need no load, so a batch normally
+        // issues only stores.  Gathers (other rules) are issued and waited for
+        // inside a wave-uniform branch of their own: waiting for a load waits
+        // for every store issued before it, and a wait after the branch would
+        // drain the wave's stores on every batch.
+        for (int32_t bq = qw & ~63; bq < we; bq += kStep) {
+          int32_t gi[kNodeBatch], rv[kNodeBatch];
+          int64_t v[kNodeBatch];
+          place(bq, gi, rv, v);
+          bool need = false;
+#pragma unroll
+          for (int u = 0; u < kNodeBatch; u++) need |= gi[u] >= 0;
+          if (__ballot(need)) {
+            gather(gi, v);
+#pragma unroll
+            for (int u = 0; u < kNodeBatch; u++) asm volatile("" : "+v"(v[u]));
+          }
+          store(bq, gi, v, rv);
+        }
+        continue;
+      }
       constexpr int D = kNodeDepth;
       int32_t gi[D][kNodeBatch], rv[D][kNodeBatch];
       int64_t v[D][kNodeBatch];
@@ -580,7 +773,7 @@ __global__ __launch_bounds__(256) void k_node_write(
 #pragma unroll
       for (int s = 0; s + 1 < D; s++)
         if (bq + s * kStep < we) {
-          place(bq + s * kStep, gi[s], rv[s]);
+          place(bq + s * kStep, gi[s], rv[s], v[s]);
           gather(gi[s], v[s]);
         }
       for (bool more = true; more;) {
@@ -588,7 +781,7 @@ __global__ __launch_bounds__(256) void k_node_write(
         for (int s = 0; s < D; s++) {  // set s holds the batch at bq
           const int nx = (s + D - 1) % D;
           if (bq + (D - 1) * kStep < we) {
-            place(bq + (D - 1) * kStep, gi[nx], rv[nx]);
+            place(bq + (D - 1) * kStep, gi[nx], rv[nx], v[nx]);
             gather(gi[nx], v[nx]);
           }
           store(bq, gi[s], v[s], rv[s]);
@@ -821,14 +1014,18 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pn_res_dev), c->pn_res_host, 0));
   }
   if ((rc = c->seg_nrec.ensure(std::max<int64_t>(NK, 1))) ||
-      (rc = c->rec_rule.ensure(std::max<int64_t>(nnz, 1))) || (rc = c->rec_dst.ensure(std::max<int64_t>(nnz, 1))) ||
-      (rc = c->rec_dlt.ensure(std::max<int64_t>(nnz, 1))))
+      (rc = c->recs.ensure(std::max<int64_t>(nnz, 1))) ||
+      (rc = c->rule_info.ensure(std::max<int64_t>(R, 1))))
     return rc;
   c->pn_res_host[1] = 0;  // error flag (nothing of this ctx is in flight here)
+  if (R > 0)
+    hipLaunchKernelGGL(k_rule_info, dim3(unsigned((R + kApRules - 1) / kApRules)), dim3(256), 0, st,
+                       c->offsets.p, c->times.p, R, t0, B, c->rule_info.p);
   if (NK > 0)
     hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
-                       c->nt_rule.p, c->offsets.p, N, K, B, R, c->seg_cnt.p, c->seg_nrec.p, c->rec_rule.p,
-                       c->rec_dst.p, c->rec_dlt.p, c->pn_tickets.p, c->pn_res_dev + 1);
+                       c->nt_rule.p, c->offsets.p, c->rule_info.p, N, K, B, R, c->seg_cnt.p, c->seg_nrec.p,
+                       c->recs.p, c->pn_tickets.p,
+                       c->pn_res_dev + 1);
   launch_scan64(c->seg_cnt.p, c->seg_pos.p, NK, c->scan_tmp.p, st);
   hipLaunchKernelGGL(k_node_off_from_seg, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
                      c->seg_pos.p, N, K, c->node_off.p, c->pn_res_dev);
@@ -859,8 +1056,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL(k_node_write<V>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
-                     0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->rec_rule.p, c->rec_dst.p,          \
-                     c->rec_dlt.p, c->offsets.p, c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p,     \
+                     0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,      \
+                     c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p,     \
                      c->node_rule.p, node_major)
       switch (variant) {
         case 1: CG_NW(1); break;
