@@ -318,7 +318,7 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
 }
 
 #ifndef CG_SEG_PAIRS_PER_LANE
-#define CG_SEG_PAIRS_PER_LANE 4
+#define CG_SEG_PAIRS_PER_LANE 8
 #endif
 constexpr int kSegPairsPerLane = CG_SEG_PAIRS_PER_LANE;
 
@@ -344,64 +344,63 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
                                                       int64_t* __restrict__ err) {
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < kTicketGroups * kTicketStride; i += blockDim.x) tickets[i] = 0;
-  const int lane = threadIdx.x & 63;
+  // Two segments per wave, one per half-wave (consecutive nodes of a band):
+  // the kernel is latency-bound (segment bounds -> pair rules -> rule infos
+  // -> records), so two independent chains share each wait.
+  constexpr int L = 32;  // lanes per segment
+  const int lane = threadIdx.x & 63, hl = lane & (L - 1);
   const int64_t NK = int64_t(N) * K;
-  const int64_t nw = int64_t(gridDim.x) * (blockDim.x >> 6);
-  for (int64_t t = blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6); t < NK; t += nw) {
-    const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
+  const int64_t nh = int64_t(gridDim.x) * (blockDim.x >> 6) * 2;
+  for (int64_t tw = (blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2; tw < NK; tw += nh) {
+    const int64_t t = tw + (lane >> 5);
+    const bool act = t < NK;
+    const int32_t k = act ? int32_t(t / N) : 0, n = act ? int32_t(t - int64_t(k) * N) : 0;
     const int64_t s = int64_t(n) * K + k;
-    const int64_t p0 = seg_pair[s], p1 = seg_pair[s + 1];
+    const int64_t p0 = act ? seg_pair[s] : 0, p1 = act ? seg_pair[s + 1] : 0;
     const int64_t band_lo = rule_off[int64_t(k) * B];
     const int64_t band_hi = rule_off[int64_t(k + 1) * B < R ? int64_t(k + 1) * B : R];
     int64_t run = 0;  // events of the segment so far
     int32_t nrec = 0;
-    // 64*P pairs per round, P consecutive ones per lane: all their loads in
-    // flight together (a segment holds ~300 pairs at config 3's shape)
+    // L*P pairs per round and segment, P consecutive ones per lane: all their
+    // loads in flight together (a segment holds ~180 pairs at config 3's shape)
     constexpr int P = kSegPairsPerLane;
-    for (int64_t pc = p0; pc < p1; pc += 64 * P) {
-      const int64_t pb = pc + P * lane;
+    const int32_t len = int32_t(p1 - p0);
+    const int32_t rounds_len = max(__builtin_amdgcn_readlane(len, 0), __builtin_amdgcn_readlane(len, 32));
+    const uint32_t below = (1u << hl) - 1u;  // lanes of this half before this one
+    for (int32_t pc = 0; pc < rounds_len; pc += L * P) {
+      // pair u*L + hl of the round: every load and record store instruction
+      // covers consecutive pairs / records
       int32_t r[P];
       RuleInfo g[P];
 #pragma unroll
-      for (int u = 0; u < P; u++) r[u] = pb + u < p1 ? nt_rule[pb + u] : -1;
+      for (int u = 0; u < P; u++) {
+        const int64_t pp = p0 + pc + u * L + hl;
+        r[u] = pp < p1 ? nt_rule[pp] : -1;
+      }
 #pragma unroll
       for (int u = 0; u < P; u++) g[u] = r[u] >= 0 ? info[r[u]] : RuleInfo{0, 0, 0, 0};
-      int64_t lsum = 0;
-      int32_t lne = 0;
 #pragma unroll
       for (int u = 0; u < P; u++) {
-        lsum += g[u].cnt;
-        lne += g[u].cnt > 0;
-      }
-      // wave exclusive scans of the lane sums (events) and non-empty counts
-      int64_t incl = lsum;
-      int32_t inc_ne = lne;
-      for (int o = 1; o < 64; o <<= 1) {
-        const int64_t y = __shfl_up(incl, o, 64);
-        const int32_t z = __shfl_up(inc_ne, o, 64);
-        if (lane >= o) {
-          incl += y;
-          inc_ne += z;
+        // events before this pair: half-wave inclusive scan of the counts
+        int64_t incl = g[u].cnt;
+        for (int o = 1; o < L; o <<= 1) {
+          const int64_t y = __shfl_up(incl, o, L);
+          if (hl >= o) incl += y;
         }
-      }
-      int64_t d = run + incl - lsum;
-      int64_t at = p0 + nrec + (inc_ne - lne);
-#pragma unroll
-      for (int u = 0; u < P; u++) {
+        const int64_t d = run + incl - g[u].cnt;
+        const uint64_t ball = __ballot(g[u].cnt > 0);
+        const uint32_t ne = uint32_t(lane < 32 ? ball : ball >> 32);  // this half's non-empty pairs
         if (g[u].cnt > 0) {
+          const int64_t at = p0 + nrec + __popc(ne & below);
           const int64_t x = int64_t(g[u].first) - d * g[u].st;
           const bool prog = g[u].st != 0 && x >= INT32_MIN && x <= INT32_MAX;
           recs[at] = PairRec{r[u], int32_t(d), int32_t(prog ? x : int64_t(g[u].off) - d), prog ? g[u].st : 0};
-          at++;
         }
-        d += g[u].cnt;
+        run += __shfl(incl, L - 1, L);  // the half's total
+        nrec += __popc(ne);
       }
-      const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(incl)), 63));
-      const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(incl) >> 32)), 63));
-      run += int64_t((uint64_t(hi) << 32) | lo);
-      nrec += __builtin_amdgcn_readlane(inc_ne, 63);
     }
-    if (lane == 0) {
+    if (hl == 0 && act) {
       seg_cnt[s] = run;
       seg_nrec[s] = nrec;
       if (run > (int64_t(1) << 30) || band_hi - band_lo > (int64_t(1) << 30)) err[0] = 1;
@@ -438,44 +437,38 @@ __device__ __forceinline__ int64_t perm64(int64_t v, int dst) {  // ds_permute: 
 // ticket in band-major order (every node's segment of band 0, then band 1, ...)
 // so the band's rule-major fire lists are read from L2 by all of them.  A
 // wave reads its segment's pair records (k_seg_records: rule, first position,
-// band-relative list index) 64 at a time, lane i holding record i, the next
-// chunk in flight.  The output is filled in aligned 64-event blocks, a batch
-// of kNodeBatch blocks at a time, each block placed on its own: the records
-// starting in it mark their first lane in the block's LDS row (tagged, no
-// clearing); lane l's record = (records starting before the block, one
-// ballot over the sorted starts) - 1 + popcount(marks at lanes <= l); its
-// list index and rule come from that record's lane (ds_bpermute).  The
-// batch's gathers are issued together, then its stores.  A block shared with
-// the next chunk of the same segment is carried in registers; only blocks at
-// segment edges are stored partially.
-// V (diagnostic build only): 1 = no gather (synthetic values), 2 = no stores,
-// 4 = no per-block placement (stores of zeros), 8 = no rule-index stores.
-#ifndef CG_NODE_BATCH
-#define CG_NODE_BATCH 4
-#endif
-constexpr int kNodeBatch = CG_NODE_BATCH;  // blocks whose gathers are in flight together
-#ifndef CG_NODE_DEPTH
-#define CG_NODE_DEPTH 2
-#endif
-constexpr int kNodeDepth = CG_NODE_DEPTH;  // batches in flight (register sets)
-#ifndef CG_NODE_CONFINE
-#define CG_NODE_CONFINE 1
-#endif
-constexpr bool kNodeConfine = CG_NODE_CONFINE;  // gathers waited for in their own branch
-#ifndef CG_NODE_RUNS
-#define CG_NODE_RUNS 1
-#endif
-constexpr bool kNodeRuns = CG_NODE_RUNS;  // blocks owned by one record stored straight from it
+// x, stride) 64 at a time, lane i holding record i, the next chunk in flight.
+// The output is filled in aligned 64-event blocks:
+//   runs   a block one record owns entirely (no record starts inside it) is
+//          stored straight from that record: a progression's fires are
+//          t0 + x + p * stride, so a run of such blocks costs two stores and
+//          an add per block (other records: one gather per block);
+//   one()  a block where records start, and the chunk's first and last blocks
+//          (shared with the neighbouring chunk, or at the segment's edges):
+//          the records starting in it mark their first lane in an LDS row
+//          (tagged, no clearing); lane l's record = (records starting before
+//          the block: one ballot over the sorted starts) - 1 + popcount(marks
+//          at lanes <= l); its x, stride and rule come from that record's lane
+//          (ds_bpermute).  A block shared with the next chunk is carried in
+//          registers; only blocks at segment edges are stored partially.
+// Gathers are waited for where they are issued: a wave's loads and stores
+// retire in issue order, so a wait after a join would drain its stores on
+// every block.
+// V (diagnostic build only): 1 = no gather (the index as the value),
+// 2 = no stores, 8 = no rule-index stores.
 #ifndef CG_NODE_STORE
 #define CG_NODE_STORE 2
 #endif
 // Output stores: 0 plain, 1 sc1 (relaxed agent-scope atomic stores), 2 nt.
 // Plain stores keep the written lines in the XCD's L2; nt (streaming) stores
 // were the fastest on one box (pernode writer 2.36 ms vs 2.60 sc1, 2.71
-// plain, profiles/r02_ab_node_store.json): the writer waits for its own
-// stores whenever it needs a load, and streaming stores retire soonest.
-template <class T>
+// plain, profiles/r02_ab_node_store.json).
+template <int V, class T>
 __device__ __forceinline__ void out_store(T* p, T v) {
+  if (V & 2) {
+    asm volatile("" ::"v"(v));
+    return;
+  }
 #if CG_NODE_STORE == 2
   __builtin_nontemporal_store(v, p);
 #elif CG_NODE_STORE == 1
@@ -484,11 +477,7 @@ __device__ __forceinline__ void out_store(T* p, T v) {
   *p = v;
 #endif
 }
-#ifndef CG_NODE_UNIFORM
-#define CG_NODE_UNIFORM 1
-#endif
-constexpr bool kNodeUniform = CG_NODE_UNIFORM;  // readlane path for batches without inner record starts
-constexpr int kNodeMajorDefault = 0;      // writer task order: 0 band-major, 1 node-major
+constexpr int kNodeMajorDefault = 0;  // writer task order: 0 band-major, 1 node-major
 
 template <int V>
 __global__ __launch_bounds__(256) void k_node_write(
@@ -497,12 +486,12 @@ __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times, int32_t N, int32_t K,
     int32_t B, int64_t cap, uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time,
     int32_t* __restrict__ out_rule, int node_major) {
-  // per wave, one 128-slot row per block of a batch (slots 64..127: the
-  // writes of lanes that mark nothing); tags only grow, so no clearing
-  __shared__ uint32_t marks_all[4][kNodeBatch * 128];
+  // per wave one 128-slot mark row (slots 64..127: the writes of lanes that
+  // mark nothing); tags only grow, so no clearing
+  __shared__ uint32_t marks_all[4][128];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint32_t* marks = marks_all[wave];
-  for (int u = 0; u < kNodeBatch; u++) marks[u * 128 + lane] = 0u;
+  marks[lane] = 0u;
   uint32_t tag = 0;
   const int64_t NK = int64_t(N) * K;
   if (seg_pos[NK] > cap) return;  // output too small: the host grows it and relaunches
@@ -514,8 +503,7 @@ __global__ __launch_bounds__(256) void k_node_write(
     if (lane == 0) t = atomicAdd(tickets + grp * kTicketStride, 1u);
     return grp + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
   };
-  // a task's descriptor, loaded one task ahead by lanes 0..4 (vector loads:
-  // they neither wait on nor hold up the LDS counter)
+  // a task's descriptor, loaded one task ahead by lanes 0..4
   auto desc = [&](int64_t t) -> int64_t {
     if (t >= NK) return 0;
     const int32_t k = node_major ? int32_t(t % K) : int32_t(t / N);
@@ -566,232 +554,75 @@ __global__ __launch_bounds__(256) void k_node_write(
       const int32_t qw = __builtin_amdgcn_readlane(dst, 0);
       if (w + 64 < nrec) fetch(w + 64);
       const bool live = lane < nc;
-      // blocks in batches, each placed on its own: the records starting in
-      // block u mark their first lane in LDS row u (the others write a slot of
-      // their own past 64), one wave barrier for the batch; lane l's record =
-      // (records starting before the block: a ballot, the records are sorted)
-      // - 1 + (marks at lanes <= l).  No block waits on the one before it.
-      // A lane of a progression record computes its fire here; the others
-      // get a gather index (gi >= 0) and are filled by gather().
-      auto place = [&](int32_t bq, int32_t (&gi)[kNodeBatch], int32_t (&rvs)[kNodeBatch],
-                       int64_t (&vals)[kNodeBatch]) {
+      auto one = [&](int32_t b) {
         tag++;
-        // No record starting strictly inside a block of the batch (a long
-        // run, e.g. an every-second rule's 3600 fires): every block has one
-        // owner for all its lanes, read with readlane -- no marks, no barrier.
-        const bool uni = kNodeUniform && !(V & 4) &&
-                         __ballot(live && dst > bq && dst < bq + 64 * kNodeBatch && (dst & 63) != 0) == 0;
-        if (!(V & 4) && !uni) {
-#pragma unroll
-          for (int u = 0; u < kNodeBatch; u++) {
-            const int32_t b = bq + 64 * u;
-            const bool mark = live && dst >= b && dst < b + 64;
-            marks[u * 128 + (mark ? dst - b : 64 + lane)] = tag;
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const bool mark = live && dst >= b && dst < b + 64;
+        marks[mark ? dst - b : 64 + lane] = tag;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int32_t q = b + lane;
+        const uint64_t M = __ballot(marks[lane] == tag);
+        const int before = __popcll(__ballot(live && dst < b));
+        int own = before - 1 + __popcll(M & le);
+        own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
+        const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
+        const int32_t sv = __builtin_amdgcn_ds_bpermute(own << 2, sst);
+        int32_t rv = __builtin_amdgcn_ds_bpermute(own << 2, rr);
+        const bool in = q >= qw && q < we;
+        int64_t val = in && sv != 0 ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
+        const int32_t gi = in && sv == 0 ? q + dl - q_lo : -1;
+        if (__ballot(gi >= 0)) {  // waited for here, not after the branch
+          if (gi >= 0) val = (V & 1) ? int64_t(gi) : tb[gi];
+          asm volatile("" : "+v"(val));
         }
-#pragma unroll
-        for (int u = 0; u < kNodeBatch; u++) {
-          const int32_t b = bq + 64 * u;
-          gi[u] = -1;  // band index of this lane's fire (-1: none to gather)
-          rvs[u] = 0;
-          vals[u] = 0;
-          if (b >= we || (V & 4)) continue;
-          const int32_t q = b + lane;
-          int32_t dl, sv;
-          if (uni) {
-            int own = __popcll(__ballot(live && dst <= b)) - 1;
-            own = own < 0 ? 0 : own;
-            dl = __builtin_amdgcn_readlane(dlt, own);
-            sv = __builtin_amdgcn_readlane(sst, own);
-            rvs[u] = __builtin_amdgcn_readlane(rr, own);
-          } else {
-            const uint64_t M = __ballot(marks[u * 128 + lane] == tag);
-            const int before = __popcll(__ballot(live && dst < b));
-            int own = before - 1 + __popcll(M & le);
-            own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
-            dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
-            sv = __builtin_amdgcn_ds_bpermute(own << 2, sst);
-            rvs[u] = __builtin_amdgcn_ds_bpermute(own << 2, rr);
+        if (b == pq) {  // lanes of the previous chunk
+          val = q < qw ? ptime : val;
+          rv = q < qw ? prule : rv;
+        }
+        if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
+          if ((b >= q_lo && b + 64 <= q_hi) || (q >= q_lo && q < q_hi)) {  // whole, or a segment edge
+            out_store<V>(ot + q, val);
+            if (!(V & 8)) out_store<V>(orl + q, rv);
           }
-          const bool in = q >= qw && q < we;
-          gi[u] = in && sv == 0 ? q + dl - q_lo : -1;
-          vals[u] = in && sv != 0 ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
+          pq = -1;
+        } else {  // carried into the next chunk
+          pq = b;
+          ptime = val;
+          prule = rv;
         }
       };
-      auto gather = [&](const int32_t (&gi)[kNodeBatch], int64_t (&vals)[kNodeBatch]) {
-#pragma unroll
-        for (int u = 0; u < kNodeBatch; u++)
-          if (gi[u] >= 0) vals[u] = (V & 1) ? int64_t(gi[u]) : tb[gi[u]];
-      };
-      auto store = [&](int32_t bq, const int32_t (&gi)[kNodeBatch], const int64_t (&vals)[kNodeBatch],
-                       const int32_t (&rvs)[kNodeBatch]) {
-#pragma unroll
-        for (int u = 0; u < kNodeBatch; u++) {
-          const int32_t b = bq + 64 * u;
-          if (b >= we) break;
-          const int32_t q = b + lane;
-          int64_t val = vals[u];
-          int32_t rv = rvs[u];
-          if (b == pq) {  // lanes of the previous chunk
-            val = q < qw ? ptime : val;
-            rv = q < qw ? prule : rv;
-          }
-          if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
-            if (V & 2) {
-              asm volatile("" ::"v"(val), "v"(rv));
-            } else if (b >= q_lo && b + 64 <= q_hi) {  // interior block: whole stores
-              out_store(ot + q, val);
-              if (!(V & 8)) out_store(orl + q, rv);
-            } else if (q >= q_lo && q < q_hi) {  // a segment edge
-              out_store(ot + q, val);
-              if (!(V & 8)) out_store(orl + q, rv);
-            }
-            pq = -1;
-          } else {
-            pq = b;
-            ptime = val;
-            prule = rv;
-          }
+      const int32_t b0 = qw & ~63, bl = we & ~63;
+      if (qw & 63) one(b0);
+      for (int32_t b = (qw + 63) & ~63; b < bl;) {
+        const int o = __popcll(__ballot(live && dst <= b)) - 1;  // owner of lane 0 (dst[0] = qw <= b)
+        const int32_t e = o + 1 < nc ? __builtin_amdgcn_readlane(dst, o + 1) : we;
+        if (e < b + 64) {  // a record starts inside
+          one(b);
+          b += 64;
+          continue;
         }
-      };
-      // Software-pipelined over kNodeDepth register sets: batches k + 1 ..
-      // k + depth - 1 are placed and their gathers issued before batch k's
-      // stores.  Vector-memory returns are counted in issue order, so waiting
-      // for gathers issued after a batch of stores would also wait for those
-      // stores' write acknowledgements.
-      constexpr int32_t kStep = 64 * kNodeBatch;
-      if (kNodeRuns && V == 0) {
-        // Runs.  A block that one record owns entirely (no record starts
-        // inside it) is stored straight from that record: a progression's
-        // fires are t0 + x + p * stride, so a run of such blocks costs two
-        // stores and an add per block.  Blocks where records start, and the
-        // chunk's first and last blocks (shared with the neighbouring chunk
-        // or at the segment's edges), go through one(): LDS start marks,
-        // bpermute of the lane's record, the carry and the edge stores.
-        auto one = [&](int32_t b) {
-          tag++;
-          const bool mark = live && dst >= b && dst < b + 64;
-          marks[mark ? dst - b : 64 + lane] = tag;
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          const int32_t q = b + lane;
-          const uint64_t M = __ballot(marks[lane] == tag);
-          const int before = __popcll(__ballot(live && dst < b));
-          int own = before - 1 + __popcll(M & le);
-          own = own < 0 ? 0 : (own >= nc ? nc - 1 : own);
-          const int32_t dl = __builtin_amdgcn_ds_bpermute(own << 2, dlt);
-          const int32_t sv = __builtin_amdgcn_ds_bpermute(own << 2, sst);
-          int32_t rv = __builtin_amdgcn_ds_bpermute(own << 2, rr);
-          const bool in = q >= qw && q < we;
-          int64_t val = in && sv != 0 ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
-          const int32_t gi = in && sv == 0 ? q + dl - q_lo : -1;
-          if (__ballot(gi >= 0)) {  // waited for here, not after the branch
-            if (gi >= 0) val = tb[gi];
+        const int32_t bend = (e & ~63) < bl ? (e & ~63) : bl;  // blocks [b, bend) all o's
+        const int32_t dl = __builtin_amdgcn_readlane(dlt, o), sv = __builtin_amdgcn_readlane(sst, o);
+        const int32_t rv = __builtin_amdgcn_readlane(rr, o);
+        if (sv != 0) {
+          int64_t val = t0 + int64_t(dl) + int64_t(b + lane - q_lo) * sv;
+          const int64_t step = int64_t(64) * sv;
+          for (; b < bend; b += 64, val += step) {
+            out_store<V>(ot + b + lane, val);
+            if (!(V & 8)) out_store<V>(orl + b + lane, rv);
+          }
+        } else {
+          for (; b < bend; b += 64) {
+            const int32_t gi = b + lane + dl - q_lo;
+            int64_t val = (V & 1) ? int64_t(gi) : tb[gi];
             asm volatile("" : "+v"(val));
-          }
-          if (b == pq) {  // lanes of the previous chunk
-            val = q < qw ? ptime : val;
-            rv = q < qw ? prule : rv;
-          }
-          if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
-            if (b >= q_lo && b + 64 <= q_hi) {
-              out_store(ot + q, val);
-              out_store(orl + q, rv);
-            } else if (q >= q_lo && q < q_hi) {  // a segment edge
-              out_store(ot + q, val);
-              out_store(orl + q, rv);
-            }
-            pq = -1;
-          } else {  // carried into the next chunk
-            pq = b;
-            ptime = val;
-            prule = rv;
-          }
-        };
-        const int32_t b0 = qw & ~63, bl = we & ~63;
-        if (qw & 63) one(b0);
-        for (int32_t b = (qw + 63) & ~63; b < bl;) {
-          const int o = __popcll(__ballot(live && dst <= b)) - 1;  // owner of lane 0 (dst[0] = qw <= b)
-          const int32_t e = o + 1 < nc ? __builtin_amdgcn_readlane(dst, o + 1) : we;
-          if (e < b + 64) {  // a record starts inside
-            one(b);
-            b += 64;
-            continue;
-          }
-          const int32_t bend = (e & ~63) < bl ? (e & ~63) : bl;  // blocks [b, bend) all o's
-          const int32_t dl = __builtin_amdgcn_readlane(dlt, o), sv = __builtin_amdgcn_readlane(sst, o);
-          const int32_t rv = __builtin_amdgcn_readlane(rr, o);
-          if (sv != 0) {
-            int64_t val = t0 + int64_t(dl) + int64_t(b + lane - q_lo) * sv;
-            const int64_t step = int64_t(64) * sv;
-            for (; b < bend; b += 64, val += step) {
-              out_store(ot + b + lane, val);
-              out_store(orl + b + lane, rv);
-            }
-          } else {
-            for (; b < bend; b += 64) {
-              int64_t val = tb[b + lane + dl - q_lo];
-              asm volatile("" : "+v"(val));
-              out_store(ot + b + lane, val);
-              out_store(orl + b + lane, rv);
-            }
-          }
-        }
-        if ((we & 63) && (bl != b0 || !(qw & 63))) one(bl);
-        continue;
-      }
-      if (kNodeConfine) {
-        // Fires of progression records need no load, so a batch normally
-        // issues only stores.  Gathers (other rules) are issued and waited for
-        // inside a wave-uniform branch of their own: waiting for a load waits
-        // for every store issued before it, and a wait after the branch would
-        // drain the wave's stores on every batch.
-        for (int32_t bq = qw & ~63; bq < we; bq += kStep) {
-          int32_t gi[kNodeBatch], rv[kNodeBatch];
-          int64_t v[kNodeBatch];
-          place(bq, gi, rv, v);
-          bool need = false;
-#pragma unroll
-          for (int u = 0; u < kNodeBatch; u++) need |= gi[u] >= 0;
-          if (__ballot(need)) {
-            gather(gi, v);
-#pragma unroll
-            for (int u = 0; u < kNodeBatch; u++) asm volatile("" : "+v"(v[u]));
-          }
-          store(bq, gi, v, rv);
-        }
-        continue;
-      }
-      constexpr int D = kNodeDepth;
-      int32_t gi[D][kNodeBatch], rv[D][kNodeBatch];
-      int64_t v[D][kNodeBatch];
-      int32_t bq = qw & ~63;
-#pragma unroll
-      for (int s = 0; s + 1 < D; s++)
-        if (bq + s * kStep < we) {
-          place(bq + s * kStep, gi[s], rv[s], v[s]);
-          gather(gi[s], v[s]);
-        }
-      for (bool more = true; more;) {
-#pragma unroll
-        for (int s = 0; s < D; s++) {  // set s holds the batch at bq
-          const int nx = (s + D - 1) % D;
-          if (bq + (D - 1) * kStep < we) {
-            place(bq + (D - 1) * kStep, gi[nx], rv[nx], v[nx]);
-            gather(gi[nx], v[nx]);
-          }
-          store(bq, gi[s], v[s], rv[s]);
-          bq += kStep;
-          if (bq >= we) {
-            more = false;
-            break;
+            out_store<V>(ot + b + lane, val);
+            if (!(V & 8)) out_store<V>(orl + b + lane, rv);
           }
         }
       }
+      if ((we & 63) && (bl != b0 || !(qw & 63))) one(bl);
     }
   }
 }
@@ -1033,7 +864,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   // the writer reads the total on the device and does nothing if it exceeds
   // the output capacity (first call or a larger result: grow, relaunch)
 #ifdef CG_DIAG
-  static const int variant = [] {  // diagnostic: 1 no gather, 2 no stores, 3 neither
+  static const int variant = [] {  // diagnostic: 1 no gather, 2 no stores, 3 neither, 8 no rule stores
     const char* e = getenv("CG_NODE_VARIANT");
     return e ? atoi(e) : 0;
   }();
@@ -1063,9 +894,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
         case 1: CG_NW(1); break;
         case 2: CG_NW(2); break;
         case 3: CG_NW(3); break;
-        case 4: CG_NW(4); break;
         case 8: CG_NW(8); break;
-        case 12: CG_NW(12); break;
         default: CG_NW(0); break;
       }
 #undef CG_NW
