@@ -69,6 +69,29 @@ def pmc_traffic(name, kernel, rules, events):
     return None
 
 
+def store_ceiling(nbytes, dev, achieved_gbps, reps=5):
+    """Fill rate of `nbytes` of HBM on this box (torch's vectorized fill
+    kernel over one buffer, HIP events, mean of `reps` after a warm-up) and
+    the kernel's achieved rate as a fraction of it: the store ceiling the
+    output-bound kernels are compared with, beside the 8 TB/s nominal peak."""
+    import torch
+    buf = torch.empty(nbytes // 8, dtype=torch.int64, device=dev)
+    buf.fill_(1)
+    torch.cuda.synchronize(dev)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for i in range(reps):
+        buf.fill_(i)
+    b.record()
+    torch.cuda.synchronize(dev)
+    ms = a.elapsed_time(b) / reps
+    gbps = buf.numel() * 8 / ms / 1e6
+    del buf
+    torch.cuda.empty_cache()
+    return {"kind": "torch fill_ of the kernel's output bytes (one int64 buffer)", "bytes": nbytes,
+            "ms": ms, "GBps": gbps, "frac_of_ceiling": achieved_gbps / gbps if gbps > 0 else None}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -501,6 +524,12 @@ def main():
         traffic = pmc_traffic("pmc_traffic.json", kname, R, E) if wl == "config2" else None
     achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
 
+    # the achievable store rate on this box, beside the nominal peak: a
+    # vectorized fill of the same output bytes (outside the timed region)
+    ceiling = None
+    if rank == 0 and wl in ("config2", "pernode") and not args.diagnostic:
+        ceiling = store_ceiling(int(E * 12 if pn else E * 8), torch.device("cuda", local), achieved)
+
     cpu = None
     if world == 1 and args.cpu_sample != 0 and pn:
         a_last = list(range(t0, t1, W))[-1]
@@ -550,6 +579,7 @@ def main():
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
             "algo_bytes_per_launch": algo_bytes,
+            "store_ceiling": ceiling,
         },
         "cpu_baseline": cpu,
         "step_wall_ms": {"min": min(step_wall) * 1e3, "p50": float(np.median(step_wall)) * 1e3,
