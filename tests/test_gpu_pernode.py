@@ -176,3 +176,55 @@ def test_per_node_time_ordered_vs_oracle(eng, zone, t0, hours):
         assert np.array_equal(rule2[a:b], exp_r[order]), n
         checked += b - a
     assert checked == len(time) > 1000
+
+
+PROGRESSION_MIX = ["* * * * * *", "*/13 * * * * *", "@every 7s", "@every 1h", "@every 90m", "0 0 * * * *",
+                   "0 30 9 * * *", "0 0 0 * * *", "0 */20 * * * *", "0 7,30,45 * * * *", "0 0 12 * * 1",
+                   "0 0 0 30 2 *", "15 * * * * *"]
+
+
+def progression_rules(R, n_nodes):
+    """Rules on two nodes each (no groups): rule i on nodes i % N and (7i + 1) % N."""
+    from cronsun_amd.engine import RulesIn
+    nids = np.stack([np.arange(R) % n_nodes, (7 * np.arange(R) + 1) % n_nodes], 1)
+    nids = np.sort(nids, 1)
+    keep = [sorted(set(p)) for p in nids.tolist()]
+    nid_off = np.zeros(R + 1, np.int64)
+    nid_off[1:] = np.cumsum([len(k) for k in keep])
+    z = np.zeros(R + 1, np.int64)
+    return RulesIn(n_nodes, 0, R, R, group_off=np.zeros(1, np.int64), group_nodes=np.zeros(0, np.int32),
+                   group_exists=np.zeros(0, np.uint8), rule_job=np.arange(R, dtype=np.int32), nid_off=nid_off,
+                   nids=np.concatenate([np.array(k, np.int32) for k in keep]), gid_off=z,
+                   gids=np.zeros(0, np.int32), ex_off=z, ex=np.zeros(0, np.int32),
+                   job_pause=np.zeros(R, np.uint8))
+
+
+@pytest.mark.parametrize("zone,t0", [("UTC", synth.T0_2026 + 64 * DAY + 1234),
+                                     ("America/New_York", 1772953200 - 36 * 3600)])
+def test_per_node_progressions_vs_oracle(eng, zone, t0):
+    """The per-node writer's computed fires (k_rule_info / k_seg_records
+    progression records: t0 + x + p * stride) against the oracle: every-second,
+    @every, hourly, daily (a 23/25-h step across the NY DST change breaks the
+    progression), weekly, never-firing and non-progression rules, over 3 days
+    and 3 rule bands, with every-second rules early in a node's band so the
+    positions of later daily rules overflow the record's 32-bit x (those fall
+    back to gathers)."""
+    R, N = 2600, 6
+    specs = [PROGRESSION_MIX[1 + i % (len(PROGRESSION_MIX) - 1)] for i in range(R)]
+    for i in (0, 1, 1030, 2100):  # a few every-second rules (259 200 fires each), early in bands
+        specs[i] = PROGRESSION_MIX[0]
+    rin = progression_rules(R, N)
+    scheds = [cron.Parse(s) for s in specs]
+    t1 = t0 + 3 * DAY
+    node_off, time, rule = eng.expand_per_node(scheds, product_zone(zone), t0, t1, rin, _lib.EXCLUDE_NONE)
+    arr = O.sched_array(oracle_parse_all(specs))
+    eo, et = O.expand_batch(arr, t0, t1, oracle_zone(zone))
+    rn = oracle_rule_nodes(rin, _lib.EXCLUDE_NONE)
+    per_node = [[] for _ in range(N)]
+    for r in range(R):
+        for n in rn[r]:
+            per_node[n].append(r)
+    for n in range(N):
+        exp_t, exp_r = O.node_list(eo, et, per_node[n])
+        assert np.array_equal(time[node_off[n]:node_off[n + 1]], exp_t), n
+        assert np.array_equal(rule[node_off[n]:node_off[n + 1]], exp_r), n
