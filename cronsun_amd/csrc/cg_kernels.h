@@ -53,11 +53,28 @@ static_assert(CG_SUPER_SHIFT_SMALL >= 6 && CG_SUPER_SHIFT_LARGE >= 6, "slices ar
 __host__ __device__ inline int super_shift(int64_t cap) {
   return cap >= (int64_t(1) << 31) ? CG_SUPER_SHIFT_LARGE : CG_SUPER_SHIFT_SMALL;
 }
+// Short windows.  Fewer than kUSlices position slices (E < 2^(shift + 14):
+// a tick loop's next minute or hour) leave most writer waves idle, and a
+// slice then stretches over thousands of runs, most of them empty (a 1-min
+// window of 1M rules: 338 k fires in 1M runs).  The writer's slices are then
+// cut in cost space instead: run j costs its fires + 1, u_j = run_off[j] + j,
+// slice c starts at the position of u = c * 2^s rounded down to a 64-event
+// block (k_chunk_map_u), with s the smallest shift (>= 6) giving at most
+// kUSlices slices.  Host and kernels decide the mode from E on the device.
+constexpr int64_t kUSlices = 16384;
+__host__ __device__ inline bool u_mode(int64_t E, int64_t cap) { return (E >> super_shift(cap)) < kUSlices; }
+__host__ __device__ inline int u_shift(int64_t U) {
+  int s = 6;
+  while ((U >> s) >= kUSlices) s++;
+  return s;
+}
 // slice-map entries for an output capacity: the map, 2 sentinels, the ticket
-// counters and 8 debug words
-inline int64_t slice_map_words(int64_t cap) {
+// counters, 8 debug words, then the cost-space map ({first position, first
+// run} per slice and one past the last)
+__host__ __device__ inline int64_t u_map_base(int64_t cap) {
   return (cap >> super_shift(cap)) + 2 + kTicketWords + 8;
 }
+inline int64_t slice_map_words(int64_t cap) { return u_map_base(cap) + 2 * (kUSlices + 2); }
 
 
 size_t plan_lds_bytes(const PlanArgs& p);
@@ -123,6 +140,10 @@ void launch_scan_runs(const int32_t* run_count, int64_t* run_off, int64_t R, int
 // on the device (no host sync) and do nothing when E > cap
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
                       hipStream_t st);
+// the cost-space slice map of a short window (u_mode; nothing otherwise);
+// launched by launch_scan_runs (with chunk_run) and launch_chunk_map
+void launch_chunk_map_u(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
+                        hipStream_t st);
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
                      int64_t nruns, int64_t* chunk_run, int64_t cap, int64_t* times,

@@ -514,6 +514,36 @@ __device__ __forceinline__ int64_t search_run(const int64_t* __restrict__ off, i
   return lo;
 }
 
+// Cost-space slice map of a short window (cg_kernels.h, u_mode): per slice c
+// {P_c, run holding P_c}, P_c = the position of u = c * 2^s rounded down to a
+// 64-event block; entry nsl = {E, last run}.  E is read on the device.
+__global__ void k_chunk_map_u(const int64_t* __restrict__ run_off, int64_t nruns, int64_t cap,
+                              int64_t* __restrict__ chunk_run) {
+  const int64_t E = run_off[nruns];
+  if (E > cap || !u_mode(E, cap)) return;
+  const int64_t U = E + nruns;
+  const int s = u_shift(U);
+  const int64_t nsl = (U + (int64_t(1) << s) - 1) >> s;
+  int64_t* m = chunk_run + u_map_base(cap);
+  for (int64_t c = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; c <= nsl; c += int64_t(gridDim.x) * blockDim.x) {
+    int64_t P = E, jr = nruns - 1;
+    if (c < nsl) {
+      const int64_t u = c << s;
+      int64_t lo = 0, hi = nruns - 1;  // the run whose cost range holds u: largest j with off_j + j <= u
+      while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (run_off[mid] + mid <= u) lo = mid;
+        else hi = mid - 1;
+      }
+      const int64_t pos = min(run_off[lo] + (u - run_off[lo] - lo), run_off[lo + 1]);
+      P = pos & ~int64_t(63);
+      jr = search_run(run_off, 0, nruns - 1, P);
+    }
+    m[2 * c] = P;
+    m[2 * c + 1] = jr;
+  }
+}
+
 // first run touched by each output slice (2^super_shift(cap) events); E is read on the device
 // so the launch needs no host sync (grid sized by capacity, extra threads exit)
 // (chunk_run holds slice_map_words(cap) entries: the map, then the
@@ -879,7 +909,11 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   if (E > cap) return;  // output buffer too small: host grows it and relaunches
   const int sh = super_shift(cap);
   const int64_t sup = int64_t(1) << sh;
-  const int64_t nsup = (E + sup - 1) >> sh;
+  // short windows: slices from the cost-space map (k_chunk_map_u)
+  const bool um = u_mode(E, cap);
+  const int64_t* umap = chunk_run + u_map_base(cap);
+  const int64_t nsup = um ? ((E + nruns + (int64_t(1) << u_shift(E + nruns)) - 1) >> u_shift(E + nruns))
+                          : (E + sup - 1) >> sh;
   int64_t woff = INT64_MAX;  // this lane's window run: offset, count
   int32_t wcnt = 0;
   int64_t jend = nruns;  // runs the current slice can touch: [.., jend)
@@ -956,14 +990,19 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   const uint64_t k_start = clk();
   for (int64_t c = take(); c < nsup;) {
     const int64_t c_next = take();
-    int64_t pos = c << sh;  // multiple of 64: every store below is a whole 512 B block
-    const int64_t S1 = E - pos < sup ? E : pos + sup;
+    // slice start: a multiple of 64, so every store below is a whole 512 B block
+    int64_t pos = um ? umap[2 * c] : c << sh;
+    const int64_t S1 = um ? umap[2 * c + 2] : (E - pos < sup ? E : pos + sup);
+    if (pos >= S1) {  // a cost-space slice of empty runs only
+      c = c_next;
+      continue;
+    }
     uint64_t t_a = clk();
     if (V & 64) {  // diagnostic: plain fill of the slice (with bit 3: + the skeleton's reads)
       for (int64_t b = pos + lane; b < S1; b += 64) put<V>(times + b, b);
     }
-    int64_t jw = chunk_run[c];  // run_off[jw] <= pos
-    jend = chunk_run[c + 1] + 1;  // the run holding S1 (or the last run)
+    int64_t jw = um ? umap[2 * c + 1] : chunk_run[c];  // run_off[jw] <= pos
+    jend = (um ? umap[2 * c + 3] : chunk_run[c + 1]) + 1;  // the run holding S1 (or the last run)
     load_window(jw);
     if (V & 32) {
       st_win += clk() - t_a;
@@ -1615,6 +1654,14 @@ void launch_scan_runs(const int32_t* run_count, int64_t* run_off, int64_t R, int
                       int64_t* offsets, int64_t* res, unsigned long long* stuck,
                       int64_t* chunk_run, int64_t cap, hipStream_t st) {
   scan_impl(run_count, run_off, R * G, temp, RunTail{offsets, res, stuck, G, chunk_run, cap}, st);
+  if (chunk_run) launch_chunk_map_u(run_off, R * G, cap, chunk_run, st);
+}
+
+void launch_chunk_map_u(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
+                        hipStream_t st) {
+  if (nruns <= 0) return;
+  hipLaunchKernelGGL(k_chunk_map_u, dim3(unsigned((kUSlices + 1 + 255) / 256)), dim3(256), 0, st, run_off,
+                     nruns, cap, chunk_run);
 }
 
 void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_t* chunk_run,
@@ -1622,6 +1669,7 @@ void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_
   int64_t max_sup = (cap >> super_shift(cap)) + 1;
   hipLaunchKernelGGL(k_chunk_map, dim3(grid_for(max_sup + 1, 256, 4096)), dim3(256), 0, st,
                      run_off, nruns, cap, chunk_run);
+  launch_chunk_map_u(run_off, nruns, cap, chunk_run, st);
 }
 
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
