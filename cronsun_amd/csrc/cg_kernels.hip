@@ -691,6 +691,16 @@ constexpr int kBatch = CG_WRITE_BATCH;  // blocks computed before their stores a
 #define CG_WRITE_TAKE 1
 #endif
 constexpr int kTake = CG_WRITE_TAKE;  // writer slices per ticket atomic
+#ifndef CG_WRITE_MIXED
+#define CG_WRITE_MIXED 1
+#endif
+constexpr bool kMixedBlocks = CG_WRITE_MIXED;  // blocks holding several runs filled lane-parallel
+// 64-bit ds_bpermute (lane src's value; src taken mod 64)
+__device__ __forceinline__ int64_t bperm64_w(int64_t v, int src) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, int(uint32_t(v)));
+  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, int(uint32_t(uint64_t(v) >> 32)));
+  return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
+}
 
 // Runs the piece [p0, p1) through the block protocol: value() is this lane's
 // current fire, step() advances it by 64 fires.  Full blocks are stored as
@@ -878,6 +888,23 @@ __device__ void coop_every(const WinRun& w, int64_t roff, int64_t p0, int64_t p1
   drive<V, false>([&]() { return t; }, [&]() { t += st; }, p0, p1, pd, times);
 }
 
+// Fire k (>= 0) of window run w, for one lane (the per-lane form of
+// coop_every / tiny_cf): @every anchor + (k + 1) D (constantdelay.go:25-27),
+// a walked run's placeholder 0 (k_write_walk writes it), else the k-th
+// closed-form fire from the anchor.
+__device__ __forceinline__ int64_t run_fire(const WinRun& w, const Segment& sg, int64_t k) {
+  if (win_every(w)) return w.anchor + (k + 1) * int64_t(w.sp.sec);
+  if (run_is_walked(sg, w.dmask)) return 0;
+  if (k == 0) return w.anchor;
+  const CFRule c = cf_rule(w.sp);
+  if (k == 1) {
+    CFIter it = cf_decode(sg, w.anchor);
+    cf_next(c, w.dmask, it);
+    return cf_value(sg, it);
+  }
+  return cf_value(sg, cf_seek_fast(c, sg, w.dmask, w.anchor, k));
+}
+
 // Persistent closed-form writer.  Waves work independently on 2^super_shift(cap)-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
 // consecutive runs (one coalesced round of loads, staged in its LDS slice;
@@ -1030,6 +1057,43 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       }
       const int64_t roff = rl64(woff, i);
       const int64_t p1 = roff + cnt < S1 ? roff + cnt : S1;
+      const int64_t b = pos & ~int64_t(63);
+      if (kMixedBlocks && !(V & 8) && p1 < b + 64 && p1 < S1) {
+        // The run ends inside this block and the slice goes on: the block
+        // holds several runs.  Fill it lane-parallel -- each lane finds its
+        // run among the window's (largest j with woff[j] <= q) and computes
+        // that run's fire -- instead of run by run.  Needs every run up to
+        // the block's end in this window.
+        const int64_t be = b + 64 < S1 ? b + 64 : S1;
+        const int jl = 63 - __builtin_clzll(__ballot(woff <= be - 1));
+        if (rl64(woff, jl) + rl32(wcnt, jl) >= be) {
+          const int64_t q = b + lane;
+          int j = 0;
+          for (int st = 32; st; st >>= 1) {
+            const int64_t wj = bperm64_w(woff, j + st);
+            if (wj <= q) j += st;
+          }
+          const int64_t rj = bperm64_w(woff, j);
+          int64_t v = 0;
+          if (q >= pos && q < be) {
+            const WinRun& wr = win[j];
+            v = run_fire(wr, segs[win_seg(wr)], q - rj);
+          } else if (q < pos) {
+            v = pd.val;  // earlier runs' fires of this block
+          }
+          if (be == b + 64) {
+            put<V>(times + q, v);
+            pd.blk = -1;
+            pos = be;
+            i = 63 - __builtin_clzll(__ballot(woff <= pos));  // the run holding pos
+          } else {  // the slice ends inside the block
+            pd.blk = b;
+            pd.val = v;
+            pos = be;
+          }
+          continue;
+        }
+      }
       const WinRun& w = win[i];
       const Segment& sg = segs[win_seg(w)];
       t_a = clk();

@@ -344,3 +344,38 @@ def test_starts_near_transitions(eng, zone):
         tau = int(when[i])
         for o in (-3600, -1, 0, 1, 3599, 3601, 18001, 90000):
             check_same(eng, scheds, zone, tau + o, tau + o + 30 * 3600, specs)
+
+
+_SHORT = {}
+
+
+def _short_window_rules(n):
+    """config-2 specs and their oracle parse (cached across the parametrized cases)"""
+    if n not in _SHORT:
+        specs = synth.spec_mix(n, seed=0x5EED)
+        _SHORT[n] = specs, O.sched_array(oracle_parse_all(specs))
+    return _SHORT[n]
+
+
+@pytest.mark.parametrize("width", [60, 3600])
+def test_short_windows_after_a_day(eng, width):
+    """Short windows (the writer's cost-space slices, cg_kernels.h u_mode) of
+    300k config-2 rules, expanded right after a 24-h call grew the output (so the
+    capacity is far above the window's events): the whole rule-major CSR
+    bit-exact against the oracle, at a window start on and off a minute."""
+    n = 300_000
+    specs, oarr = _short_window_rules(n)
+    arr, status = cron.parse_batch(specs)
+    assert (status == 0).all()
+    sp = eng.upload_c(arr, n)
+    eng.expand_device(sp, None, synth.T0_2026, synth.T0_2026 + DAY)
+    from cronsun_amd._lib import check, lib
+    for t0 in (synth.T0_2026 + 7 * 3600, synth.T0_2026 + 7 * 3600 + 37):
+        t1 = t0 + width
+        E = eng.expand_device(sp, None, t0, t1)
+        off = np.empty(n + 1, dtype=np.int64)
+        check(lib().cg_result_copy_offsets(eng._h, off.ctypes.data))
+        times = eng.copy_times(0, E)
+        eo, et = O.expand_batch(oarr, t0, t1, oracle_zone("UTC"), threads=8)
+        assert np.array_equal(off, eo), (width, t0)
+        assert np.array_equal(times, et), (width, t0)
