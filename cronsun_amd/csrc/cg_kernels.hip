@@ -694,6 +694,9 @@ constexpr int kTake = CG_WRITE_TAKE;  // writer slices per ticket atomic
 #ifndef CG_WRITE_MIXED
 #define CG_WRITE_MIXED 1
 #endif
+#ifndef CG_WRITE_SPARE_BLOCKS
+#define CG_WRITE_SPARE_BLOCKS 0
+#endif
 constexpr bool kMixedBlocks = CG_WRITE_MIXED;  // blocks holding several runs filled lane-parallel
 // 64-bit ds_bpermute (lane src's value; src taken mod 64)
 __device__ __forceinline__ int64_t bperm64_w(int64_t v, int src) {
@@ -1761,7 +1764,10 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
   hipLaunchKernelGGL(k_write_lw<0>, dim3(cus * lw_per_cu[key]), dim3((kLwWriters + 1) * 64), lds, st, specs,
                      p, run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
 #else
-  hipLaunchKernelGGL(k_write_cf<0>, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p,
+  // CG_WRITE_SPARE_BLOCKS block slots left to the next pipelined call's
+  // count and scan (they run beside the persistent writer instead of after it)
+  const int nb = std::max(1, n_blocks - CG_WRITE_SPARE_BLOCKS);
+  hipLaunchKernelGGL(k_write_cf<0>, dim3(nb), dim3(kWriteWaves * 64), lds, st, specs, p,
                      run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
 #endif
 #else
