@@ -277,7 +277,8 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
 constexpr int kApRules = 256;
 __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ rule_off,
                                                     const int64_t* __restrict__ times, int64_t R, int64_t t0,
-                                                    int32_t B, RuleInfo* __restrict__ info) {
+                                                    int32_t B, RuleInfo* __restrict__ info,
+                                                    int64_t* __restrict__ err) {
   __shared__ int64_t off[kApRules + 1];
   __shared__ int64_t step[kApRules];
   __shared__ int32_t ok[kApRules];
@@ -285,6 +286,10 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
   const int nr = int(R - r0 < kApRules ? R - r0 : kApRules);
   const int tid = threadIdx.x;
   const int64_t band_lo = rule_off[(r0 / B) * B];  // B is a multiple of kApRules
+  // the writer's 32-bit band-relative indices and k_seg_records' int32
+  // scans need a band to hold < 2^30 events (else the call fails)
+  if (r0 % B == 0 && threadIdx.x == 0 && rule_off[r0 + B < R ? r0 + B : R] - band_lo > (int64_t(1) << 30))
+    err[0] = 1;
   int64_t first = 0, cnt = 0;
   if (tid < nr) {
     const int64_t a = rule_off[r0 + tid];
@@ -317,6 +322,23 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
   }
 }
 
+// Inclusive scan of x within each 32-lane half of the wave, by DPP (no LDS
+// round trips): row_shr 1/2/4/8 inside each 16-lane row, then row_bcast:15
+// adds the last lane of rows 0 and 2 to rows 1 and 3.
+__device__ __forceinline__ int32_t scan_halves(int32_t x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+  return x;
+}
+// lane 31's value in the low half, lane 63's in the high half
+__device__ __forceinline__ int32_t half_total(int32_t incl) {
+  const int32_t lo = __builtin_amdgcn_readlane(incl, 31), hi = __builtin_amdgcn_readlane(incl, 63);
+  return (threadIdx.x & 63) < 32 ? lo : hi;
+}
+
 #ifndef CG_SEG_PAIRS_PER_LANE
 #define CG_SEG_PAIRS_PER_LANE 8
 #endif
@@ -344,67 +366,83 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
                                                       int64_t* __restrict__ err) {
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < kTicketGroups * kTicketStride; i += blockDim.x) tickets[i] = 0;
-  // Two segments per wave, one per half-wave (consecutive nodes of a band):
-  // the kernel is latency-bound (segment bounds -> pair rules -> rule infos
-  // -> records), so two independent chains share each wait.
+  // Two segments per wave, one per half-wave (consecutive nodes of a band),
+  // software-pipelined: the kernel is latency-bound (segment bounds -> pair
+  // rules -> rule infos -> records), so each iteration issues the bounds two
+  // segment pairs ahead, the first round of pair rules one ahead and its own
+  // rule infos together, and waits once.
   constexpr int L = 32;  // lanes per segment
+  constexpr int P = kSegPairsPerLane;
   const int lane = threadIdx.x & 63, hl = lane & (L - 1);
   const int64_t NK = int64_t(N) * K;
   const int64_t nh = int64_t(gridDim.x) * (blockDim.x >> 6) * 2;
-  for (int64_t tw = (blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2; tw < NK; tw += nh) {
+  const uint32_t below = (1u << hl) - 1u;  // lanes of this half before this one
+  struct Seg {
+    int64_t s, p0, p1;
+  };
+  auto bounds = [&](int64_t tw) -> Seg {
     const int64_t t = tw + (lane >> 5);
-    const bool act = t < NK;
-    const int32_t k = act ? int32_t(t / N) : 0, n = act ? int32_t(t - int64_t(k) * N) : 0;
-    const int64_t s = int64_t(n) * K + k;
-    const int64_t p0 = act ? seg_pair[s] : 0, p1 = act ? seg_pair[s + 1] : 0;
-    const int64_t band_lo = rule_off[int64_t(k) * B];
-    const int64_t band_hi = rule_off[int64_t(k + 1) * B < R ? int64_t(k + 1) * B : R];
+    Seg g{-1, 0, 0};
+    if (t < NK) {
+      const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
+      g.s = int64_t(n) * K + k;
+      g.p0 = seg_pair[g.s];
+      g.p1 = seg_pair[g.s + 1];
+    }
+    return g;
+  };
+  // pair u*L + hl of round pc: every load and record store instruction covers
+  // consecutive pairs / records
+  auto rules = [&](const Seg& g, int32_t pc, int32_t (&r)[P]) {
+#pragma unroll
+    for (int u = 0; u < P; u++) {
+      const int64_t pp = g.p0 + pc + u * L + hl;
+      r[u] = pp < g.p1 ? nt_rule[pp] : -1;
+    }
+  };
+  int64_t tw = (blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2;
+  Seg cur = bounds(tw), nxt = bounds(tw + nh);
+  int32_t r[P], rn[P];
+  rules(cur, 0, r);
+  for (; tw < NK; tw += nh) {
+    const Seg nn = bounds(tw + 2 * nh);  // two ahead
+    rules(nxt, 0, rn);                   // the next pair's first round
     int64_t run = 0;  // events of the segment so far
     int32_t nrec = 0;
-    // L*P pairs per round and segment, P consecutive ones per lane: all their
-    // loads in flight together (a segment holds ~180 pairs at config 3's shape)
-    constexpr int P = kSegPairsPerLane;
-    const int32_t len = int32_t(p1 - p0);
+    const int32_t len = int32_t(cur.p1 - cur.p0);
     const int32_t rounds_len = max(__builtin_amdgcn_readlane(len, 0), __builtin_amdgcn_readlane(len, 32));
-    const uint32_t below = (1u << hl) - 1u;  // lanes of this half before this one
     for (int32_t pc = 0; pc < rounds_len; pc += L * P) {
-      // pair u*L + hl of the round: every load and record store instruction
-      // covers consecutive pairs / records
-      int32_t r[P];
+      if (pc > 0) rules(cur, pc, r);  // segments of more than L*P pairs
       RuleInfo g[P];
-#pragma unroll
-      for (int u = 0; u < P; u++) {
-        const int64_t pp = p0 + pc + u * L + hl;
-        r[u] = pp < p1 ? nt_rule[pp] : -1;
-      }
 #pragma unroll
       for (int u = 0; u < P; u++) g[u] = r[u] >= 0 ? info[r[u]] : RuleInfo{0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < P; u++) {
         // events before this pair: half-wave inclusive scan of the counts
-        int64_t incl = g[u].cnt;
-        for (int o = 1; o < L; o <<= 1) {
-          const int64_t y = __shfl_up(incl, o, L);
-          if (hl >= o) incl += y;
-        }
-        const int64_t d = run + incl - g[u].cnt;
+        // (int32: a band holds < 2^30 events, k_rule_info checks)
+        const int32_t incl = scan_halves(g[u].cnt);
+        const int64_t d = run + (incl - g[u].cnt);
         const uint64_t ball = __ballot(g[u].cnt > 0);
         const uint32_t ne = uint32_t(lane < 32 ? ball : ball >> 32);  // this half's non-empty pairs
         if (g[u].cnt > 0) {
-          const int64_t at = p0 + nrec + __popc(ne & below);
+          const int64_t at = cur.p0 + nrec + __popc(ne & below);
           const int64_t x = int64_t(g[u].first) - d * g[u].st;
           const bool prog = g[u].st != 0 && x >= INT32_MIN && x <= INT32_MAX;
           recs[at] = PairRec{r[u], int32_t(d), int32_t(prog ? x : int64_t(g[u].off) - d), prog ? g[u].st : 0};
         }
-        run += __shfl(incl, L - 1, L);  // the half's total
+        run += half_total(incl);
         nrec += __popc(ne);
       }
     }
-    if (hl == 0 && act) {
-      seg_cnt[s] = run;
-      seg_nrec[s] = nrec;
-      if (run > (int64_t(1) << 30) || band_hi - band_lo > (int64_t(1) << 30)) err[0] = 1;
+    if (hl == 0 && cur.s >= 0) {
+      seg_cnt[cur.s] = run;
+      seg_nrec[cur.s] = nrec;
+      if (run > (int64_t(1) << 30)) err[0] = 1;
     }
+    cur = nxt;
+    nxt = nn;
+#pragma unroll
+    for (int u = 0; u < P; u++) r[u] = rn[u];
   }
 }
 
@@ -851,7 +889,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_res_host[1] = 0;  // error flag (nothing of this ctx is in flight here)
   if (R > 0)
     hipLaunchKernelGGL(k_rule_info, dim3(unsigned((R + kApRules - 1) / kApRules)), dim3(256), 0, st,
-                       c->offsets.p, c->times.p, R, t0, B, c->rule_info.p);
+                       c->offsets.p, c->times.p, R, t0, B, c->rule_info.p, c->pn_res_dev + 1);
   if (NK > 0)
     hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
                        c->nt_rule.p, c->offsets.p, c->rule_info.p, N, K, B, R, c->seg_cnt.p, c->seg_nrec.p,
