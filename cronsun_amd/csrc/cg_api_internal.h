@@ -157,10 +157,16 @@ struct cg_ctx {
   // pipelined expansion (cg_async.cpp): two run sets used in turn, count +
   // scan on st_cs, writers on st; as_last = set of the last async result
   // (-1: the last result came from the synchronous path)
-  AsyncSet as[2];
+  // Three run sets: a call's count and scan are enqueued while the writer
+  // two calls back is long done, so they sit ready in the hardware queue and
+  // run in the previous writer's tail instead of racing the next writer's
+  // start (two sets: the count alternately ran before and after that start,
+  // 19 vs 50 us between writers, profiles/r02_ab_async_sets.json)
+  static constexpr int kAsyncSets = 3;
+  AsyncSet as[kAsyncSets];
   int as_next = 0, as_last = -1;
   hipStream_t st_cs = nullptr;
-  hipEvent_t cs_done[2] = {};
+  hipEvent_t cs_done[kAsyncSets] = {};
   int async_rc = 0;  // first error of the calls since the last cg_expand_wait
   std::string async_msg;
   double wr_ms_sum = 0;  // writer (k_write_cf) time of the checked async calls

@@ -4,8 +4,8 @@
 // A synchronous cg_expand_device ends every call with a stream sync (the
 // caller reads the event total) and runs count -> scan -> write in series.
 // cg_expand_device_async enqueues the same kernels and returns: the count and
-// scan of call k run on a second stream, into the run set not read by call
-// k-1's writer, while that writer streams its output; call k's writer then
+// scan of call k run on a second stream, into a run set no queued writer
+// reads (three sets), while call k-1's writer streams its output; call k's writer then
 // follows call k-1's on the ctx stream.  The plan of each call (zone table,
 // segments, day table) is staged through pinned memory of its run set, so a
 // moving T0 costs no stream sync either.  cg_expand_wait drains the pipeline
@@ -71,7 +71,9 @@ int ensure_async(cg_ctx* c) {
 
 // every pending async call finished and checked (errors kept for the next wait)
 int async_drain(cg_ctx* c) {
-  if (!(c->as[0].pending || c->as[1].pending)) return CG_OK;
+  bool any = false;
+  for (const AsyncSet& a : c->as) any = any || a.pending;
+  if (!any) return CG_OK;
   HIPCHK(hipStreamSynchronize(c->st));
   for (AsyncSet& a : c->as) check_set(c, a);
   return CG_OK;
@@ -93,8 +95,8 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   if (rc) return rc;
   const int k = c->as_next;
   AsyncSet& a = c->as[k];
-  // the set was last used two calls ago: its writer must be done before the
-  // host restages its plan or the count stream rewrites its runs
+  // the set was last used kAsyncSets calls ago: its writer must be done
+  // before the host restages its plan or the count stream rewrites its runs
   HIPCHK(hipEventSynchronize(a.written));
   check_set(c, a);
   const int64_t R = int64_t(s->n);
@@ -125,7 +127,7 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
     HIPCHK(hipMemsetAsync(a.offsets.p, 0, (R + 1) * 8, c->st));
     a.res_host[0] = 0;
     a.res_host[1] = -1;
-    c->as_next = k ^ 1;
+    c->as_next = (k + 1) % cg_ctx::kAsyncSets;
     c->as_last = k;
     c->last_R = R;
     c->last_E = 0;
@@ -159,7 +161,7 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   a.R = R;
   a.cap = cap;
   a.pending = true;
-  c->as_next = k ^ 1;
+  c->as_next = (k + 1) % cg_ctx::kAsyncSets;
   c->as_last = k;
   c->last_R = R;
   c->last_E = 0;  // known at cg_expand_wait
