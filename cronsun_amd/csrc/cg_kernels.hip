@@ -334,8 +334,15 @@ __global__ __launch_bounds__(256) void k_dispatch_min(const int64_t* __restrict_
   }
 }
 
+#ifndef CG_COUNT_WPE
+#define CG_COUNT_WPE 0  // > 0: register budget of k_count for that many waves per SIMD (A/B)
+#endif
 template <bool kWalk>
-__global__ __launch_bounds__(256) void k_count(const DSpec* __restrict__ specs, int64_t R,
+__global__ __launch_bounds__(256)
+#if CG_COUNT_WPE
+__attribute__((amdgpu_waves_per_eu(CG_COUNT_WPE)))
+#endif
+void k_count(const DSpec* __restrict__ specs, int64_t R,
                                                 PlanArgs p, int64_t* __restrict__ run_anchor,
                                                 int32_t* __restrict__ run_count,
                                                 uint32_t* __restrict__ run_dmask,
