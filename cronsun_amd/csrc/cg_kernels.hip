@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void k_dispatch_min(const int64_t* __restrict_
 }
 
 #ifndef CG_COUNT_WPE
-#define CG_COUNT_WPE 0  // > 0: register budget of k_count for that many waves per SIMD (A/B)
+#define CG_COUNT_WPE 4  // register budget of k_count: 4 waves per SIMD (walk path 133 -> 128 VGPRs, 24 B spill; DST-day step 2.37 -> 2.12 ms)
 #endif
 template <bool kWalk>
 __global__ __launch_bounds__(256)
