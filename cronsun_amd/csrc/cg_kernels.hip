@@ -1492,7 +1492,14 @@ __global__ __launch_bounds__(kWriteWaves * 64) void k_fill_probe(const int64_t* 
   }
 }
 
-__global__ __launch_bounds__(256) void k_write_walk(const DSpec* __restrict__ specs, int64_t R,
+#ifndef CG_WALK_WPE
+#define CG_WALK_WPE 5  // register budget of k_write_walk: 5 waves per SIMD (98 -> 96 VGPRs, 12 B spill; 0.41 -> 0.37 ms on a DST day)
+#endif
+__global__ __launch_bounds__(256)
+#if CG_WALK_WPE
+__attribute__((amdgpu_waves_per_eu(CG_WALK_WPE)))
+#endif
+void k_write_walk(const DSpec* __restrict__ specs, int64_t R,
                                                      PlanArgs p,
                                                      const int64_t* __restrict__ run_anchor,
                                                      const int32_t* __restrict__ run_count,
