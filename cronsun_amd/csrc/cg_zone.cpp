@@ -371,6 +371,37 @@ ZoneTable build_table(const ZoneRules& z, int64_t lo, int64_t hi) {
   return t;
 }
 
+// Is breakpoint i of table t a "clean" transition -- one the Go walk crosses
+// exactly as the closed form in the local time of each instant does, so it
+// needs no WALK window and no exact walk from T0 (clean
+// transitions)?  Conditions: a one-hour shift (d = o2 - o1 = +-3600) between
+// whole-minute offsets, at a local hour start, whose skipped or repeated local
+// hour lies at least one hour away from local midnight on both sides, with no
+// other breakpoint within three days.  Then (1) every Date call of the walk
+// (midnights, month starts, hour starts) either resolves to its own instant or
+// is an hour-level reset inside a mismatching hour whose other pass mismatches
+// too; (2) the hour, minute and second walks step across tau without missing a
+// wrap (no midnight nearby, minutes continuous); (3) Truncate(Minute) is wall
+// truncation.  America/New_York's, Europe's and Australia's DST changes are
+// clean; Havana's (midnight), Lord_Howe's (30 min), Chatham's (02:45) and
+// Apia's (a day) are not.
+static int64_t floormod_i64(int64_t a, int64_t b) { return a - floordiv64(a, b) * b; }
+
+bool clean_transition(const ZoneTable& t, size_t i) {
+  const int64_t kDay = 86400;
+  const int64_t tau = t.when[i];
+  const int64_t o1 = t.off[i - 1], o2 = t.off[i], d = o2 - o1;
+  if (d != 3600 && d != -3600) return false;
+  if (o1 % 60 != 0 || o2 % 60 != 0) return false;
+  if (floormod_i64(tau + o1, 3600) != 0) return false;
+  const int64_t lo = std::min(tau + o1, tau + o2);  // the skipped / repeated local hour [lo, lo + 3600)
+  const int64_t sod = floormod_i64(lo, kDay);
+  if (sod < 3600 || sod + 3600 > kDay - 3600) return false;
+  if (i > 1 && tau - t.when[i - 1] < 3 * kDay) return false;
+  if (i + 1 < t.when.size() && t.when[i + 1] - tau < 3 * kDay) return false;
+  return true;
+}
+
 Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
   Plan plan;
   const int64_t kDay = 86400;
@@ -378,10 +409,14 @@ Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
   // past T1) may walk up to five years on (spec.go:70-76)
   plan.table = build_table(z, t0 - 64 * kDay, t1 + (6 * 366 + 64) * kDay);
   if (t1 <= t0) return plan;
+  std::vector<char> clean(plan.table.when.size(), 0);
+  for (size_t i = 1; i < plan.table.when.size(); i++) clean[i] = clean_transition(plan.table, i);
   for (size_t i = 1; i < plan.table.when.size(); i++) {
     const int64_t tau = plan.table.when[i];
     // the walk from T0 may reset back across a transition of the last 40 days
-    if (tau > t0 - 40 * kDay && tau <= t0) plan.flags |= kPlanT0Walk;
+    // (harmless across a clean one: its resets land on midnights, month
+    // starts and hour starts Date resolves exactly, or inside a mismatching hour)
+    if (tau > t0 - 40 * kDay && tau <= t0 && !clean[i]) plan.flags |= kPlanT0Walk;
     // a skipped local day (e.g. Pacific/Apia 2011-12-30): AddDate(0,0,1) can
     // stall there, so the last Next must be walked to its end
     if (tau > t0 && plan.table.off[i] - plan.table.off[i - 1] >= kDay) plan.flags |= kPlanFinalWalk;
@@ -408,8 +443,13 @@ Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
   plan.margin = A;
   std::vector<std::pair<int64_t, int64_t>> win;  // (lo, hi] WALK windows
   int64_t prev_tau = INT64_MIN;
+  std::vector<int64_t> cuts;  // clean transitions: a CF span is only cut there, (.., tau - 1] | (tau - 1, ..]
   for (size_t i = 1; i < plan.table.when.size(); i++) {
     const int64_t tau = plan.table.when[i];
+    if (clean[i]) {
+      if (tau - 1 > t0 && tau - 1 < t1) cuts.push_back(tau - 1);
+      continue;
+    }
     const int64_t o1 = plan.table.off[i - 1], o2 = plan.table.off[i], d = o2 - o1;
     int64_t before = (d < 0 && o1 > 0) ? std::min(o1, -d) : 0;
     int64_t after = (d < 0 && o2 < 0) ? std::min(-o2, -d) : 0;
@@ -434,10 +474,13 @@ Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1) {
   }
   auto add_cf = [&](int64_t a, int64_t b) {
     const int64_t kChunk = 30 * kDay;
-    for (int64_t x = a; x < b; x += kChunk) {
+    for (int64_t x = a, xe; x < b; x = xe) {
+      xe = std::min(b, x + kChunk);
+      for (int64_t cut : cuts)
+        if (cut > x && cut < xe) { xe = cut; break; }  // cuts ascend
       Segment s;
       s.a = x;
-      s.b = std::min(b, x + kChunk);
+      s.b = xe;
       s.kind = 0;
       s.off = plan.table.off[0];
       ZoneView zv{plan.table.when.data(), plan.table.off.data(), int32_t(plan.table.when.size())};

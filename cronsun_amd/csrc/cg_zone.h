@@ -70,5 +70,8 @@ struct Plan {
   uint32_t flags = 0;  // kPlanT0Walk | kPlanFinalWalk | kPlanWalkSegs
 };
 Plan build_plan(const ZoneRules& z, int64_t t0, int64_t t1);
+// breakpoint i (>= 1) of t is a clean transition: no WALK window, no exact
+// walk from T0 after it (cg_zone.cpp)
+bool clean_transition(const ZoneTable& t, size_t i);
 
 }  // namespace cg

@@ -85,6 +85,22 @@ int main(int argc, char** argv) {
     for (size_t i : pick)
       for (int64_t o : offs) hz.push_back({nt.when[i] + o, nt.when[i] + o + 30 * 3600});
   }
+  // clean mode: every transition of 2011-2027 that the plan treats as clean
+  // (no WALK window, no exact walk from T0): horizons of 30 h from T0 at
+  // offsets around it, and 24 h from T0 = tau + k days (k = 1..39, the days a
+  // walk from T0 could reset back across it)
+  const bool clean_mode = argc > 4 && std::string(argv[4]) == "clean";
+  int clean_plans = 0;
+  if (clean_mode) {
+    hz.clear();
+    ZoneTable nt = build_table(zr, 1293840000, 1830297600);
+    const int64_t offs[] = {-86400, -7201, -3601, -3600, -3599, -2, -1, 0, 1, 2, 1799, 3599, 3600, 3601, 7199, 7200};
+    for (size_t i = 1; i < nt.when.size(); i++) {
+      if (!clean_transition(nt, i)) continue;
+      for (int64_t o : offs) hz.push_back({nt.when[i] + o, nt.when[i] + o + 30 * 3600});
+      for (int k = 1; k < 40; k += (i % 3) + 1) hz.push_back({nt.when[i] + k * 86400 + 3 * k * 877, nt.when[i] + k * 86400 + 3 * k * 877 + 86400});
+    }
+  }
   if (long_mode)  // three years from 2026; 2095-06-01 .. 2106-06-01 (Feb 29 gap over 2100)
     hz = {{1767571200 - 77, 1767571200 + 1096 * 86400}, {3957984000, 3957984000 + 4018 * 86400}};
   int bad = 0;
@@ -93,6 +109,7 @@ int main(int argc, char** argv) {
     Plan plan = build_plan(zr, t0, t1);
     ZoneView zv{plan.table.when.data(), plan.table.off.data(), int32_t(plan.table.when.size())};
     int G = int(plan.segs.size());
+    if (clean_mode && plan.flags == 0) clean_plans++;
     for (size_t r = 0; r < scheds.size(); r++) {
       DSpec d = pack(scheds[r]);
       std::vector<int64_t> anc(G);
@@ -147,6 +164,7 @@ int main(int argc, char** argv) {
       }
     }
   }
+  if (clean_mode) printf("%s: %d of %zu horizons planned without any exact walk\n", zone, clean_plans, hz.size());
   printf("%s: %d mismatches, %lld events checked\n", zone, bad, total);
   return bad ? 1 : 0;
 }

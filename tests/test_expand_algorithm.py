@@ -61,3 +61,20 @@ def test_host_algorithm_near_transitions(expand_host, zone):
                          text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     assert " 0 mismatches" in out.stdout
+
+
+@pytest.mark.parametrize("zone", ["America/New_York", "Europe/London", "Australia/Sydney", "America/St_Johns",
+                                  "Africa/Casablanca"])
+def test_host_algorithm_clean_transitions(expand_host, zone):
+    """Every clean transition of 2011-2027 (cg_zone.cpp clean_transition: a
+    one-hour shift at a local hour start away from midnight -- the plan cuts
+    the closed form there, with no WALK window and no exact walk from T0):
+    T0 at 16 offsets around it (30-h horizons) and on days 1-39 after it
+    (24-h horizons).  Every such plan must run without an exact walk."""
+    out = subprocess.run([expand_host, zone, "60", "17", "clean"], cwd=ROOT, capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
+    assert " 0 mismatches" in out.stdout
+    line = [l for l in out.stdout.splitlines() if "planned without any exact walk" in l][0]
+    n_clean, n_all = int(line.split(": ")[1].split()[0]), int(line.split(" of ")[1].split()[0])
+    assert n_all > 100 and n_clean == n_all, line

@@ -236,12 +236,13 @@ def test_output_growth_and_reuse():
         check_same(eng, scheds, "UTC", t0, t1)
 
 
-@pytest.mark.parametrize("t0", [1772910000, 1793469600], ids=["ny-spring", "ny-fall"])
+@pytest.mark.parametrize("t0", [1772910000, 1793469600, 1773792000], ids=["ny-spring", "ny-fall", "ny-spring+10d"])
 def test_config2_scale_dst_day(eng, t0):
     """Config 2 at full size in America/New_York over the 24 h centred on the
-    2026 spring-forward / fall-back (the walk path: the transition's WALK
-    window, its crossing walks, the fall-back overlap), bit-exact on a seeded
-    sample that includes every every-second rule."""
+    2026 spring-forward / fall-back (clean transitions: the closed form cut at
+    the transition, the fall-back overlap's repeated hour), and over a day ten
+    days after the spring-forward (a walk from T0 could reset back across it),
+    bit-exact on a seeded sample that includes every every-second rule."""
     n = 1_000_000
     specs = synth.spec_mix(n, seed=0x5EED)
     arr, status = cron.parse_batch(specs)

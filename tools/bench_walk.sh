@@ -1,13 +1,13 @@
 #!/bin/bash
 # Walk-path bench: config 2 (1M rules x 24 h) in America/New_York on the 24 h
 # around the 2026 DST transitions (spring-forward 2026-03-08 07:00Z, fall-back
-# 2026-11-01 06:00Z), plus a kernel trace of each (k_count / k_write_cf /
+# 2026-11-01 06:00Z) and on 2026-03-18 (ten days after the spring-forward), plus a kernel trace of each (k_count / k_write_cf /
 # k_write_walk).   tools/bench_walk.sh <tag>
 set -o pipefail
 OUT=gpurun_out/${1:-walk}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-for day in spring:1772910000 fall:1793469600; do
+for day in spring:1772910000 fall:1793469600 after10d:1773792000; do
   name=${day%%:*}
   t0=${day##*:}
   B="bench.py --zone America/New_York --t0 $t0 --steps 10 --warmup 3"
