@@ -141,6 +141,7 @@ def _declare(L):
         "cg_node_result_order_by_time": ([vp], C.c_int),
         "cg_checksum_device": ([vp, vp, i64, C.c_int, i64, i64, P(u64)], C.c_int),
         "cg_fill_device": ([vp, vp, i64, C.c_int], C.c_int),
+        "cg_fill_rate_device": ([vp, vp, i64, C.c_int, P(C.c_float)], C.c_int),
         "cg_count_value_device": ([vp, vp, i64, C.c_int, i64, P(i64)], C.c_int),
         "cg_rules_upload": ([vp, P(cg_rules_in), P(vp)], C.c_int),
         "cg_rules_free": ([vp], None),

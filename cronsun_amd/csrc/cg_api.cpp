@@ -415,9 +415,13 @@ int cg_lock_ttl_batch(cg_ctx* c, const cg_specs* s, const cg_zone* z, const int6
 // for an output capacity of map_cap events (no k_chunk_map launch).
 static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
                        bool* empty, int64_t map_cap = 0) {
-  // no readable result until this call succeeds (the accessors check last_R/E)
+  // no readable result until this call succeeds (the accessors check last_R/E).
+  // Asynchronous calls still pending are drained and their results and errors
+  // discarded: this call's result replaces them (cronsun_gpu.h).
   int rc0 = async_drain(c);
   if (rc0) return rc0;
+  c->async_rc = 0;
+  c->async_msg.clear();
   c->as_last = -1;
   c->last_R = 0;
   c->last_E = 0;
@@ -614,8 +618,15 @@ int cg_expand(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_
   return CG_OK;
 }
 
+static int refuse_pending(cg_ctx* c, const char* what) {
+  if (!async_pending(c)) return CG_OK;
+  return cg_fail(CG_EINVAL, std::string(what) + ": asynchronous expansions pending (call cg_expand_wait first)");
+}
+
 int cg_result_device(cg_ctx* c, const int64_t** d_off, const int64_t** d_times, int64_t* n) {
   if (!c) return cg_fail(CG_EINVAL, "cg_result_device: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (int rc = refuse_pending(c, "cg_result_device")) return rc;
   if (d_off) *d_off = c->as_last >= 0 ? c->as[c->as_last].offsets.p : c->offsets.p;
   if (d_times) *d_times = c->times.p;
   if (n) *n = c->last_E;
@@ -625,6 +636,7 @@ int cg_result_device(cg_ctx* c, const int64_t** d_off, const int64_t** d_times, 
 int cg_result_copy_times(cg_ctx* c, int64_t first, int64_t count, int64_t* host) {
   if (!c || (count && !host)) return cg_fail(CG_EINVAL, "cg_result_copy_times: null");
   std::lock_guard<std::mutex> g(c->mu);
+  if (int rc = refuse_pending(c, "cg_result_copy_times")) return rc;
   if (first < 0 || count < 0 || first + count > c->last_E)
     return cg_fail(CG_EINVAL, "range outside the last result");
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
@@ -636,6 +648,7 @@ int cg_result_copy_times(cg_ctx* c, int64_t first, int64_t count, int64_t* host)
 int cg_result_copy_offsets(cg_ctx* c, int64_t* host) {
   if (!c || !host) return cg_fail(CG_EINVAL, "cg_result_copy_offsets: null");
   std::lock_guard<std::mutex> g(c->mu);
+  if (int rc = refuse_pending(c, "cg_result_copy_offsets")) return rc;
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   HIPCHK(hipSetDevice(c->device));
   const int64_t* off = c->as_last >= 0 ? c->as[c->as_last].offsets.p : c->offsets.p;
@@ -669,6 +682,31 @@ int cg_fill_device(cg_ctx* c, void* d_ptr, int64_t bytes, int byte_value) {
   HIPCHK(hipSetDevice(c->device));
   if (bytes) HIPCHK(hipMemsetAsync(d_ptr, byte_value & 0xFF, size_t(bytes), c->st));
   HIPCHK(hipStreamSynchronize(c->st));
+  return CG_OK;
+}
+
+int cg_fill_rate_device(cg_ctx* c, void* d_ptr, int64_t bytes, int reps, float* ms) {
+  if (!c || !ms || bytes <= 0 || bytes % 16 != 0 || !d_ptr || reps < 1)
+    return cg_fail(CG_EINVAL, "cg_fill_rate_device: bad argument (bytes a positive multiple of 16, reps >= 1)");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  HIPCHK(hipStreamSynchronize(c->st));
+  for (int kind = 0; kind < 3; kind++) {
+    auto fill = [&]() -> hipError_t {
+      if (kind == 2) return hipMemsetAsync(d_ptr, 0x5E, size_t(bytes), c->st);
+      launch_fill_stream(d_ptr, bytes / 16, kind == 0, c->st);
+      return hipGetLastError();
+    };
+    HIPCHK(fill());  // warm-up
+    HIPCHK(hipEventRecord(c->ev[0], c->st));
+    for (int r = 0; r < reps; r++) HIPCHK(fill());
+    HIPCHK(hipEventRecord(c->ev[1], c->st));
+    HIPCHK(hipEventSynchronize(c->ev[1]));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, c->ev[0], c->ev[1]));
+    ms[kind] = t / float(reps);
+  }
   return CG_OK;
 }
 

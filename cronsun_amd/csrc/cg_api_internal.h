@@ -256,3 +256,4 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
 // finish and check every pending cg_expand_device_async call (cg_async.cpp);
 // their errors are reported by the next cg_expand_wait
 int async_drain(cg_ctx* c);
+bool async_pending(const cg_ctx* c);  // an asynchronous expansion not yet waited for

@@ -69,6 +69,12 @@ int ensure_async(cg_ctx* c) {
 
 }  // namespace
 
+bool async_pending(const cg_ctx* c) {
+  for (const AsyncSet& a : c->as)
+    if (a.pending) return true;
+  return false;
+}
+
 // every pending async call finished and checked (errors kept for the next wait)
 int async_drain(cg_ctx* c) {
   bool any = false;
@@ -127,6 +133,7 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
     HIPCHK(hipMemsetAsync(a.offsets.p, 0, (R + 1) * 8, c->st));
     a.res_host[0] = 0;
     a.res_host[1] = -1;
+    a.R = R;
     c->as_next = (k + 1) % cg_ctx::kAsyncSets;
     c->as_last = k;
     c->last_R = R;
@@ -163,8 +170,8 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   a.pending = true;
   c->as_next = (k + 1) % cg_ctx::kAsyncSets;
   c->as_last = k;
-  c->last_R = R;
-  c->last_E = 0;  // known at cg_expand_wait
+  c->last_R = 0;  // nothing readable until cg_expand_wait (the accessors refuse while a call is pending)
+  c->last_E = 0;
   return CG_OK;
 }
 
@@ -185,12 +192,13 @@ int cg_expand_wait(cg_ctx* c, int64_t* n_events) {
   const std::string msg = c->async_msg;
   c->async_rc = 0;
   c->async_msg.clear();
+  int64_t E = 0;
   if (c->as_last >= 0) {
-    const int64_t E = c->as[c->as_last].res_host[0];
+    E = c->as[c->as_last].res_host[0];
     c->last_E = rc_async ? 0 : E;
-    if (rc_async) c->last_R = 0;
-    if (n_events) *n_events = E;
+    c->last_R = rc_async ? 0 : c->as[c->as_last].R;
   }
+  if (n_events) *n_events = E;  // 0 when no asynchronous call was made since the last synchronous one
   if (rc_async) return cg_fail(rc_async, msg);
   return CG_OK;
 }

@@ -85,6 +85,10 @@ void launch_checksum(const void* v, int64_t n, int elem_bytes, int64_t first, in
                      unsigned long long* out, hipStream_t st);
 
 // *out += count of elements (int64 or int32) of v equal to x (cg_count_value_device)
+// streaming fill of n16 16-B words (store-ceiling probe of cg_fill_rate_device):
+// nt = 1 nontemporal stores, 0 plain
+void launch_fill_stream(void* p, int64_t n16, int nt, hipStream_t st);
+
 void launch_count_eq(const void* v, int64_t n, int elem_bytes, int64_t x, unsigned long long* out,
                      hipStream_t st);
 
@@ -152,6 +156,15 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,
                        const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
                        int64_t cap, int64_t* times, hipStream_t st);
+
+#ifdef CG_DIAG
+// diagnostic library only (cg_diag.hip): launches a probe or an experimental
+// writer in place of k_write_cf when CG_WRITE_PROBE / CG_WRITE_VARIANT ask for
+// one (returns true), else nothing
+bool launch_write_diag(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor, const int32_t* run_count,
+                       const uint32_t* run_dmask, const int64_t* run_off, int64_t nruns, int64_t* chunk_run,
+                       int64_t cap, int64_t* times, int n_blocks, size_t lds, hipStream_t st);
+#endif
 
 
 }  // namespace cg

@@ -20,13 +20,8 @@
 #include <cstdlib>
 
 #include "cg_expand.h"
-#ifndef CG_WRITE_BATCH
-#define CG_WRITE_BATCH 8
-#endif
-#ifndef CG_WRITE_LOADER
-#define CG_WRITE_LOADER 0  // production writer: k_write_lw (1) or k_write_cf (0)
-#endif
 #include "cg_kernels.h"
+#include "cg_write.h"
 
 namespace cg {
 
@@ -570,351 +565,6 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 }
 
 
-// one run of a wave's 64-run window (lane i holds run jw + i), staged in LDS
-// (48 B; the run offset stays in a VGPR of lane i, the plan segment index
-// rides in the spec's kind word: kind | seg << 8)
-struct WinRun {
-  int64_t anchor;  // run_anchor[j]
-  DSpec sp;        // specs[j / G]
-  int32_t count;   // run_count[j]
-  uint32_t dmask;  // run_dmask[j]
-};
-__device__ __forceinline__ bool win_every(const WinRun& w) { return (w.sp.kind & 0xFFu) == KIND_EVERY; }
-__device__ __forceinline__ int win_seg(const WinRun& w) { return int(w.sp.kind >> 8); }
-
-__device__ __forceinline__ int32_t rl32(int32_t v, int i) { return __builtin_amdgcn_readlane(v, i); }
-__device__ __forceinline__ int64_t rl64(int64_t v, int i) {
-  const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(v)), i));
-  const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(uint64_t(v) >> 32)), i));
-  return int64_t((uint64_t(hi) << 32) | lo);
-}
-
-// Lane k of the result holds unit * (position of the k-th set bit of m), for
-// k < popcount(m): each lane pushes its own position to the lane of its rank
-// (set bits to 0..n-1, clear bits to n..63 -- a permutation), ds_permute_b32.
-// All 64 lanes must be active.
-__device__ __forceinline__ int32_t rank_table(uint64_t m, int32_t unit) {
-  const int lane = threadIdx.x & 63;
-  const bool set = (m >> lane) & 1ull;
-  const int32_t below = __popcll(m & ((1ull << lane) - 1ull));
-  const int32_t n = __popcll(m);
-  const int32_t dst = set ? below : n + (lane - below);
-  return __builtin_amdgcn_ds_permute(dst << 2, lane * unit);
-}
-// entry idx of a rank table (ds_bpermute_b32; idx is taken mod 64)
-__device__ __forceinline__ int32_t rank_at(int32_t table, uint32_t idx) {
-  return __builtin_amdgcn_ds_bpermute(int(idx << 2), table);
-}
-// floor(x / n) for x < 2^16, n >= 1, with inv = 1/n (the +0.5 keeps the
-// product at least 0.5/n away from an integer, far above the f32 error)
-__device__ __forceinline__ uint32_t small_div(uint32_t x, float inv) {
-  return uint32_t((float(x) + 0.5f) * inv);
-}
-// floor(x / n) for x < 2^24, n >= 1, inv = 1/n: the f32 quotient is off by at
-// most one, fixed by one remainder test each way (cheaper than a u32 divide)
-__device__ __forceinline__ uint32_t fdiv(uint32_t x, uint32_t n, float inv) {
-  uint32_t q = uint32_t(float(x) * inv);
-  const int32_t r = int32_t(x) - int32_t(q * n);
-  q = r < 0 ? q - 1u : (r >= int32_t(n) ? q + 1u : q);
-  return q;
-}
-
-// Output store.  V (diagnostic variants, CG_WRITE_VARIANT; 0 in production):
-// bit 0 = compute only (no store, value kept live), bit 1 = non-temporal store,
-// bit 2 = skip the short runs, bit 3 = skip the long runs, bit 4 = static slice
-// split instead of tickets, bit 5 = per-phase clock stats, bit 6 = plain fill.
-template <int V>
-__device__ __forceinline__ void put(int64_t* p, int64_t v) {
-  if (V & 1) {
-    asm volatile("" ::"v"(v));
-  } else if (V & 2) {
-    __builtin_nontemporal_store(v, p);
-  } else {
-    *p = v;
-  }
-}
-
-// cf_seek (cg_expand.h) with the three variable divisions done by fdiv
-// (quotients < 2^24); same result, fewer instructions.
-__device__ __forceinline__ CFIter cf_seek_fast(const CFRule& c, const Segment& sg, uint32_t dmask,
-                                               int64_t uf, int64_t k) {
-  if (k == 0) return cf_decode(sg, uf);
-  const uint32_t rf = uint32_t(uf - sg.base);
-  const uint32_t jf = rf / 86400u, tf = rf - jf * 86400u;
-  uint32_t idx = cf_rank(c, int32_t(tf)) - 1u + uint32_t(k);
-  CFIter it;
-  it.day = int32_t(jf);
-  if (idx >= c.C) {
-    idx -= c.C;
-    const uint32_t dskip = fdiv(idx, c.C, 1.0f / float(c.C));
-    idx -= dskip * c.C;
-    const uint64_t above = uint64_t(dmask) & ~((2ull << jf) - 1ull);
-    it.day = select64(above, dskip);
-  }
-  const uint32_t hi = fdiv(idx, c.nMS, 1.0f / float(c.nMS));
-  const uint32_t rem = idx - hi * c.nMS;
-  const uint32_t mi = fdiv(rem, c.nS, 1.0f / float(c.nS));
-  const uint32_t si = rem - mi * c.nS;
-  it.h = select64(c.H, hi);
-  it.m = select64(c.M, mi);
-  it.s = select64(c.S, si);
-  return it;
-}
-
-// Does mask m (n set bits) hold an arithmetic progression p0 + r*step?
-// (rank r -> position is then linear; n <= 1 counts, with step 0)
-__device__ __forceinline__ bool ap_level(uint64_t m, uint32_t n, int32_t* p0, int32_t* step) {
-  *p0 = m ? __builtin_ctzll(m) : 0;
-  *step = 0;
-  if (n <= 1) return true;
-  const uint64_t rest = m >> *p0;  // bit 0 set
-  const int32_t st = __builtin_ctzll(rest >> 1) + 1;
-  *step = st;
-  // {0, st, 2st, ...} up to the top bit  <=>  ((rest << st) | 1) below the top == rest
-  const int32_t top = 63 - __builtin_clzll(rest);
-  const uint64_t low = top >= 63 ? ~0ull : ((2ull << top) - 1ull);
-  return (((rest << st) | 1ull) & low) == rest;
-}
-
-// The aligned 64-fire block holding a run boundary, assembled across runs:
-// each run fills its lanes, and the run that completes the block stores it
-// with one whole 512 B store (no partially written cache line reaches HBM).
-struct Pending {
-  int64_t blk;  // block start, or -1 (wave-uniform)
-  int64_t val;  // this lane's fire in it
-};
-
-// Position offset of this lane's first fire of a piece starting at p0: lane l
-// covers p0 + x, x = (floor64(p0) + l - p0) mod 64 -- lanes before p0 in the
-// head block belong to earlier runs and start one block later.
-__device__ __forceinline__ uint32_t lane_offset(int64_t p0) {
-  const int lane = threadIdx.x & 63;
-  const int32_t x = int32_t((p0 & ~int64_t(63)) + lane - p0);
-  return uint32_t(x < 0 ? x + 64 : x);
-}
-
-constexpr int kBatch = CG_WRITE_BATCH;  // blocks computed before their stores are issued
-#ifndef CG_WRITE_TAKE
-#define CG_WRITE_TAKE 1
-#endif
-constexpr int kTake = CG_WRITE_TAKE;  // writer slices per ticket atomic
-#ifndef CG_WRITE_MIXED
-#define CG_WRITE_MIXED 1
-#endif
-#ifndef CG_WRITE_SPARE_BLOCKS
-#define CG_WRITE_SPARE_BLOCKS 0
-#endif
-constexpr bool kMixedBlocks = CG_WRITE_MIXED;  // blocks holding several runs filled lane-parallel
-// 64-bit ds_bpermute (lane src's value; src taken mod 64)
-__device__ __forceinline__ int64_t bperm64_w(int64_t v, int src) {
-  const int lo = __builtin_amdgcn_ds_bpermute(src << 2, int(uint32_t(v)));
-  const int hi = __builtin_amdgcn_ds_bpermute(src << 2, int(uint32_t(uint64_t(v) >> 32)));
-  return int64_t((uint64_t(uint32_t(hi)) << 32) | uint32_t(lo));
-}
-
-// Runs the piece [p0, p1) through the block protocol: value() is this lane's
-// current fire, step() advances it by 64 fires.  Full blocks are stored as
-// computed (8 values first, then 8 stores: a wave held back by a full memory
-// pipe has no arithmetic queued behind the store); the head block merges the
-// pending fires of earlier runs; a partial tail block becomes pending.
-// GAP: a walked run -- its fires come from k_write_walk, so only the shared
-// blocks are written (placeholders there), never its own full blocks.
-template <int V, bool GAP, class Val, class Step>
-__device__ __forceinline__ void drive(Val&& value, Step&& step, int64_t p0, int64_t p1,
-                                      Pending& pd, int64_t* __restrict__ times) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b0 = p0 & ~int64_t(63);
-  const bool mine0 = b0 + lane >= p0;
-  {
-    int64_t v = GAP ? 0 : value();
-    if (!mine0) v = pd.val;
-    if (b0 + 64 > p1) {  // the run ends inside its head block
-      pd.blk = b0;
-      pd.val = v;
-      return;
-    }
-    put<V>(times + b0 + lane, v);
-    pd.blk = -1;
-    if (!GAP && mine0) step();
-  }
-  int64_t b = b0 + 64;
-  if (GAP) {
-    b += (p1 - b) & ~int64_t(63);
-  } else {
-    for (; b + kBatch * 64 <= p1; b += kBatch * 64) {
-      int64_t vv[kBatch];
-#pragma unroll
-      for (int u = 0; u < kBatch; u++) {
-        vv[u] = value();
-        step();
-      }
-#pragma unroll
-      for (int u = 0; u < kBatch; u++) asm volatile("" : "+v"(vv[u]));
-#pragma unroll
-      for (int u = 0; u < kBatch; u++) put<V>(times + b + 64 * u + lane, vv[u]);
-    }
-    for (; b + 64 <= p1; b += 64) {
-      put<V>(times + b + lane, value());
-      step();
-    }
-  }
-  if (b < p1) {
-    pd.blk = b;
-    pd.val = GAP ? 0 : value();
-  }
-}
-
-// Fires [p0, p1) of closed-form run w (run start roff), wave-cooperatively.
-// A fire's index g = rank(anchor) - 1 + (p - roff) counts (day, hour, minute,
-// second) combinations from the anchor's local day, so it is carried as
-// mixed-radix digits (matching-day rank, hour/minute/second ranks; radices -,
-// nH, nM, nS) and stepped by the constant 64.  Same enumeration as
-// cf_seek/cf_next.  Rank -> seconds, cheapest form first:
-//   linear   every level an arithmetic progression and the sequence has one
-//            stride (e.g. */10 s with every minute/hour/day): t += 64*stride;
-//   affine   every level an arithmetic progression: t = C0 + sum r_i * w_i;
-//   tables   otherwise: per-level lane tables read with ds_bpermute.
-template <int V>
-__device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_t p0, int64_t p1,
-                        Pending& pd, int64_t* __restrict__ times) {
-  const CFRule c = cf_rule(w.sp);
-  const uint32_t nS = c.nS, nM = c.nM, nH = uint32_t(__builtin_popcount(c.H));
-  const uint32_t rf = uint32_t(w.anchor - sg.base);
-  const uint32_t jf = rf / 86400u, tf = rf - jf * 86400u;
-  const uint32_t dmask = w.dmask >> jf;  // matching days from the anchor's (bit 0)
-  const float iS = 1.0f / float(nS), iM = 1.0f / float(nM), iH = 1.0f / float(nH);
-  // g < 31 * 86400 < 2^24
-  uint32_t g = cf_rank(c, int32_t(tf)) - 1u + uint32_t(p0 - roff);
-  uint32_t d = fdiv(g, c.C, 1.0f / float(c.C));
-  g -= d * c.C;
-  uint32_t h = fdiv(g, c.nMS, 1.0f / float(c.nMS));
-  g -= h * c.nMS;
-  uint32_t m = fdiv(g, nS, iS);
-  uint32_t s = g - m * nS;
-  // + this lane's offset (< 128)
-  uint32_t q;
-  s += lane_offset(p0);
-  q = small_div(s, iS);
-  s -= q * nS;
-  m += q;
-  q = small_div(m, iM);
-  m -= q * nM;
-  h += q;
-  q = small_div(h, iH);
-  h -= q * nH;
-  d += q;
-  // digits of 64
-  uint32_t a = small_div(64, iS);
-  const uint32_t a0 = 64 - a * nS;
-  uint32_t a_ = small_div(a, iM);
-  const uint32_t a1 = a - a_ * nM;
-  a = small_div(a_, iH);
-  const uint32_t a2 = a_ - a * nH;
-  const uint32_t a3 = a;
-  auto step = [&]() {
-    s += a0;
-    const uint32_t cs = s >= nS;
-    s -= cs ? nS : 0u;
-    m += a1 + cs;
-    const uint32_t cm = m >= nM;
-    m -= cm ? nM : 0u;
-    h += a2 + cm;
-    const uint32_t ch = h >= nH;
-    h -= ch ? nH : 0u;
-    d += a3 + ch;
-  };
-  int32_t s0, ss, m0, ms, h0, hs, d0, ds;
-  const uint32_t nD = uint32_t(__builtin_popcount(dmask));
-  const bool apS = ap_level(c.S, nS, &s0, &ss), apM = ap_level(c.M, nM, &m0, &ms);
-  const bool apH = ap_level(c.H, nH, &h0, &hs), apD = ap_level(dmask, nD, &d0, &ds);
-  if (apS && apM && apH && apD) {
-    const int64_t C0 = sg.base + s0 + 60 * m0 + 3600 * h0 + 86400 * int32_t(jf);  // d0 == 0
-    const uint32_t ws = uint32_t(ss), wm = 60u * uint32_t(ms), wh = 3600u * uint32_t(hs),
-                   wd = 86400u * uint32_t(ds);
-    auto value = [&]() -> int64_t {
-      // every product < 2^24 x 2^24 operands: v_mul_u32_u24 (full rate)
-      return C0 + int64_t(__umul24(s, ws) + __umul24(m, wm) + __umul24(h, wh) + __umul24(d, wd));
-    };
-    // one stride: the lowest level with > 1 value wraps evenly into the next
-    // unit, and every level above it takes every value (days: consecutive)
-    const bool days_full = nD <= 1 || ds == 1;
-    int32_t stride = 0;
-    if (nS > 1) {
-      if (uint32_t(ss) * nS == 60 && s0 < ss && nM == 60 && nH == 24 && days_full) stride = ss;
-    } else if (nM > 1) {
-      if (uint32_t(ms) * nM == 60 && m0 < ms && nH == 24 && days_full) stride = 60 * ms;
-    } else if (nH > 1) {
-      if (uint32_t(hs) * nH == 24 && h0 < hs && days_full) stride = 3600 * hs;
-    } else {
-      stride = 86400 * ds;
-    }
-    if (stride > 0) {
-      int64_t v = value();
-      const int64_t st = 64 * int64_t(stride);
-      drive<V, false>([&]() { return v; }, [&]() { v += st; }, p0, p1, pd, times);
-    } else {
-      drive<V, false>(value, step, p0, p1, pd, times);
-    }
-    return;
-  }
-  const int32_t ts = rank_table(c.S, 1);
-  const int32_t tm = rank_table(c.M, 60);
-  const int32_t th = rank_table(c.H, 3600);
-  const int32_t td = rank_table(uint64_t(dmask), 86400) + int32_t(jf) * 86400;
-  const int64_t base = sg.base;
-  auto value = [&]() -> int64_t {  // all lanes active: the table reads are cross-lane
-    return base + int64_t(rank_at(td, d) + rank_at(th, h) + rank_at(tm, m) + rank_at(ts, s));
-  };
-  drive<V, false>(value, step, p0, p1, pd, times);
-}
-
-// Fires [p0, p1) of a short closed-form run: each lane seeks its own fire
-// (the anchor itself, its successor, or cf_seek).
-template <int V>
-__device__ void tiny_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_t p0, int64_t p1,
-                        Pending& pd, int64_t* __restrict__ times) {
-  int32_t k = int32_t(p0 - roff) + int32_t(lane_offset(p0));
-  const CFRule c = cf_rule(w.sp);
-  auto value = [&]() -> int64_t {
-    if (k == 0) return w.anchor;
-    if (int64_t(k) >= p1 - roff) return 0;  // not this run's (a later run's lane)
-    if (k == 1) {
-      CFIter it = cf_decode(sg, w.anchor);
-      cf_next(c, w.dmask, it);
-      return cf_value(sg, it);
-    }
-    return cf_value(sg, cf_seek_fast(c, sg, w.dmask, w.anchor, k));
-  };
-  drive<V, false>(value, [&]() { k += 64; }, p0, p1, pd, times);
-}
-
-// Fires [p0, p1) of @every run w: anchor + (k + 1) * D (constantdelay.go:25-27)
-template <int V>
-__device__ void coop_every(const WinRun& w, int64_t roff, int64_t p0, int64_t p1, Pending& pd,
-                           int64_t* __restrict__ times) {
-  const int64_t D = int64_t(w.sp.sec);
-  int64_t t = w.anchor + (p0 - roff + int64_t(lane_offset(p0)) + 1) * D;
-  const int64_t st = 64 * D;
-  drive<V, false>([&]() { return t; }, [&]() { t += st; }, p0, p1, pd, times);
-}
-
-// Fire k (>= 0) of window run w, for one lane (the per-lane form of
-// coop_every / tiny_cf): @every anchor + (k + 1) D (constantdelay.go:25-27),
-// a walked run's placeholder 0 (k_write_walk writes it), else the k-th
-// closed-form fire from the anchor.
-__device__ __forceinline__ int64_t run_fire(const WinRun& w, const Segment& sg, int64_t k) {
-  if (win_every(w)) return w.anchor + (k + 1) * int64_t(w.sp.sec);
-  if (run_is_walked(sg, w.dmask)) return 0;
-  if (k == 0) return w.anchor;
-  const CFRule c = cf_rule(w.sp);
-  if (k == 1) {
-    CFIter it = cf_decode(sg, w.anchor);
-    cf_next(c, w.dmask, it);
-    return cf_value(sg, it);
-  }
-  return cf_value(sg, cf_seek_fast(c, sg, w.dmask, w.anchor, k));
-}
-
 // Persistent closed-form writer.  Waves work independently on 2^super_shift(cap)-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
 // consecutive runs (one coalesced round of loads, staged in its LDS slice;
@@ -926,7 +576,6 @@ __device__ __forceinline__ int64_t run_fire(const WinRun& w, const Segment& sg, 
 // @every progression (coop_every); short runs by per-lane seeks (tiny_cf).
 // Walked runs' own blocks are left to k_write_walk, which runs after this
 // kernel.
-template <int V>
 __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
     const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
@@ -994,37 +643,17 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
   // slices 23.7 vs 24.5 ms; config 2 with 2048-event slices 1.03 vs 0.99 ms:
   // moving on only pays with the large slices)
   const bool steal = sh == CG_SUPER_SHIFT_LARGE;
-  int64_t static_next = int64_t(blockIdx.x) * kWriteWaves + wave;
-  // kTake consecutive tickets of the group per atomic (the atomic's result is
-  // waited for behind every store the wave has issued).  Same-box A/B,
-  // profiles/r02_ab_writer_lw.json: 1 is best -- 2/4/8 lose more to the
-  // coarser tail than the fewer atomics save
-  uint32_t tk_next = 0, tk_left = 0;
+  // One ticket per atomic (same-box A/B, profiles/r02_ab_writer_lw.json:
+  // taking 2/4/8 per atomic loses more to the coarser tail than it saves).
   auto take = [&]() -> int64_t {
-    if (V & 16) {  // diagnostic: static grid-stride split
-      const int64_t t = static_next;
-      static_next += int64_t(gridDim.x) * kWriteWaves;
-      return t;
-    }
     for (;;) {
-      if (tk_left == 0) {
-        unsigned int t = 0;
-        if (lane == 0) t = atomicAdd(tickets + cur * kTicketStride, unsigned(kTake));
-        tk_next = uint32_t(__builtin_amdgcn_readfirstlane(int(t)));
-        tk_left = kTake;
-      }
-      const int64_t c = cur + int64_t(ng) * int64_t(tk_next);
-      tk_next++;
-      tk_left--;
+      unsigned int t = 0;
+      if (lane == 0) t = atomicAdd(tickets + cur * kTicketStride, 1u);
+      const int64_t c = cur + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
       if (c < nsup || !steal || ++hops >= ng) return c;
       cur = cur + 1 == ng ? 0 : cur + 1;
-      tk_left = 0;
     }
   };
-  // V & 32 (diagnostic): per-phase shader-clock totals and counts
-  uint64_t st_win = 0, st_long = 0, st_all = 0, n_win = 0, n_long = 0, st_mix = 0, n_mix = 0;
-  auto clk = [&]() -> uint64_t { return (V & 32) ? __builtin_amdgcn_s_memtime() : 0; };
-  const uint64_t k_start = clk();
   for (int64_t c = take(); c < nsup;) {
     const int64_t c_next = take();
     // slice start: a multiple of 64, so every store below is a whole 512 B block
@@ -1034,17 +663,9 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       c = c_next;
       continue;
     }
-    uint64_t t_a = clk();
-    if (V & 64) {  // diagnostic: plain fill of the slice (with bit 3: + the skeleton's reads)
-      for (int64_t b = pos + lane; b < S1; b += 64) put<V>(times + b, b);
-    }
     int64_t jw = um ? umap[2 * c + 1] : chunk_run[c];  // run_off[jw] <= pos
     jend = (um ? umap[2 * c + 3] : chunk_run[c + 1]) + 1;  // the run holding S1 (or the last run)
     load_window(jw);
-    if (V & 32) {
-      st_win += clk() - t_a;
-      n_win++;
-    }
     Pending pd;
     pd.blk = -1;
     pd.val = 0;
@@ -1052,12 +673,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
     while (pos < S1) {
       if (i == 64) {  // past the window (the slice's runs continue: jw + 64 < jend)
         jw += 64;
-        t_a = clk();
         load_window(jw);
-        if (V & 32) {
-          st_win += clk() - t_a;
-          n_win++;
-        }
         i = 0;
       }
       const int32_t cnt = rl32(wcnt, i);
@@ -1068,7 +684,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       const int64_t roff = rl64(woff, i);
       const int64_t p1 = roff + cnt < S1 ? roff + cnt : S1;
       const int64_t b = pos & ~int64_t(63);
-      if (kMixedBlocks && !(V & 8) && p1 < b + 64 && p1 < S1) {
+      if (p1 < b + 64 && p1 < S1) {
         // The run ends inside this block and the slice goes on: the block
         // holds several runs.  Fill it lane-parallel -- each lane finds its
         // run among the window's (largest j with woff[j] <= q) and computes
@@ -1092,7 +708,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
             v = pd.val;  // earlier runs' fires of this block
           }
           if (be == b + 64) {
-            put<V>(times + q, v);
+            put(times + q, v);
             pd.blk = -1;
             pos = be;
             i = 63 - __builtin_clzll(__ballot(woff <= pos));  // the run holding pos
@@ -1106,391 +722,24 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       }
       const WinRun& w = win[i];
       const Segment& sg = segs[win_seg(w)];
-      t_a = clk();
-      if (V & 8) {
-      } else if (win_every(w)) {
-        coop_every<V>(w, roff, pos, p1, pd, times);
+      if (win_every(w)) {
+        coop_every(w, roff, pos, p1, pd, times);
       } else if (run_is_walked(sg, w.dmask)) {
-        drive<V, true>([]() { return int64_t(0); }, []() {}, pos, p1, pd, times);
+        drive<true>([]() { return int64_t(0); }, []() {}, pos, p1, pd, times);
       } else if (p1 - pos >= 64) {
-        coop_cf<V>(w, roff, sg, pos, p1, pd, times);
+        coop_cf(w, roff, sg, pos, p1, pd, times);
       } else {
-        tiny_cf<V>(w, roff, sg, pos, p1, pd, times);
-      }
-      if (V & 32) {
-        const uint64_t dt = clk() - t_a;
-        if (p1 - pos >= 64) {
-          st_long += dt;
-          n_long++;
-        } else {
-          st_mix += dt;
-          n_mix++;
-        }
+        tiny_cf(w, roff, sg, pos, p1, pd, times);
       }
       pos = p1;
       i++;
     }
     // the last slice ends inside a block
-    if (pd.blk >= 0 && pd.blk + lane < S1 && !(V & 8)) put<V>(times + pd.blk + lane, pd.val);
+    if (pd.blk >= 0 && pd.blk + lane < S1) put(times + pd.blk + lane, pd.val);
     c = c_next;
   }
-  if (V & 32) {
-    st_all = clk() - k_start;
-    unsigned long long* dbg =
-        reinterpret_cast<unsigned long long*>(chunk_run + (cap >> sh) + 2 + kTicketWords);
-    if (lane == 0) {
-      atomicAdd(dbg + 0, st_all);
-      atomicAdd(dbg + 1, st_win);
-      atomicAdd(dbg + 2, st_long);
-      atomicAdd(dbg + 3, st_mix);
-      atomicAdd(dbg + 4, n_win);
-      atomicAdd(dbg + 5, n_long);
-      atomicAdd(dbg + 6, n_mix);
-      atomicAdd(dbg + 7, 1ull);
-    }
-  }
 }
 
-// ---- k_write_lw: the closed-form writer with its loads split off ----------
-// On gfx9 a wave's vector loads and stores retire in issue order (one vmcnt),
-// so every load a writer wave waits for -- its slice ticket, the slice's run
-// window -- also waits for every store it issued before: in k_write_cf each
-// slice drains the wave's store queue one to three times.  Here each block
-// has kLwWriters writer waves that issue no vector loads and one loader wave
-// that issues them all: it takes the tickets, reads the slice map and copies
-// each slice's 64-run windows (run offsets, anchors, counts, day masks and
-// the runs' rule specs) into one LDS slot per writer with global->LDS DMA
-// (no registers; one wait for every writer's copies).  A writer turns its
-// slot into its own window (as k_write_cf's) and hands the slot back at once,
-// so the next window is copied while it writes.  Writers wait on LDS flags
-// only (lgkmcnt): their stores stream without drains.  Every wait is
-// bounded: a wave that waits ~2 s (the other side gone) sets an error word
-// and leaves, so the grid always drains.
-#ifndef CG_LW_WRITERS
-#define CG_LW_WRITERS 7
-#endif
-constexpr int kLwWriters = CG_LW_WRITERS;
-#ifndef CG_LW_WPE
-#define CG_LW_WPE 4  // waves per SIMD the register allocation must allow
-#endif
-constexpr uint32_t kLwSpin = 1u << 25;  // polls of ~64 clocks each before giving up
-
-struct LwSlot {  // one window, as copied: structure of arrays
-  int64_t off[64];     // run_off
-  int64_t anchor[64];  // run_anchor
-  int32_t count[64];   // run_count
-  uint32_t dmask[64];  // run_dmask
-  DSpec spec[65];      // specs of rules jw / G .. (jw + 63) / G
-  int64_t c, jw, jend;  // slice (-1: no more slices for this writer), first run, runs end
-  int32_t k, nw;        // window k of the slice's nw windows
-  int32_t seg0;         // jw % G (the first run's segment; spec[0] is rule jw / G)
-};
-
-__device__ __forceinline__ uint32_t lds_flag_get(const uint32_t* f) {
-  return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_flag_set(uint32_t* f, uint32_t v) {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's reads/writes are done
-  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-// global -> LDS copy of `bytes` (a multiple of 4) by the whole wave, 256 B a round
-__device__ __forceinline__ void lds_copy(void* lds, const void* g, int bytes) {
-  const int lane = threadIdx.x & 63;
-  for (int b = 0; b < bytes; b += 256)
-    if (b + 4 * lane < bytes)
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(g) + b + 4 * lane,
-                                       (__attribute__((address_space(3))) void*)(reinterpret_cast<char*>(lds) + b),
-                                       4, 0, 0);
-}
-
-template <int V>
-__global__ __launch_bounds__((kLwWriters + 1) * 64) __attribute__((amdgpu_waves_per_eu(CG_LW_WPE)))
-void k_write_lw(
-    const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
-    const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
-    const int64_t* __restrict__ run_off, int64_t nruns, int64_t* __restrict__ chunk_run,
-    int64_t cap, int64_t* __restrict__ times) {
-  __shared__ LwSlot slots[kLwWriters];
-  __shared__ WinRun win_all[kLwWriters][64];
-  __shared__ uint32_t flags[kLwWriters];  // 1: filled by the loader, 0: free
-  extern __shared__ __align__(16) char dyn[];  // the plan's G segments
-  Segment* segs = reinterpret_cast<Segment*>(dyn);
-  for (int i = threadIdx.x; i < p.G * int(sizeof(Segment) / 8); i += blockDim.x)
-    reinterpret_cast<int64_t*>(segs)[i] = reinterpret_cast<const int64_t*>(p.segs)[i];
-  for (int i = threadIdx.x; i < kLwWriters; i += blockDim.x) flags[i] = 0u;
-  __syncthreads();
-
-  const int G = p.G;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t E = run_off[nruns];
-  if (E > cap) return;  // output buffer too small: host grows it and relaunches
-  const int sh = super_shift(cap);
-  const int64_t sup = int64_t(1) << sh;
-  const int64_t nsup = (E + sup - 1) >> sh;
-  unsigned long long* dbg =
-      reinterpret_cast<unsigned long long*>(chunk_run + (cap >> sh) + 2 + kTicketWords);
-
-  if (wave == kLwWriters) {
-    // ---- loader.  Lane w < kLwWriters keeps writer w's state, three stages
-    // deep: a ticket (the slice after next), the next slice's map entries,
-    // and the slice being copied window by window.  Each round issues every
-    // stage's loads for every writer at once -- atomics, slice-map reads,
-    // window copies -- and waits once.
-    const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
-    unsigned int* tickets = reinterpret_cast<unsigned int*>(chunk_run + (cap >> sh) + 2);
-    const bool steal = sh == CG_SUPER_SHIFT_LARGE;
-    int cur = int(blockIdx.x % unsigned(ng)), hops = 0;
-    int64_t c = 0, jw0 = 0, jend = 0;   // the slice being copied
-    int32_t k = 0, nw = 0;              // its next window, its windows
-    int64_t nc = 0, njw0 = 0, njend = 0;  // the next slice (has_nx)
-    int64_t tk = 0;                       // a ticket's slice (has_tk)
-    bool has_nx = false, has_tk = false, no_more = false;
-    bool fin = lane >= kLwWriters;  // writer `lane` has been sent its end item
-    uint32_t idle = 0, idle_total = 0;
-    while (__ballot(!fin)) {
-      const bool live = !fin;
-      const bool ready = live && lds_flag_get(&flags[lane]) == 0u;  // writer's slot free
-      if (live && k == nw && has_nx) {  // the next slice becomes current
-        c = nc;
-        jw0 = njw0;
-        jend = njend;
-        nw = int32_t((jend - jw0 + 63) >> 6);
-        k = 0;
-        has_nx = false;
-      }
-      const bool go = ready && k < nw;
-      if (ready && k == nw && !has_nx && no_more) {  // nothing left: the end item
-        slots[lane].c = -1;
-        lds_flag_set(&flags[lane], 1u);
-        fin = true;
-      }
-      bool busy = go;
-      // slice map of the ticket taken last round
-      if (live && !has_nx && has_tk) {
-        has_tk = false;
-        busy = true;
-        if (tk < nsup) {
-          nc = tk;
-          njw0 = chunk_run[tk];           // run_off[njw0] <= tk << sh
-          njend = chunk_run[tk + 1] + 1;  // the run holding the slice's end (or the last run)
-          has_nx = true;
-        } else if (steal && ++hops < ng) {  // this group is used up: move to the next one
-          cur = cur + 1 == ng ? 0 : cur + 1;
-        } else {
-          no_more = true;
-        }
-      }
-      // a ticket, one slice ahead of the slice map
-      if (live && !has_tk && !no_more) {
-        const unsigned int t = atomicAdd(tickets + cur * kTicketStride, 1u);
-        tk = cur + int64_t(ng) * int64_t(t);
-        has_tk = true;
-        busy = true;
-      }
-      // window copies, every writer's, then one wait for everything above
-      for (uint64_t m = __ballot(go); m; m &= m - 1) {
-        const int w = __builtin_ctzll(m);
-        const int64_t jw = rl64(jw0, w) + 64 * int64_t(rl32(k, w));
-        const int64_t je = rl64(jend, w);
-        const int n = int(je - jw < 64 ? je - jw : 64);
-        const int64_t r0 = G == 1 ? jw : jw / G, r1 = G == 1 ? jw + n - 1 : (jw + n - 1) / G;
-        LwSlot& s = slots[w];
-        lds_copy(s.off, run_off + jw, 8 * n);
-        lds_copy(s.anchor, run_anchor + jw, 8 * n);
-        lds_copy(s.count, run_count + jw, 4 * n);
-        lds_copy(s.dmask, run_dmask + jw, 4 * n);
-        lds_copy(s.spec, specs + r0, int(sizeof(DSpec)) * int(r1 - r0 + 1));
-        if (lane == 0) {
-          s.c = rl64(c, w);
-          s.jw = jw;
-          s.jend = je;
-          s.seg0 = int32_t(jw - r0 * G);
-          s.k = rl32(k, w);
-          s.nw = rl32(nw, w);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // copies, map reads and tickets have landed
-      if (go) {
-        lds_flag_set(&flags[lane], 1u);
-        k++;
-      }
-      if (!__ballot(busy)) {
-        if (++idle > kLwSpin) {
-          if (lane == 0) atomicOr(dbg, 1ull);
-          break;
-        }
-        if (V & 32) idle_total++;
-        __builtin_amdgcn_s_sleep(1);
-      } else {
-        idle = 0;
-      }
-    }
-    if ((V & 32) && lane == 0) atomicAdd(dbg + 1, (unsigned long long)idle_total);
-    return;
-  }
-
-  // ---- writer wave: its slices' windows, in order
-  WinRun* win = win_all[wave];
-  uint32_t* f = &flags[wave];
-  const LwSlot& s = slots[wave];
-  Pending pd;
-  pd.blk = -1;
-  pd.val = 0;
-  int64_t pos = 0, S1 = 0;
-  uint32_t waits = 0;
-  for (;;) {
-    for (uint32_t n = 0; lds_flag_get(f) != 1u; n++) {
-      if (n > kLwSpin) {
-        if (lane == 0) atomicOr(dbg, 2ull);
-        return;
-      }
-      if (V & 32) waits++;
-      __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");
-    const int64_t c = s.c;
-    if (c < 0) break;
-    const int32_t k = s.k, nw = s.nw;
-    const int64_t jw = s.jw, jend = s.jend;
-    // the slot -> this wave's window (k_write_cf's layout), then the slot is free
-    // lane index re-derived each window: addresses built from it are not
-    // hoisted out of the loop (and spilled: scratch reloads wait on vmcnt)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int64_t j = jw + ln;
-    int64_t woff = INT64_MAX;
-    int32_t wcnt = 0;
-    // field by field (a WinRun temporary lands in scratch: vector-memory
-    // traffic the writer would wait for behind its stores)
-    WinRun& r = win[ln];
-    if (j < jend) {
-      // run j = rule (jw / G + q), segment x - q G with x = jw % G + lane
-      const uint32_t x = uint32_t(s.seg0 + ln);
-      uint32_t q = x;
-      if (G > 1) {  // x < G + 64 < 2^24: f32 quotient, one correction each way
-        const float inv = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(1.0f / float(G))));
-        q = uint32_t(float(x) * inv);
-        const int32_t rem = int32_t(x) - int32_t(q * uint32_t(G));
-        q = rem < 0 ? q - 1u : (rem >= G ? q + 1u : q);
-      }
-      const DSpec& sp = s.spec[q];
-      const uint32_t seg = x - q * uint32_t(G);
-      woff = s.off[ln];
-      wcnt = s.count[ln];
-      r.anchor = s.anchor[ln];
-      r.count = wcnt;
-      r.dmask = s.dmask[ln];
-      r.sp.sec = sp.sec;
-      r.sp.min = sp.min;
-      r.sp.hour = sp.hour;
-      r.sp.dom = sp.dom;
-      r.sp.mondow = sp.mondow;
-      r.sp.kind = sp.kind | (seg << 8);
-    } else {
-      r.anchor = 0;
-      r.count = 0;
-      r.dmask = 0;
-      r.sp.sec = 0;
-      r.sp.min = 0;
-      r.sp.hour = 0;
-      r.sp.dom = 0;
-      r.sp.mondow = 0;
-      r.sp.kind = 0;
-    }
-    lds_flag_set(f, 0u);  // also waits for this lane's window write
-    int i = 0;
-    if (k == 0) {
-      pos = c << sh;  // multiple of 64: every store below is a whole 512 B block
-      S1 = E - pos < sup ? E : pos + sup;
-      pd.blk = -1;
-      pd.val = 0;
-      i = 63 - __builtin_clzll(__ballot(woff <= pos));  // the run holding pos
-    }
-    while (pos < S1 && i < 64) {
-      const int32_t cnt = rl32(wcnt, i);
-      if (cnt == 0) {
-        i++;
-        continue;
-      }
-      const int64_t roff = rl64(woff, i);
-      const int64_t p1 = roff + cnt < S1 ? roff + cnt : S1;
-      const WinRun& w = win[i];
-      const Segment& sg = segs[win_seg(w)];
-      if (V & 8) {
-      } else if (win_every(w)) {
-        coop_every<V>(w, roff, pos, p1, pd, times);
-      } else if (run_is_walked(sg, w.dmask)) {
-        drive<V, true>([]() { return int64_t(0); }, []() {}, pos, p1, pd, times);
-      } else if (p1 - pos >= 64) {
-        coop_cf<V>(w, roff, sg, pos, p1, pd, times);
-      } else {
-        tiny_cf<V>(w, roff, sg, pos, p1, pd, times);
-      }
-      pos = p1;
-      i++;
-    }
-    if (k == nw - 1) {
-      // the slice ends inside a block
-      if (pd.blk >= 0 && pd.blk + lane < S1 && !(V & 8)) put<V>(times + pd.blk + lane, pd.val);
-      pd.blk = -1;
-    }
-    // every lane is done with this window before the next one overwrites it
-    __builtin_amdgcn_wave_barrier();
-  }
-  if ((V & 32) && lane == 0) atomicAdd(dbg + 2, (unsigned long long)waits);
-}
-
-// diagnostic store ceiling (CG_WRITE_PROBE): fill the writer's slices of the
-// output with W*8-byte-per-lane stores, 64 lanes contiguous
-template <int W>
-__global__ __launch_bounds__(kWriteWaves * 64) void k_fill_probe(const int64_t* __restrict__ run_off,
-                                                                 int64_t nruns, int64_t cap,
-                                                                 int64_t* __restrict__ times) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t E = run_off[nruns];
-  if (E > cap) return;
-  const int64_t kSup = int64_t(1) << super_shift(cap);
-  if (W == 6 || W == 7) {  // per-wave streams with a pause (s_sleep) after every 24 stores
-    const int64_t nsup = (E + kSup - 1) / kSup;
-    const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
-    for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
-      const int64_t p0 = c * kSup, p1 = E - p0 < kSup ? E : p0 + kSup;
-      int k = 0;
-      for (int64_t b = p0 + lane; b < p1; b += 64) {
-        times[b] = b;
-        if (++k == 24) {
-          k = 0;
-          if (W == 6) __builtin_amdgcn_s_sleep(16);
-          else __builtin_amdgcn_s_sleep(64);
-        }
-      }
-    }
-    return;
-  }
-  if (W == 4) {  // block-wide streams: the 4 waves interleave 512 B pieces of one slice
-    const int64_t nsup = (E + kSup - 1) / kSup;
-    for (int64_t c = blockIdx.x; c < nsup; c += gridDim.x) {
-      const int64_t p0 = c * kSup, p1 = E - p0 < kSup ? E : p0 + kSup;
-      for (int64_t b = p0 + wave * 64 + lane; b < p1; b += 64 * kWriteWaves) times[b] = b;
-    }
-    return;
-  }
-  const int64_t nsup = (E + kSup - 1) / kSup;
-  const int64_t nwaves = int64_t(gridDim.x) * kWriteWaves;
-  for (int64_t c = int64_t(blockIdx.x) * kWriteWaves + wave; c < nsup; c += nwaves) {
-    const int64_t p0 = c * kSup + (W == 3 ? 8 : 0), p1 = E - c * kSup < kSup ? E : c * kSup + kSup;
-    for (int64_t b = p0 + lane * (W == 3 ? 1 : W); b < p1; b += 64 * (W == 3 ? 1 : W)) {
-      if (W == 2 && b + 1 < p1) {
-        longlong2 v;
-        v.x = b;
-        v.y = b + 1;
-        *reinterpret_cast<longlong2*>(times + b) = v;
-      } else {
-        times[b] = b;
-      }
-    }
-  }
-}
 
 #ifndef CG_WALK_WPE
 #define CG_WALK_WPE 5  // register budget of k_write_walk: 5 waves per SIMD (98 -> 96 VGPRs, 12 B spill; 0.41 -> 0.37 ms on a DST day)
@@ -1577,6 +826,28 @@ __global__ __launch_bounds__(256) void k_count_eq(const T* __restrict__ v, int64
   if (threadIdx.x == 0) atomicAdd(out, (unsigned long long)(s[0] + s[1] + s[2] + s[3]));
 }
 
+// Store ceiling (cg_fill_rate_device): every lane writes 16 B per store, a
+// wave 1 KB of consecutive bytes, four stores in flight per lane per round;
+// the grid strides over the whole buffer.  No loads: nothing ever drains.
+typedef int v4i32 __attribute__((ext_vector_type(4)));
+template <bool kNT>
+__global__ __launch_bounds__(256) void k_fill_stream(v4i32* __restrict__ p, int64_t n16) {
+  const int64_t stride = int64_t(gridDim.x) * blockDim.x;
+  int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  const v4i32 v = {int(0x5EED0000u), 0x5EED, int(0x5EED0000u), 0x5EED};
+  for (; i + 3 * stride < n16; i += 4 * stride) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (kNT) __builtin_nontemporal_store(v, p + i + u * stride);
+      else p[i + u * stride] = v;
+    }
+  }
+  for (; i < n16; i += stride) {
+    if (kNT) __builtin_nontemporal_store(v, p + i);
+    else p[i] = v;
+  }
+}
+
 int grid_for(int64_t n, int threads, int max_blocks) {
   int64_t b = (n + threads - 1) / threads;
   if (b < 1) b = 1;
@@ -1613,6 +884,17 @@ void launch_count_eq(const void* v, int64_t n, int elem_bytes, int64_t x, unsign
   else
     hipLaunchKernelGGL(k_count_eq<int32_t>, dim3(grid), dim3(256), 0, st, static_cast<const int32_t*>(v), n,
                        int32_t(x), out);
+}
+
+void launch_fill_stream(void* p, int64_t n16, int nt, hipStream_t st) {
+  if (n16 <= 0) return;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int grid = grid_for((n16 + 3) / 4, 256, cus * 8);  // 8 blocks of 4 waves per CU: full occupancy
+  if (nt)
+    hipLaunchKernelGGL(k_fill_stream<true>, dim3(grid), dim3(256), 0, st, static_cast<v4i32*>(p), n16);
+  else
+    hipLaunchKernelGGL(k_fill_stream<false>, dim3(grid), dim3(256), 0, st, static_cast<v4i32*>(p), n16);
 }
 
 void launch_next_batch(const DSpec* specs, int64_t n, const PlanArgs& p, const int64_t* t_in,
@@ -1758,121 +1040,16 @@ void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_a
                      int64_t nruns, int64_t* chunk_run, int64_t cap, int64_t* times,
                      int n_blocks, hipStream_t st) {
   const size_t lds = size_t(p.G) * sizeof(Segment);
-#ifndef CG_DIAG
-  // production build: the writer, nothing else (the probes and store-dropping
-  // variants below exist only in the diagnostic library, `make diag`)
-#if CG_WRITE_LOADER
-  // persistent k_write_lw grid: as many blocks per CU as its registers and
-  // LDS (slots + the plan's segments) let run at once
-  static int lw_per_cu[2] = {0, 0};  // by whether the segments fit the small-LDS case
-  const int key = lds <= 4096 ? 0 : 1;
-  if (!lw_per_cu[key]) {
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write_lw<0>, (kLwWriters + 1) * 64,
-                                                     key ? kMaxSegments * sizeof(Segment) : 4096) != hipSuccess ||
-        n < 1)
-      n = 1;
-    lw_per_cu[key] = n;
-  }
-  const int cus = std::max(1, n_blocks / kWriteBlocksPerCU);
-  hipLaunchKernelGGL(k_write_lw<0>, dim3(cus * lw_per_cu[key]), dim3((kLwWriters + 1) * 64), lds, st, specs,
-                     p, run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
-#else
-  // CG_WRITE_SPARE_BLOCKS block slots left to the next pipelined call's
-  // count and scan (they run beside the persistent writer instead of after it)
-  const int nb = std::max(1, n_blocks - CG_WRITE_SPARE_BLOCKS);
-  hipLaunchKernelGGL(k_write_cf<0>, dim3(nb), dim3(kWriteWaves * 64), lds, st, specs, p,
-                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
+#ifdef CG_DIAG
+  // the diagnostic library only (`make diag`): store-ceiling probes and the
+  // experimental loader/writer split replace the writer when asked for
+  // (CG_WRITE_PROBE / CG_WRITE_VARIANT, cg_diag.hip)
+  if (launch_write_diag(specs, p, run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times, n_blocks,
+                        lds, st))
+    return;
 #endif
-#else
-  // CG_WRITE_PROBE (diagnostic build only): replace the
-  // writer by a plain fill of the same E*8 output bytes, same grid and slices,
-  // with 8 B (1) or 16 B (2) per lane per store -- the store ceiling the
-  // writer is compared against.
-  static const int probe = [] {
-    const char* e = getenv("CG_WRITE_PROBE");
-    return e ? atoi(e) : 0;
-  }();
-  if (probe == 1) {
-    hipLaunchKernelGGL(k_fill_probe<1>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
-                       nruns, cap, times);
-    return;
-  }
-  if (probe == 4) {
-    hipLaunchKernelGGL(k_fill_probe<4>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
-                       nruns, cap, times);
-    return;
-  }
-  if (probe == 6) {
-    hipLaunchKernelGGL(k_fill_probe<6>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
-                       nruns, cap, times);
-    return;
-  }
-  if (probe == 7) {
-    hipLaunchKernelGGL(k_fill_probe<7>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
-                       nruns, cap, times);
-    return;
-  }
-  if (probe == 5) {  // hipMemsetAsync of the capacity (>= the E*8 bytes)
-    (void)hipMemsetAsync(times, 0, size_t(cap) * 8, st);
-    return;
-  }
-  if (probe == 3) {  // 8 B per lane, every store instruction 64 B off a 512 B boundary
-    hipLaunchKernelGGL(k_fill_probe<3>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
-                       nruns, cap, times);
-    return;
-  }
-  if (probe == 2) {
-    hipLaunchKernelGGL(k_fill_probe<2>, dim3(n_blocks), dim3(kWriteWaves * 64), 0, st, run_off,
-                       nruns, cap, times);
-    return;
-  }
-  static const int variant = [] {
-    const char* e = getenv("CG_WRITE_VARIANT");  // diagnostic only (see put<V>)
-    return e ? atoi(e) : 0;
-  }();
-#define CG_WCF(V)                                                                             \
-  hipLaunchKernelGGL(k_write_cf<V>, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p, \
-                     run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times)
-  if (variant == 256) {  // k_write_lw with wait counters
-    int n = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_write_lw<32>, (kLwWriters + 1) * 64, lds);
-    const int blocks = std::max(1, n_blocks / kWriteBlocksPerCU) * std::max(n, 1);
-    hipLaunchKernelGGL(k_write_lw<32>, dim3(blocks), dim3((kLwWriters + 1) * 64), lds, st, specs, p,
-                       run_anchor, run_count, run_dmask, run_off, nruns, chunk_run, cap, times);
-    unsigned long long d[8];
-    (void)hipMemcpyAsync(d, chunk_run + (cap >> super_shift(cap)) + 2 + kTicketWords, sizeof d,
-                         hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
-    fprintf(stderr, "[k_write_lw stats] blocks=%d err=%llu loader idle rounds=%llu writer waits=%llu\n", blocks,
-            d[0], d[1], d[2]);
-    return;
-  }
-  switch (variant) {
-    case 1: CG_WCF(1); break;
-    case 2: CG_WCF(2); break;
-    case 4: CG_WCF(4); break;
-    case 8: CG_WCF(8); break;
-    case 12: CG_WCF(12); break;
-    case 16: CG_WCF(16); break;
-    case 32: CG_WCF(32); break;
-    case 76: CG_WCF(76); break;
-    case 128: CG_WCF(128); break;
-    default: CG_WCF(0); break;
-  }
-#undef CG_WCF
-  if (variant & 32) {
-    unsigned long long d[8];
-    (void)hipMemcpyAsync(d, chunk_run + (cap >> super_shift(cap)) + 2 + kTicketWords, sizeof d,
-                         hipMemcpyDeviceToHost, st);
-    (void)hipStreamSynchronize(st);
-    fprintf(stderr,
-            "[k_write_cf stats] waves=%llu cycles/wave: all=%.0f window=%.0f coop=%.0f tiny=%.0f | "
-            "per wave: windows=%.1f coop_pieces=%.1f tiny_pieces=%.1f\n",
-            d[7], double(d[0]) / d[7], double(d[1]) / d[7], double(d[2]) / d[7], double(d[3]) / d[7],
-            double(d[4]) / d[7], double(d[5]) / d[7], double(d[6]) / d[7]);
-  }
-#endif  // CG_DIAG
+  hipLaunchKernelGGL(k_write_cf, dim3(n_blocks), dim3(kWriteWaves * 64), lds, st, specs, p, run_anchor, run_count,
+                     run_dmask, run_off, nruns, chunk_run, cap, times);
 }
 
 void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const int64_t* run_anchor,

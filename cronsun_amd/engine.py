@@ -460,6 +460,14 @@ class Engine:
         """Fill a device buffer with one byte value (cg_fill_device)."""
         check(lib().cg_fill_device(self._h, C.c_void_p(d_ptr), int(nbytes), int(byte_value)))
 
+    def fill_rates(self, d_ptr, nbytes, reps=5):
+        """Store ceiling of this device over nbytes of a device buffer
+        (cg_fill_rate_device): mean ms of k_fill_stream with nontemporal
+        stores, with plain stores, and of hipMemsetAsync."""
+        ms = (C.c_float * 3)()
+        check(lib().cg_fill_rate_device(self._h, C.c_void_p(d_ptr), int(nbytes), int(reps), ms))
+        return {"fill_stream_nt": ms[0], "fill_stream_plain": ms[1], "hipMemsetAsync": ms[2]}
+
     def count_value(self, d_ptr, n, elem_bytes=8, value=-1):
         """Elements of a device array equal to value (cg_count_value_device)."""
         out = C.c_int64()

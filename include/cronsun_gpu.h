@@ -275,7 +275,16 @@ int cg_expand_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64
  * call issued since the last wait, returns the first error among them (a
  * rule whose reference loop never ends: CG_ERANGE, as cg_expand_device), and
  * sets *n_events of the last call, whose result the accessors below then
- * read.  cg_last_kernel_times [3] = the mean write time of those calls. */
+ * read.  cg_last_kernel_times [3] = the mean write time of those calls.
+ * Every call writes into the same output buffer: after the wait only the
+ * LAST call's result is readable (earlier calls leave nothing readable), and
+ * a returned error may belong to any call since the previous wait (its
+ * message names the rule or the sizes).  *n_events is always set (0 when no
+ * asynchronous call was made).  While calls are pending the result accessors
+ * below refuse with CG_EINVAL.  A synchronous expansion (cg_expand,
+ * cg_expand_device, cg_count, cg_expand_per_node*) made while calls are
+ * pending drains them and discards their results and errors: call
+ * cg_expand_wait first to observe them. */
 int cg_expand_device_async(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
                            int64_t t1);
 int cg_expand_wait(cg_ctx* ctx, int64_t* n_events);
@@ -315,6 +324,17 @@ int cg_checksum_device(cg_ctx* ctx, const void* d_ptr, int64_t n, int elem_bytes
 int cg_fill_device(cg_ctx* ctx, void* d_ptr, int64_t bytes, int byte_value);
 int cg_count_value_device(cg_ctx* ctx, const void* d_ptr, int64_t n, int elem_bytes, int64_t value,
                           int64_t* count);
+/* The store ceiling of this device (instrumentation; no reference
+ * counterpart): the rate at which `bytes` (a multiple of 16) of the device
+ * buffer d_ptr can be written, measured on the ctx stream with HIP events as
+ * the mean over `reps` launches after one warm-up, for three fills:
+ *   ms[0]  k_fill_stream, 16 B per lane nontemporal stores, a grid-stride
+ *          loop over the whole buffer at full occupancy (one launch);
+ *   ms[1]  the same with plain stores;
+ *   ms[2]  hipMemsetAsync of the same bytes.
+ * The output-bound kernels' roofline fractions are also reported against the
+ * fastest of the three.  The buffer's contents are overwritten. */
+int cg_fill_rate_device(cg_ctx* ctx, void* d_ptr, int64_t bytes, int reps, float* ms /* [3] */);
 
 /* --------------------------------------------- rule -> node resolution --- */
 /* Integer-interned jobs/groups (host interns string IDs; see cg_jobset_*).

@@ -10,6 +10,11 @@
 // per-node Job.Cmds filter (job.go:591-614, driven by node/node.go:121-158),
 // Cmd.lockTtl (job.go:194-233) and Cron.run's wake loop (cron.go:210-275).
 //
+// cgo rules kept: Go memory passed to C never holds Go pointers (structs that
+// point at buffers, and those buffers, are C.malloc'ed), and every wrapper that
+// passes a handle keeps its owner alive across the call (runtime.KeepAlive;
+// Specs and Dispatcher hold their Engine).  Needs Go >= 1.17 (unsafe.Slice).
+//
 // Go is not installed in the image this package was written in, so it is not
 // compiled there; tests/native/abi_c.c runs the same call sequence against the
 // header in C (gcc -std=c11) and, on an MI355X, against the library.
@@ -102,10 +107,13 @@ func FixedZone(offsetSec int) (*Zone, error) {
 	return newZone(z), nil
 }
 
-// Specs is a rule set resident in HBM (32 B per rule).
+// Specs is a rule set resident in HBM (32 B per rule).  It keeps its Engine
+// reachable: cg_specs_free reads the engine's context, so the Engine's
+// finalizer (cg_destroy) must not run first.
 type Specs struct {
 	s *C.cg_specs
 	n int
+	e *Engine
 }
 
 func (s *Specs) Len() int { return s.n }
@@ -135,8 +143,10 @@ func (e *Engine) Upload(scheds []cron.Schedule) (*Specs, error) {
 	if rc := C.cg_specs_upload_schedules(e.ctx, p, C.size_t(len(cs)), &out); rc != 0 {
 		return nil, lastErr(rc)
 	}
-	sp := &Specs{out, len(scheds)}
+	sp := &Specs{out, len(scheds), e}
 	runtime.SetFinalizer(sp, func(s *Specs) { C.cg_specs_free(s.s) })
+	runtime.KeepAlive(cs)
+	runtime.KeepAlive(e)
 	return sp, nil
 }
 
@@ -161,7 +171,11 @@ func (e *Engine) NextBatch(sp *Specs, z *Zone, t []time.Time) ([]time.Time, erro
 	for i := range t {
 		in[i] = C.int64_t(t[i].Unix())
 	}
-	if rc := C.cg_next_batch(e.ctx, sp.s, z.z, &in[0], &out[0]); rc != 0 {
+	rc := C.cg_next_batch(e.ctx, sp.s, z.z, &in[0], &out[0])
+	runtime.KeepAlive(e)
+	runtime.KeepAlive(sp)
+	runtime.KeepAlive(z)
+	if rc != 0 {
 		return nil, lastErr(rc)
 	}
 	res := make([]time.Time, len(t))
@@ -177,12 +191,21 @@ func (e *Engine) NextBatch(sp *Specs, z *Zone, t []time.Time) ([]time.Time, erro
 // (no times buffer: offsets and n_events only); the times are then copied out
 // of the engine's last result, so the horizon is expanded once.
 func (e *Engine) Expand(sp *Specs, z *Zone, t0, t1 time.Time) (offsets, times []int64, err error) {
-	offsets = make([]int64, sp.n+1)
-	var csr C.cg_csr
-	csr.offsets = (*C.int64_t)(unsafe.Pointer(&offsets[0]))
-	if rc := C.cg_expand(e.ctx, sp.s, z.z, C.int64_t(t0.Unix()), C.int64_t(t1.Unix()), &csr); rc != 0 {
+	defer runtime.KeepAlive(e)
+	defer runtime.KeepAlive(sp)
+	defer runtime.KeepAlive(z)
+	// The cg_csr struct holds a pointer, so it and the buffer it points to live
+	// in C memory: cgo forbids passing Go memory that holds a Go pointer.
+	csr := (*C.cg_csr)(C.calloc(1, C.size_t(unsafe.Sizeof(C.cg_csr{}))))
+	defer C.free(unsafe.Pointer(csr))
+	coff := (*C.int64_t)(C.malloc(C.size_t(sp.n+1) * 8))
+	defer C.free(unsafe.Pointer(coff))
+	csr.offsets = coff
+	if rc := C.cg_expand(e.ctx, sp.s, z.z, C.int64_t(t0.Unix()), C.int64_t(t1.Unix()), csr); rc != 0 {
 		return nil, nil, lastErr(rc)
 	}
+	offsets = make([]int64, sp.n+1)
+	copy(offsets, unsafe.Slice((*int64)(unsafe.Pointer(coff)), sp.n+1))
 	times = make([]int64, int64(csr.n_events))
 	if len(times) > 0 {
 		if rc := C.cg_result_copy_times(e.ctx, 0, csr.n_events, (*C.int64_t)(unsafe.Pointer(&times[0]))); rc != 0 {
@@ -206,8 +229,12 @@ func (e *Engine) LockTtls(sp *Specs, z *Zone, now time.Time, kinds []int32, avgM
 		t[i] = C.int64_t(now.Unix())
 	}
 	out := make([]int64, sp.n)
-	if rc := C.cg_lock_ttl_batch(e.ctx, sp.s, z.z, &t[0], (*C.int32_t)(unsafe.Pointer(&kinds[0])),
-		(*C.int64_t)(unsafe.Pointer(&avgMs[0])), C.int64_t(lockTtl), (*C.int64_t)(unsafe.Pointer(&out[0]))); rc != 0 {
+	rc := C.cg_lock_ttl_batch(e.ctx, sp.s, z.z, &t[0], (*C.int32_t)(unsafe.Pointer(&kinds[0])),
+		(*C.int64_t)(unsafe.Pointer(&avgMs[0])), C.int64_t(lockTtl), (*C.int64_t)(unsafe.Pointer(&out[0])))
+	runtime.KeepAlive(e)
+	runtime.KeepAlive(sp)
+	runtime.KeepAlive(z)
+	if rc != 0 {
 		return nil, lastErr(rc)
 	}
 	return out, nil
@@ -310,6 +337,13 @@ func (j *Jobset) Schedules() []cron.Schedule { return j.scheds }
 // byTime set in the order a node's Cron keeps its entries (sort.Sort(byTime),
 // cron.go:64-79: times ascending, equal times in rule order).
 func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, mode int, byTime bool) (map[string][]Fire, error) {
+	defer runtime.KeepAlive(e)
+	defer runtime.KeepAlive(sp)
+	defer runtime.KeepAlive(z)
+	defer runtime.KeepAlive(j)
+	// cg_rules_in holds C pointers into the jobset (C memory): it may live in Go
+	// memory.  cg_node_csr would hold a pointer to the node offsets, so it and
+	// that buffer live in C memory (cgo's rule on Go pointers to Go pointers).
 	var rin C.cg_rules_in
 	if rc := C.cg_jobset_rules(j.js, &rin); rc != 0 {
 		return nil, lastErr(rc)
@@ -317,13 +351,18 @@ func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, 
 	if int(rin.n_rules) != sp.n {
 		return nil, fmt.Errorf("gpu: ExpandPerNode: %d specs for %d rules", sp.n, int(rin.n_rules))
 	}
-	nodeOff := make([]int64, int(rin.n_nodes)+1)
-	var out C.cg_node_csr // no event buffers: node offsets and n_events only
-	out.node_off = (*C.int64_t)(unsafe.Pointer(&nodeOff[0]))
+	nn := int(rin.n_nodes)
+	out := (*C.cg_node_csr)(C.calloc(1, C.size_t(unsafe.Sizeof(C.cg_node_csr{})))) // no event buffers: node offsets and n_events only
+	defer C.free(unsafe.Pointer(out))
+	coff := (*C.int64_t)(C.malloc(C.size_t(nn+1) * 8))
+	defer C.free(unsafe.Pointer(coff))
+	out.node_off = coff
 	if rc := C.cg_expand_per_node(e.ctx, sp.s, z.z, C.int64_t(t0.Unix()), C.int64_t(t1.Unix()), &rin,
-		C.int(mode), &out); rc != 0 {
+		C.int(mode), out); rc != 0 {
 		return nil, lastErr(rc)
 	}
+	nodeOff := make([]int64, nn+1)
+	copy(nodeOff, unsafe.Slice((*int64)(unsafe.Pointer(coff)), nn+1))
 	if byTime {
 		if rc := C.cg_node_result_order_by_time(e.ctx); rc != 0 {
 			return nil, lastErr(rc)
@@ -366,15 +405,20 @@ func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, 
 //		case id := <-c.del: d.Remove([]int64{slot(id)})
 //		}
 //	}
-type Dispatcher struct{ d *C.cg_dispatcher }
+type Dispatcher struct {
+	d *C.cg_dispatcher
+	e *Engine // cg_dispatcher_free locks the engine's context: keep it reachable
+}
 
 func (e *Engine) NewDispatcher(sp *Specs, z *Zone, now time.Time) (*Dispatcher, error) {
 	var d *C.cg_dispatcher
 	if rc := C.cg_dispatcher_new(e.ctx, sp.s, z.z, C.int64_t(now.Unix()), &d); rc != 0 {
 		return nil, lastErr(rc)
 	}
-	dd := &Dispatcher{d}
+	dd := &Dispatcher{d, e}
 	runtime.SetFinalizer(dd, func(d *Dispatcher) { C.cg_dispatcher_free(d.d) })
+	runtime.KeepAlive(sp)
+	runtime.KeepAlive(z)
 	return dd, nil
 }
 
@@ -382,7 +426,9 @@ func (e *Engine) NewDispatcher(sp *Specs, z *Zone, now time.Time) (*Dispatcher, 
 // zero time when nothing can fire.
 func (d *Dispatcher) Effective() (time.Time, error) {
 	var eff C.int64_t
-	if rc := C.cg_dispatcher_effective(d.d, &eff); rc != 0 {
+	rc := C.cg_dispatcher_effective(d.d, &eff)
+	runtime.KeepAlive(d)
+	if rc != 0 {
 		return time.Time{}, lastErr(rc)
 	}
 	return unixOf(eff, time.Local), nil
@@ -390,6 +436,7 @@ func (d *Dispatcher) Effective() (time.Time, error) {
 
 // Fire is one wake at now (cron.go:234-244): the due slots, ascending.
 func (d *Dispatcher) Fire(now time.Time) ([]int32, error) {
+	defer runtime.KeepAlive(d)
 	var n, eff C.int64_t
 	if rc := C.cg_dispatcher_fire(d.d, C.int64_t(now.Unix()), &n, &eff); rc != 0 {
 		return nil, lastErr(rc)
@@ -424,8 +471,10 @@ func (d *Dispatcher) Set(idx []int64, scheds []cron.Schedule, now time.Time) err
 			return ErrUnsupported
 		}
 	}
-	if rc := C.cg_dispatcher_set(d.d, (*C.int64_t)(unsafe.Pointer(&idx[0])), &cs[0], C.size_t(len(cs)),
-		C.int64_t(now.Unix())); rc != 0 {
+	rc := C.cg_dispatcher_set(d.d, (*C.int64_t)(unsafe.Pointer(&idx[0])), &cs[0], C.size_t(len(cs)),
+		C.int64_t(now.Unix()))
+	runtime.KeepAlive(d)
+	if rc != 0 {
 		return lastErr(rc)
 	}
 	return nil
@@ -436,7 +485,9 @@ func (d *Dispatcher) Remove(idx []int64) error {
 	if len(idx) == 0 {
 		return nil
 	}
-	if rc := C.cg_dispatcher_remove(d.d, (*C.int64_t)(unsafe.Pointer(&idx[0])), C.size_t(len(idx))); rc != 0 {
+	rc := C.cg_dispatcher_remove(d.d, (*C.int64_t)(unsafe.Pointer(&idx[0])), C.size_t(len(idx)))
+	runtime.KeepAlive(d)
+	if rc != 0 {
 		return lastErr(rc)
 	}
 	return nil

@@ -380,3 +380,33 @@ def test_short_windows_after_a_day(eng, width):
         eo, et = O.expand_batch(oarr, t0, t1, oracle_zone("UTC"), threads=8)
         assert np.array_equal(off, eo), (width, t0)
         assert np.array_equal(times, et), (width, t0)
+
+
+def test_async_result_hygiene():
+    """cg_expand_wait with nothing pending sets n_events = 0; the result
+    accessors refuse while asynchronous calls are pending; a synchronous call
+    made while a failing asynchronous call is pending discards that call's
+    error (the next wait reports only its own calls)."""
+    from cronsun_amd.engine import Engine
+    from cronsun_amd._lib import check, lib
+    e2 = Engine(0)
+    specs = synth.spec_mix(5_000, seed=13)
+    arr, status = cron.parse_batch(specs)
+    sp = e2.upload_c(arr, len(specs))
+    t0 = synth.T0_2026
+    E = e2.expand_device(sp, None, t0, t0 + DAY)
+    assert e2.expand_wait() == 0
+    e2.expand_async(sp, None, t0, t0 + DAY)
+    off = np.empty(len(specs) + 1, dtype=np.int64)
+    with pytest.raises(_lib.CgError) as err:
+        check(lib().cg_result_copy_offsets(e2._h, off.ctypes.data))
+    assert err.value.code == _lib.CG_EINVAL
+    assert e2.expand_wait() == E
+    check(lib().cg_result_copy_offsets(e2._h, off.ctypes.data))
+    assert off[-1] == E
+    e2.expand_async(sp, None, t0, t0 + 30 * DAY)  # exceeds the capacity: CG_ECAPACITY at a wait
+    E2 = e2.expand_device(sp, None, t0, t0 + 3600)  # drains and discards it
+    e2.expand_async(sp, None, t0, t0 + 3600)
+    assert e2.expand_wait() == E2
+    sp.free()
+    e2.close()

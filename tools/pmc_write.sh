@@ -13,10 +13,10 @@ pass() {  # name counters... (env via PMC_ENV)
   python3 tools/pmc_traffic.py --sq $O/$name --out $O/$name.json > /dev/null
   python3 -c "import json; d=json.load(open('$O/$name.json'))['kernels']; k=d.get('k_write_cf') or d.get('k_fill_probe'); print('$name', json.dumps(k))"
 }
-for mode in base compute; do
+for mode in base fill16; do
   case $mode in
     base) PMC_ENV="X=0";;
-    compute) PMC_ENV="CG_WRITE_VARIANT=1";;
+    fill16) PMC_ENV="CG_WRITE_PROBE=2";;
   esac
   pass ${mode}_sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU
 done

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Diagnostic matrix for k_write_cf on the bench workload (no parity checks):
 #   CG_WRITE_PROBE=1/2   plain fill of the same bytes (8/16 B per lane): store ceiling
-#   CG_WRITE_VARIANT=1   writer without stores (compute only); =2 non-temporal stores
+#   CG_WRITE_VARIANT=255 the loader/writer split k_write_lw (cg_diag.hip)
 #   CG_WRITE_BLOCKS_PER_CU  persistent grid size
 set -o pipefail
 # the probe/variant switches exist only in the diagnostic build (make -C cronsun_amd/csrc diag)
