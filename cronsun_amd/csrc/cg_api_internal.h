@@ -187,6 +187,9 @@ struct cg_ctx {
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
+  // the segment records, rule-major times and offsets still describe the last
+  // per-node result (k_node_timed reads them); any expansion clears it
+  bool pn_recs_valid = false;
   int64_t* pn_res_host = nullptr;  // mapped pinned: per-node event total of the last call
   int64_t* pn_res_dev = nullptr;
   // the rule->node join + transpose depend only on (rule set, exclude mode):

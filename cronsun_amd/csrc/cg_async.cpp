@@ -99,6 +99,7 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
     return cg_fail(CG_ECAPACITY, "cg_expand_device_async: no output capacity yet (run cg_expand_device once)");
   int rc = ensure_async(c);
   if (rc) return rc;
+  c->pn_recs_valid = false;  // the rule-major buffers are about to change
   const int k = c->as_next;
   AsyncSet& a = c->as[k];
   // the set was last used kAsyncSets calls ago: its writer must be done

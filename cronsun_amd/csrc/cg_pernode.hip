@@ -665,6 +665,39 @@ __global__ __launch_bounds__(256) void k_node_write(
   }
 }
 
+// One rank's per-node slice placed into the gathered per-node CSR
+// (cg_node_csr_place): node n's events [src_off[n], src_off[n+1]) go to
+// dst_start[n] onwards, rules shifted to global indices.  One block per node
+// (grid-stride over nodes), four loads in flight per thread.
+__global__ __launch_bounds__(256) void k_node_place(const int64_t* __restrict__ src_off, int32_t N,
+                                                     const int64_t* __restrict__ src_time,
+                                                     const int32_t* __restrict__ src_rule, int32_t rule_add,
+                                                     const int64_t* __restrict__ dst_start,
+                                                     int64_t* __restrict__ dst_time, int32_t* __restrict__ dst_rule) {
+  for (int64_t n = blockIdx.x; n < N; n += gridDim.x) {
+    const int64_t a = src_off[n], b = src_off[n + 1], d = dst_start[n] - a;
+    int64_t i = a + threadIdx.x;
+    for (; i + 768 < b; i += 1024) {
+      int64_t t[4];
+      int32_t r[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        t[u] = src_time[i + 256 * u];
+        r[u] = src_rule[i + 256 * u];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        dst_time[i + 256 * u + d] = t[u];
+        dst_rule[i + 256 * u + d] = r[u] + rule_add;
+      }
+    }
+    for (; i < b; i += 256) {
+      dst_time[i + d] = src_time[i];
+      dst_rule[i + d] = src_rule[i] + rule_add;
+    }
+  }
+}
+
 // persistent k_node_write grid: as many 4-wave blocks per CU as its register
 // and LDS use let run at once (no block of the grid waits for a slot)
 int node_write_blocks_per_cu() {
@@ -954,6 +987,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   (void)hipEventElapsedTime(&c->kt[7], c->pev[1], c->pev[2]);
   (void)hipEventElapsedTime(&c->kt[8], c->pev[2], c->pev[3]);
   c->pn_E = En;
+  c->pn_recs_valid = true;
   c->pn_nnz = nnz;
   c->pn_N = N;
   c->pn_t0 = t0;
@@ -1121,6 +1155,23 @@ int cg_node_result_copy_range(cg_ctx* c, int64_t first, int64_t count, int64_t* 
                          "copy rule")))
     return rc;
   return CG_OK;
+}
+
+int cg_node_csr_place(cg_ctx* c, int32_t n_nodes, const int64_t* d_src_node_off, const int64_t* d_src_time,
+                      const int32_t* d_src_rule, int32_t rule_add, const int64_t* d_dst_start, int64_t* d_dst_time,
+                      int32_t* d_dst_rule) {
+  if (!c || n_nodes < 0 || (n_nodes > 0 && (!d_src_node_off || !d_dst_start)))
+    return cg_fail(CG_EINVAL, "cg_node_csr_place: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
+  if (rc) return rc;
+  if (n_nodes > 0)
+    hipLaunchKernelGGL(k_node_place, dim3(unsigned(std::min<int64_t>(n_nodes, int64_t(c->write_blocks) * 2))),
+                       dim3(256), 0, c->st, d_src_node_off, n_nodes, d_src_time, d_src_rule, rule_add, d_dst_start,
+                       d_dst_time, d_dst_rule);
+  if ((rc = cg_hip_check(hipGetLastError(), "k_node_place"))) return rc;
+  return cg_hip_check(hipStreamSynchronize(c->st), "sync");
 }
 
 int cg_node_counts_to_device(cg_ctx* c, int64_t* d_counts) {

@@ -453,6 +453,14 @@ class Engine:
         lib().cg_last_kernel_times(self._h, buf, 13)
         return buf[12]
 
+    def node_csr_place(self, n_nodes, src_node_off, src_time, src_rule, rule_add, dst_start, dst_time, dst_rule):
+        """Place one rank's per-node slice into the gathered per-node CSR on
+        this engine's device (cg_node_csr_place); arguments are device
+        pointers (ints), e.g. torch tensors' data_ptr()."""
+        check(lib().cg_node_csr_place(self._h, int(n_nodes), C.c_void_p(src_node_off), C.c_void_p(src_time),
+                                      C.c_void_p(src_rule), int(rule_add), C.c_void_p(dst_start),
+                                      C.c_void_p(dst_time), C.c_void_p(dst_rule)))
+
     def node_counts_to_device(self, d_ptr):
         check(lib().cg_node_counts_to_device(self._h, C.c_void_p(d_ptr)))
 

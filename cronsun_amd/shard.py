@@ -162,7 +162,47 @@ def gather_csr(local_offsets, local_times, dist, dst=0):
     return offsets, times
 
 
-def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst=0):
+def node_slice_starts(allc, rank):
+    """Per-node destinations of rank `rank`'s slices in the gathered per-node
+    CSR: node_base[n] + sum_{g' < rank} count[g'][n] (allc: [world, N]
+    all-gathered counts).  Returns (starts [N], node_base [N + 1])."""
+    import torch
+    per_node = allc.sum(dim=0)
+    node_base = torch.zeros(allc.shape[1] + 1, dtype=torch.int64, device=allc.device)
+    node_base[1:] = torch.cumsum(per_node, dim=0)
+    before = allc[:rank].sum(dim=0) if rank > 0 else torch.zeros_like(per_node)
+    return node_base[:-1] + before, node_base
+
+
+def place_node_slice(node_off, time, rule, rule_add, starts, out_time, out_rule, engine=None):
+    """Copy one rank's per-node slice (node_off [N+1] from 0, time, rule) to
+    out_time / out_rule at starts[n] per node, rules + rule_add.  Device
+    tensors go through the library's kernel (cg_node_csr_place); host tensors
+    (gloo runs on CPU) are copied per node."""
+    import torch
+    N = node_off.numel() - 1
+    if time.is_cuda:
+        if engine is None:
+            if (time.device.index or 0) != 0:
+                raise ValueError("place_node_slice: pass the Engine of the tensors' device")
+            from .engine import default_engine
+            engine = default_engine()
+        torch.cuda.synchronize(time.device)  # the library runs on its own stream
+        engine.node_csr_place(N, node_off.data_ptr(), time.data_ptr(), rule.data_ptr(), int(rule_add),
+                              starts.contiguous().data_ptr(), out_time.data_ptr(), out_rule.data_ptr())
+        return
+    off = node_off.numpy()
+    st = starts.numpy()
+    t, r = time.numpy(), rule.numpy()
+    ot, orl = out_time.numpy(), out_rule.numpy()
+    for n in range(N):
+        a, b = int(off[n]), int(off[n + 1])
+        if b > a:
+            ot[st[n]:st[n] + b - a] = t[a:b]
+            orl[st[n]:st[n] + b - a] = r[a:b] + rule_add
+
+
+def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst=0, engine=None):
     """Gather the per-node (time, rule) CSR of job-ID-range shards on rank `dst`.
 
     local_node_off: int64 tensor [N+1] (this rank's node offsets, from 0);
@@ -175,7 +215,8 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
     collective node_offsets uses).  Payload: one isend of each array per rank
     into a staging buffer on `dst` (one xGMI link per peer, all in flight
     together), then each rank's slice of node n is placed at
-    node_base[n] + sum_{g' < g} count[g'][n] by one index scatter per rank."""
+    node_base[n] + sum_{g' < g} count[g'][n] by the library's placement
+    kernel (cg_node_csr_place; rule indices made global there)."""
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
     dev = local_time.device
@@ -185,22 +226,25 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
     dist.all_gather_into_tensor(allc, counts)
     allc = allc.view(world, N)
     sizes = allc.sum(dim=1).cpu().numpy()
-    grule = (local_rule.to(torch.int64) + int(rule_base)).to(torch.int32).contiguous()
+    # every rank's range base (the placement makes rule indices global)
+    base_t = torch.tensor([int(rule_base)], dtype=torch.int64, device=dev)
+    bases = torch.zeros(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(bases, base_t)
+    bases = bases.cpu().numpy()
     if rank != dst:
-        ops = [dist.P2POp(dist.isend, local_time.contiguous(), dst), dist.P2POp(dist.isend, grule, dst)]
+        ops = [dist.P2POp(dist.isend, local_time.contiguous(), dst),
+               dist.P2POp(dist.isend, local_rule.contiguous(), dst)]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
         return None
-    per_node = allc.sum(dim=0)
-    node_base = torch.zeros(N + 1, dtype=torch.int64, device=dev)
-    node_base[1:] = torch.cumsum(per_node, dim=0)
-    E = int(node_base[-1].item())
+    node_base = None
+    E = int(sizes.sum())
     out_time = torch.empty(E, dtype=torch.int64, device=dev)
     out_rule = torch.empty(E, dtype=torch.int32, device=dev)
     stage, ops = {}, []
     for g in range(world):
         if g == dst:
-            stage[g] = (local_time, grule)
+            stage[g] = (local_time.contiguous(), local_rule.contiguous())
             continue
         stage[g] = (torch.empty(int(sizes[g]), dtype=torch.int64, device=dev),
                     torch.empty(int(sizes[g]), dtype=torch.int32, device=dev))
@@ -208,16 +252,11 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-    before = torch.zeros(N, dtype=torch.int64, device=dev)
     for g in range(world):
-        c = allc[g]
+        starts, node_base = node_slice_starts(allc, g)
+        off = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+        off[1:] = torch.cumsum(allc[g], dim=0)
         if int(sizes[g]) > 0:
-            src_start = torch.cumsum(c, dim=0) - c
-            delta = node_base[:-1] + before - src_start  # destination - source, per node
-            dest = torch.arange(int(sizes[g]), dtype=torch.int64, device=dev) + \
-                torch.repeat_interleave(delta, c)
-            out_time[dest] = stage[g][0]
-            out_rule[dest] = stage[g][1]
-        before += c
+            place_node_slice(off, stage[g][0], stage[g][1], int(bases[g]), starts, out_time, out_rule, engine)
         stage[g] = None
     return node_base, out_time, out_rule

@@ -403,6 +403,19 @@ int cg_node_result_copy_range(cg_ctx* ctx, int64_t first, int64_t count, int64_t
 /* per-node event counts of the last per-node result, copied to a DEVICE
  * buffer of N int64 (e.g. a torch tensor for an RCCL allgather) */
 int cg_node_counts_to_device(cg_ctx* ctx, int64_t* d_counts);
+/* Multi-GPU per-node gather, placement step (north_star: RCCL "gathers the
+ * final per-node CSR"; the node lists node/node.go:121-158 builds from
+ * Job.Cmds over every job in job-ID order).  One rank's slice of the
+ * per-node CSR -- d_src_node_off[N+1] (from 0), d_src_time / d_src_rule
+ * (rule indices local to the rank's job-ID range) -- is copied on the ctx's
+ * device so that node n's slice starts at d_dst_start[n] (= the node's global
+ * offset plus the slices of the ranks before this one, from the all-gathered
+ * per-node counts) in d_dst_time / d_dst_rule, rule indices plus rule_add
+ * (the range's first global rule).  All pointers are device memory of the
+ * ctx's device; the call returns after the copy (stream synchronised). */
+int cg_node_csr_place(cg_ctx* ctx, int32_t n_nodes, const int64_t* d_src_node_off, const int64_t* d_src_time,
+                      const int32_t* d_src_rule, int32_t rule_add, const int64_t* d_dst_start,
+                      int64_t* d_dst_time, int32_t* d_dst_rule);
 
 /* Device-resident rule sets: a cg_rules_in validated and copied into HBM once
  * (as specs are by cg_specs_upload), then used by any number of per-node

@@ -161,3 +161,66 @@ def test_config4_sharded_ranges_stitch_to_unsharded():
     finally:
         A.close()
         B.close()
+
+
+def test_config3_sharded_ranges_place_to_unsharded(config3):
+    """North_star's second collective on one GPU: config 3 (1M jobs x 10k
+    nodes, 1 h) split into 2/4/8 job-ID ranges, every range's per-node CSR
+    computed alone on a second context and placed into the gathered per-node
+    CSR by the library's kernel (cg_node_csr_place: node n's slice of range g
+    at node_base[n] + sum_{g' < g} count[g'][n], rule indices made global),
+    exactly as shard.gather_node_csr does on rank 0 after the RCCL transfers.
+    The placed CSR must equal the unsharded one (order-sensitive device
+    checksums of times and rules), and a node sample is bit-exact against the
+    oracle (node.go:121-158 -> Job.Cmds over every job, in job-ID order)."""
+    import torch
+    from cronsun_amd.engine import Engine
+    eng, sp, drules, rin, (t0, t1), (eo, et) = config3
+    utc = cron.UTC()
+    En, _ = eng.expand_per_node_rules_device(sp, utc, t0, t1, drules, _lib.EXCLUDE_NONE)
+    node_off = np.empty(rin.n_nodes + 1, dtype=np.int64)
+    from cronsun_amd._lib import check, lib
+    check(lib().cg_node_result_copy(eng._h, node_off.ctypes.data, None, None, 0))
+    _, dt, dr, _ = eng.node_result_device()
+    ck_t, ck_r = eng.checksum(dt, En, 8), eng.checksum(dr, En, 4)
+    dev = torch.device("cuda", 0)
+    N, R = rin.n_nodes, rin.n_rules
+    B = Engine(0)
+    try:
+        arr, _ = cron.parse_batch(synth.spec_mix(R, seed=0x5EED + 3, mix=synth.MIX_CONFIG2), threads=16)
+        spB = B.upload_c(arr, R)
+        out_t = torch.empty(En, dtype=torch.int64, device=dev)
+        out_r = torch.empty(En, dtype=torch.int32, device=dev)
+        for world in (2, 4, 8):
+            ranges = [shard.shard_range(R, world, g) for g in range(world)]
+            parts = []
+            for lo, hi in ranges:
+                view = spB.slice(lo, hi - lo)
+                dr_g = B.upload_rules(rin.slice_rules(lo, hi))
+                parts.append((view, dr_g))
+            allc = torch.zeros(world, N, dtype=torch.int64, device=dev)
+            for g, (view, dr_g) in enumerate(parts):  # the per-node counts every rank all-gathers
+                B.expand_per_node_rules_device(view, utc, t0, t1, dr_g, _lib.EXCLUDE_NONE)
+                B.node_counts_to_device(allc[g].data_ptr())
+            assert int(allc.sum()) == En
+            out_t.fill_(-1)
+            for g, ((lo, hi), (view, dr_g)) in enumerate(zip(ranges, parts)):
+                B.expand_per_node_rules_device(view, utc, t0, t1, dr_g, _lib.EXCLUDE_NONE)
+                o, t, r, n = B.node_result_device()
+                starts, node_base = shard.node_slice_starts(allc, g)
+                B.node_csr_place(N, o, t, r, lo, starts.contiguous().data_ptr(), out_t.data_ptr(), out_r.data_ptr())
+                view.free()
+                dr_g.free()
+            torch.cuda.synchronize(dev)
+            assert np.array_equal(node_base.cpu().numpy(), node_off), world
+            assert B.checksum(out_t.data_ptr(), En, 8) == ck_t, world
+            assert B.checksum(out_r.data_ptr(), En, 4) == ck_r, world
+        nodes = np.sort(np.random.default_rng(303).choice(N, 24, replace=False))
+        roff, rules = O.node_rules(rin, _lib.EXCLUDE_NONE, nodes, threads=host_threads())
+        for k, n in enumerate(nodes):
+            exp_t, exp_r = O.node_list(eo, et, rules[roff[k]:roff[k + 1]])
+            a, b = int(node_off[n]), int(node_off[n + 1])
+            assert np.array_equal(out_r[a:b].cpu().numpy(), exp_r), n
+            assert np.array_equal(out_t[a:b].cpu().numpy(), exp_t), n
+    finally:
+        B.close()

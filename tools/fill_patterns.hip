@@ -79,6 +79,56 @@ __global__ __launch_bounds__(256) void k_ticket(long long* p, long long n, int S
   }
 }
 
+// per-wave slices by ticket from G counters (blocks round-robin over the
+// groups; group g hands out slices g, g + G, g + 2G, ...): k_write_cf's scheme
+__global__ __launch_bounds__(256) void k_ticket_groups(long long* p, long long n, int S, unsigned* tickets, int G) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x % G;
+  for (;;) {
+    unsigned t = 0;
+    if (lane == 0) t = atomicAdd(tickets + g * 32, 1u);
+    const long long c = g + (long long)G * __builtin_amdgcn_readfirstlane((int)t);
+    if (c * S >= n) break;
+    const long long e = (c + 1) * S < n ? (c + 1) * S : n;
+    for (long long i = c * S + lane; i < e; i += 64) p[i] = i;
+  }
+}
+
+// range tickets: group g (blocks b with b % G == g) owns the contiguous slice
+// range [g Q, (g + 1) Q) and hands it out in order; a wave whose group is used
+// up moves on to the next group's counter (until every group is used up)
+__global__ __launch_bounds__(256) void k_range_tickets(long long* p, long long n, int S, unsigned* tickets, int G) {
+  const int lane = threadIdx.x & 63;
+  const long long ns = (n + S - 1) / S, Q = (ns + G - 1) / G;
+  int g = blockIdx.x % G, hops = 0;
+  for (;;) {
+    unsigned t = 0;
+    if (lane == 0) t = atomicAdd(tickets + g * 32, 1u);
+    const long long k = __builtin_amdgcn_readfirstlane((int)t);
+    const long long c = g * Q + k;
+    if (k >= Q || c >= ns) {
+      if (++hops >= G) break;
+      g = g + 1 == G ? 0 : g + 1;
+      continue;
+    }
+    const long long e = (c + 1) * S < n ? (c + 1) * S : n;
+    for (long long i = c * S + lane; i < e; i += 64) p[i] = i;
+  }
+}
+
+// static per-wave slices, XCD-grouped: the waves of XCD x (blocks x, x + 8, ...)
+// take consecutive slices, so each XCD writes its own contiguous stretch per round
+__global__ __launch_bounds__(256) void k_slices_xcd(long long* p, long long n, int S) {
+  const int lane = threadIdx.x & 63;
+  const long long nw = (long long)gridDim.x * 4;
+  const long long per_xcd = (long long)(gridDim.x / 8) * 4;
+  const long long w = (long long)(blockIdx.x % 8) * per_xcd + (blockIdx.x / 8) * 4 + (threadIdx.x >> 6);
+  for (long long c = w; c * S < n; c += nw) {
+    const long long e = (c + 1) * S < n ? (c + 1) * S : n;
+    for (long long i = c * S + lane; i < e; i += 64) p[i] = i;
+  }
+}
+
 // per-block slices: the block's 4 waves interleave 64*W-event pieces of one slice of S events
 template <int W>
 __global__ __launch_bounds__(256) void k_block_slices(long long* p, long long n, int S) {
@@ -105,7 +155,7 @@ int main(int argc, char** argv) {
   long long* p = nullptr;
   unsigned* ticket = nullptr;
   CHK(hipMalloc(&p, n * 8));
-  CHK(hipMalloc(&ticket, 4));
+  CHK(hipMalloc(&ticket, 64 * 32 * 4));
   hipEvent_t a, b;
   CHK(hipEventCreate(&a));
   CHK(hipEventCreate(&b));
@@ -114,7 +164,7 @@ int main(int argc, char** argv) {
     CHK(hipDeviceSynchronize());
     float best = 1e9f, sum = 0.f;
     for (int r = 0; r < reps; r++) {
-      CHK(hipMemset(ticket, 0, 4));
+      CHK(hipMemset(ticket, 0, 64 * 32 * 4));
       CHK(hipEventRecord(a));
       launch();
       CHK(hipEventRecord(b));
@@ -130,7 +180,7 @@ int main(int argc, char** argv) {
     fflush(stdout);
   };
   timeit("hipMemsetAsync", [&] { CHK(hipMemsetAsync(p, 0, n * 8)); });
-  for (int bpc : {1, 2, 4, 8}) {
+  for (int bpc : {1}) {
     char nm[128];
     snprintf(nm, sizeof nm, "stride 16B/lane %d blk/CU", bpc);
     timeit(nm, [&] { hipLaunchKernelGGL((k_stride<2, false>), dim3(cus * bpc), dim3(256), 0, 0, p, n); });
@@ -139,19 +189,17 @@ int main(int argc, char** argv) {
     snprintf(nm, sizeof nm, "stride 8B/lane %d blk/CU", bpc);
     timeit(nm, [&] { hipLaunchKernelGGL((k_stride<1, false>), dim3(cus * bpc), dim3(256), 0, 0, p, n); });
   }
-  for (int S : {512, 2048, 16384}) {
-    for (int bpc : {1, 4}) {
+  for (int S : {2048, 4096}) {
+    for (int bpc : {4}) {
       char nm[128];
       snprintf(nm, sizeof nm, "wave slices S=%d 8B/lane %d blk/CU", S, bpc);
       timeit(nm, [&] { hipLaunchKernelGGL((k_slices<1, false>), dim3(cus * bpc), dim3(256), 0, 0, p, n, S); });
-      snprintf(nm, sizeof nm, "wave slices S=%d 16B/lane %d blk/CU", S, bpc);
-      timeit(nm, [&] { hipLaunchKernelGGL((k_slices<2, false>), dim3(cus * bpc), dim3(256), 0, 0, p, n, S); });
-      snprintf(nm, sizeof nm, "wave slices S=%d 8B/lane nt %d blk/CU", S, bpc);
-      timeit(nm, [&] { hipLaunchKernelGGL((k_slices<1, true>), dim3(cus * bpc), dim3(256), 0, 0, p, n, S); });
-      snprintf(nm, sizeof nm, "ticket slices S=%d 8B/lane %d blk/CU", S, bpc);
-      timeit(nm, [&] { hipLaunchKernelGGL((k_ticket<1>), dim3(cus * bpc), dim3(256), 0, 0, p, n, S, ticket); });
-      snprintf(nm, sizeof nm, "block slices S=%d 8B/lane %d blk/CU", S * 4, bpc);
-      timeit(nm, [&] { hipLaunchKernelGGL((k_block_slices<1>), dim3(cus * bpc), dim3(256), 0, 0, p, n, S * 4); });
+      snprintf(nm, sizeof nm, "32-group ticket slices S=%d 8B/lane %d blk/CU", S, bpc);
+      timeit(nm, [&] { hipLaunchKernelGGL(k_ticket_groups, dim3(cus * bpc), dim3(256), 0, 0, p, n, S, ticket, 32); });
+      for (int G : {8, 16, 32, 64}) {
+        snprintf(nm, sizeof nm, "%d-range tickets S=%d 8B/lane %d blk/CU", G, S, bpc);
+        timeit(nm, [&] { hipLaunchKernelGGL(k_range_tickets, dim3(cus * bpc), dim3(256), 0, 0, p, n, S, ticket, G); });
+      }
     }
   }
   CHK(hipFree(p));
