@@ -296,6 +296,22 @@ def main():
             wake["due"] += n_due
             wake["wakes"] += 1
             return n_due
+        if pn and pn_pipelined and last.get("pn_sized"):
+            # pipelined windows: window k+1's expansion and records overlap
+            # window k's per-node writer; one wait per step (the node events
+            # of every window come with it)
+            wins = list(range(t0, t1, W))
+            for a in wins:
+                eng.expand_per_node_async(sp, utc, a, min(a + W, t1), drules, xmode)
+            En_w, En = eng.expand_per_node_wait(with_total=True)
+            last["En_last"] = En_w
+            nk = eng.node_kernel_times()
+            last.update(kt=np.array(last["kt_sync"]), windows=len(wins),
+                        nkt=np.array([last["nkt_sync"][0], last["nkt_sync"][1], nk[2] * len(wins)]))
+            if world > 1:  # per-node offsets of every rank's slice of the last window
+                eng.node_counts_to_device(node_counts.data_ptr())
+                shard.node_offsets(node_counts.to(cdev), dist)
+            return En
         if pn:
             En = 0
             kt_sum = np.zeros(6)
@@ -324,7 +340,8 @@ def main():
                     # per-node offsets of every rank's slice (RCCL allgather of N int64)
                     eng.node_counts_to_device(node_counts.data_ptr())
                     shard.node_offsets(node_counts.to(cdev), dist)
-            last.update(nnz=nnz, kt=kt_sum, nkt=nkt_sum, windows=len(range(t0, t1, W)))
+            last.update(nnz=nnz, kt=kt_sum, nkt=nkt_sum, windows=len(range(t0, t1, W)), pn_sized=True,
+                        kt_sync=kt_sum, nkt_sync=nkt_sum)
             return En
         off_t = args.tick * last.get("step_no", 0)
         last["step_no"] = last.get("step_no", 0) + 1
@@ -356,6 +373,12 @@ def main():
     # other phases are timed afterwards, outside the timed region.
     lean = not pn and wl != "dispatch"
     pipelined = lean and not args.sync
+    # per-node windows pipelined (cg_expand_per_node_rules_device_async) after
+    # a synchronous warmup step sized the outputs; the time-order pass and the
+    # gather need every window's result, so they keep synchronous windows
+    pn_pipelined = pn and not args.sync and not args.time_order and not args.gather_node_csr
+    if pn_pipelined and args.warmup < 1:
+        args.warmup = 1
     if lean:
         eng.set_phase_timing(1)
     if pipelined:  # a synchronous call sizes the output for the pipelined ones
@@ -495,7 +518,7 @@ def main():
 
     if wl == "dispatch":
         print(json.dumps(dispatch_line(args, R, world, elapsed, wake, nkt, build_info,
-                                       cpu_dispatch(specs[:args.cpu_sample], t0)
+                                       cpu_dispatch(specs[:args.cpu_sample], t0, args.cpu_threads)
                                        if world == 1 and args.cpu_sample > 0 else None)), flush=True)
         if world > 1:
             dist.destroy_process_group()
@@ -536,6 +559,10 @@ def main():
         cpu = cpu_baseline_per_node(spec_of, rin, xmode, a_last, min(a_last + W, t1), args.zone)
     if world == 1 and args.cpu_sample != 0 and wl == "config2":
         cpu = cpu_baseline(specs, args.cpu_sample, t0, t1, args.cpu_threads, zone=args.zone)
+    if world == 1 and args.cpu_sample != 0 and wl == "config4":
+        # the 10M-rule set (rule i = base[i % 1M]); a strided sample sized for ~15 s
+        cpu = cpu_baseline([spec_of(i) for i in range(R)], args.cpu_sample, t0, t1, args.cpu_threads,
+                           zone=args.zone)
 
     out = {
         "metric": metric,
@@ -564,7 +591,11 @@ def main():
         "hbm_gbps_step": algo_bytes * world / (elapsed / args.steps) / 1e9,
         "steps_mode": ("pipelined (cg_expand_device_async: count/scan of a step overlap the previous "
                        "step's write; one cg_expand_wait at the end of the timed steps)" if pipelined else
-                       "synchronous (one call and stream sync per step)") if lean else "synchronous",
+                       "synchronous (one call and stream sync per step)") if lean else
+                      ("pipelined per-node windows (cg_expand_per_node_rules_device_async: a window's "
+                       "expansion and records overlap the previous window's writer; one wait per step; "
+                       "per-phase times from the synchronous warmup step, node_write from the timed steps)"
+                       if pn_pipelined else "synchronous"),
         "kernel_ms": {"count": kt[0], "scan": kt[1], "block_map": kt[2], "write_cf": kt[3],
                       "write_walk": kt[4], "offsets": kt[5],
                       "timing": "write_cf: HIP events around it in the timed steps; the other "
@@ -781,34 +812,56 @@ def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed, zon
             "mismatched_nodes": int(bad), "offsets_consistent": mono}
 
 
-def cpu_dispatch(specs, t0):
+def cpu_dispatch(specs, t0, threads=0):
     """The reference's wake (sort.Sort(byTime) + Next for the due prefix,
-    cron.go:220-244) as the oracle's C port, on a bounded sample: the time of
-    one steady-state wake (after the start wake has sorted the table)."""
+    cron.go:220-244) as the oracle's C port, on a bounded sample, on all of
+    this host's CPUs: the sample is split into one Cron per thread (the
+    reference runs one single-goroutine Cron per node process; here each
+    thread is such a Cron over its share of the entries, all waking on the
+    same schedule), and the time of one steady-state wake of all of them
+    (after the start wake has sorted every table) is reported."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import ctypes as C
+    from concurrent.futures import ThreadPoolExecutor
     import oracle_lib as O
-    scheds = [O.parse(s)[0] for s in specs]
-    arr = (O.OrEntry * len(scheds))()
-    for i, sc in enumerate(scheds):
-        arr[i].s = C.pointer(sc)
-        arr[i].id = i
+    avail, cpuinfo = host_cpus()
+    T = max(1, min(threads or avail, len(specs)))
+    memo = {}
+    scheds = []
+    for sp in specs:
+        if sp not in memo:
+            memo[sp] = O.parse(sp)[0]
+        scheds.append(memo[sp])
     loc = O.Loc("UTC")
     L = O.lib()
-    L.or_cron_start(arr, len(scheds), t0, loc.h)
-    ids = (C.c_int32 * len(scheds))()
-    e = L.or_cron_effective(arr, len(scheds))
-    L.or_cron_fire(arr, len(scheds), e, e, loc.h, ids)
-    ts = time.perf_counter()
-    wakes = 0
-    while time.perf_counter() - ts < 5.0 and wakes < 50:
-        e = L.or_cron_effective(arr, len(scheds))
-        L.or_cron_fire(arr, len(scheds), e, e, loc.h, ids)
-        wakes += 1
-    dt = (time.perf_counter() - ts) / wakes
-    return {"value": len(scheds) / dt, "unit": "entries/s", "cores": 1, "kind": "port",
-            "sample": f"{len(scheds)} entries of the same mix, {wakes} steady-state wakes "
-                      f"({dt * 1e3:.1f} ms per wake: qsort by Next + Next for the due prefix)"}
+    shards = []
+    for k in range(T):
+        part = scheds[k * len(scheds) // T:(k + 1) * len(scheds) // T]
+        arr = (O.OrEntry * len(part))()
+        for i, sc in enumerate(part):
+            arr[i].s = C.pointer(sc)
+            arr[i].id = i
+        shards.append((arr, len(part), (C.c_int32 * max(len(part), 1))()))
+    for arr, n, _ in shards:
+        L.or_cron_start(arr, n, t0, loc.h)
+
+    def wake(sh):  # ctypes releases the GIL for the C call
+        arr, n, ids = sh
+        e = L.or_cron_effective(arr, n)
+        L.or_cron_fire(arr, n, e, e, loc.h, ids)
+
+    with ThreadPoolExecutor(T) as ex:
+        list(ex.map(wake, shards))  # the first wake after the start
+        ts = time.perf_counter()
+        wakes = 0
+        while time.perf_counter() - ts < 5.0 and wakes < 50:
+            list(ex.map(wake, shards))
+            wakes += 1
+        dt = (time.perf_counter() - ts) / wakes
+    return {"value": len(scheds) / dt, "unit": "entries/s", "cores": T, "kind": "port",
+            "sample": f"{len(scheds)} entries of the same mix in {T} Cron tables (one per thread), {wakes} "
+                      f"steady-state wakes ({dt * 1e3:.1f} ms per wake: qsort by Next + Next for the due "
+                      f"prefix, every table)", **cpuinfo}
 
 
 def cpu_baseline_per_node(spec_of, rin, mode, a, b, zone, n_nodes=24, seed=0x5EED + 55):

@@ -422,10 +422,14 @@ static int count_phase(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
   if (rc0) return rc0;
   c->async_rc = 0;
   c->async_msg.clear();
+  if ((rc0 = pn_async_drain(c))) return rc0;  // the same for pipelined per-node windows
+  c->pa_rc = 0;
+  c->pa_msg.clear();
+  c->pa_last = -1;
+  c->pa_en_sum = 0;
   c->as_last = -1;
   c->last_R = 0;
   c->last_E = 0;
-  c->pn_recs_valid = false;  // the rule-major buffers are about to change
   HIPCHK(hipSetDevice(c->device));
   if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
     return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON (40 years)");

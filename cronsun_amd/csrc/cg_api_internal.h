@@ -114,6 +114,35 @@ struct AsyncSet {
   }
 };
 
+// One set of the pipelined per-node path (cg_expand_per_node_rules_device_async):
+// the window's rule-major expansion (its own run set and fire times), rule
+// infos and segment records, so window k+1's expansion and records are built
+// on the second stream while window k's per-node writer streams on the first.
+struct PnAsyncSet {
+  AsyncSet rm;
+  DBuf<int64_t> times, seg_cnt, seg_pos, node_off;
+  DBuf<int32_t> seg_nrec;
+  DBuf<RuleInfo> rule_info;
+  DBuf<PairRec> recs;
+  DBuf<uint32_t> tickets;
+  DBuf<char> seg_tmp;
+  int64_t* res_host = nullptr;  // {En, error}: mapped pinned, written by the records / node offsets
+  int64_t* res_dev = nullptr;
+  hipEvent_t side_done = nullptr, written = nullptr, nw0 = nullptr, nw1 = nullptr;
+  bool pending = false;
+  int64_t t0 = 0, t1 = 0, node_cap = 0, rm_cap = 0;
+  int32_t N = 0;
+  void release() {
+    rm.release();
+    times.release(); seg_cnt.release(); seg_pos.release(); node_off.release(); seg_nrec.release();
+    rule_info.release(); recs.release(); tickets.release(); seg_tmp.release();
+    if (res_host) (void)hipHostFree(res_host);
+    res_host = res_dev = nullptr;
+    for (hipEvent_t* e : {&side_done, &written, &nw0, &nw1})
+      if (*e) (void)hipEventDestroy(*e), *e = nullptr;
+  }
+};
+
 struct cg_ctx {
   int device = 0;
   int write_blocks = 1024;  // persistent k_write_cf grid (set from the CU count)
@@ -172,6 +201,16 @@ struct cg_ctx {
   double wr_ms_sum = 0;  // writer (k_write_cf) time of the checked async calls
   int wr_n = 0;
 
+  // pipelined per-node windows (cg_pernode.hip): three sets in turn
+  static constexpr int kPnSets = 3;
+  PnAsyncSet pns[kPnSets];
+  int pa_next = 0, pa_last = -1;
+  int pa_rc = 0;  // first error of the per-node calls since the last wait
+  std::string pa_msg;
+  double nw_ms_sum = 0;  // per-node writer time of the checked calls
+  int nw_n = 0;
+  int64_t pa_en_sum = 0;  // node events of the checked calls since the last wait
+
   // per-node buffers: the rule->node join (rule-major pairs), its node-major
   // transpose, the (node, rule band) segments and the node CSR
   DBuf<int64_t> rn_off, node_off, node_time, nt_off, rs_off, seg_pair, seg_cnt, seg_pos;
@@ -187,9 +226,6 @@ struct cg_ctx {
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
-  // the segment records, rule-major times and offsets still describe the last
-  // per-node result (k_node_timed reads them); any expansion clears it
-  bool pn_recs_valid = false;
   int64_t* pn_res_host = nullptr;  // mapped pinned: per-node event total of the last call
   int64_t* pn_res_dev = nullptr;
   // the rule->node join + transpose depend only on (rule set, exclude mode):
@@ -201,6 +237,7 @@ struct cg_ctx {
 
   void free_all() {
     for (AsyncSet& a : as) a.release();
+    for (PnAsyncSet& a : pns) a.release();
     for (hipEvent_t& e : cs_done)
       if (e) (void)hipEventDestroy(e), e = nullptr;
     if (st_cs) (void)hipStreamDestroy(st_cs);
@@ -259,4 +296,13 @@ int expand_device_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t
 // finish and check every pending cg_expand_device_async call (cg_async.cpp);
 // their errors are reported by the next cg_expand_wait
 int async_drain(cg_ctx* c);
-bool async_pending(const cg_ctx* c);  // an asynchronous expansion not yet waited for
+int ensure_async(cg_ctx* c);  // the second stream and the run sets' events / pinned records
+// stage a call's plan into run set a and enqueue its count + scan on the second
+// stream (cg_async.cpp); *empty when there is nothing to count
+int async_count_scan(cg_ctx* c, AsyncSet& a, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                     int64_t cap, bool* empty);
+bool async_pending(const cg_ctx* c);
+// pipelined per-node calls (cg_pernode.hip): drain (errors kept for the next
+// wait) / any pending
+int pn_async_drain(cg_ctx* c);
+bool pn_async_pending(const cg_ctx* c);  // an asynchronous expansion not yet waited for

@@ -51,6 +51,8 @@ void check_set(cg_ctx* c, AsyncSet& a) {
   }
 }
 
+}  // namespace
+
 int ensure_async(cg_ctx* c) {
   if (c->st_cs) return CG_OK;
   HIPCHK(hipStreamCreateWithFlags(&c->st_cs, hipStreamNonBlocking));
@@ -66,8 +68,6 @@ int ensure_async(cg_ctx* c) {
   }
   return CG_OK;
 }
-
-}  // namespace
 
 bool async_pending(const cg_ctx* c) {
   for (const AsyncSet& a : c->as)
@@ -85,27 +85,13 @@ int async_drain(cg_ctx* c) {
   return CG_OK;
 }
 
-extern "C" {
-
-int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1) {
-  if (!c || !s || !z) return cg_fail(CG_EINVAL, "cg_expand_device_async: null");
-  std::lock_guard<std::mutex> g(c->mu);
-  (void)hipGetLastError();
-  HIPCHK(hipSetDevice(c->device));
-  if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
-    return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON (40 years)");
-  const int64_t cap = int64_t(c->times.cap);
-  if (cap == 0)
-    return cg_fail(CG_ECAPACITY, "cg_expand_device_async: no output capacity yet (run cg_expand_device once)");
-  int rc = ensure_async(c);
-  if (rc) return rc;
-  c->pn_recs_valid = false;  // the rule-major buffers are about to change
-  const int k = c->as_next;
-  AsyncSet& a = c->as[k];
-  // the set was last used kAsyncSets calls ago: its writer must be done
-  // before the host restages its plan or the count stream rewrites its runs
-  HIPCHK(hipEventSynchronize(a.written));
-  check_set(c, a);
+// Stages call (t0, t1]'s plan into run set a (pinned memory, no stream sync)
+// and enqueues its count and scan on the ctx's second stream, building the
+// writer's slice map for an output capacity of cap events.  *empty: R or G
+// is 0 (nothing enqueued).
+int async_count_scan(cg_ctx* c, AsyncSet& a, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                     int64_t cap, bool* empty) {
+  int rc;
   const int64_t R = int64_t(s->n);
   if (!(a.plan_valid && a.plan_zone == z->serial && a.plan_t0 == t0 && a.plan_t1 == t1)) {
     a.plan_valid = false;
@@ -130,15 +116,8 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   const PlanArgs& pa = a.pa;
   const int64_t G = pa.G;
   if ((rc = a.offsets.ensure(R + 1))) return rc;
-  if (R == 0 || G == 0) {  // nothing to count: zero offsets, an empty result
-    HIPCHK(hipMemsetAsync(a.offsets.p, 0, (R + 1) * 8, c->st));
-    a.res_host[0] = 0;
-    a.res_host[1] = -1;
-    a.R = R;
-    c->as_next = (k + 1) % cg_ctx::kAsyncSets;
-    c->as_last = k;
-    c->last_R = R;
-    c->last_E = 0;
+  if (R == 0 || G == 0) {
+    *empty = true;
     return CG_OK;
   }
   const int64_t nruns = R * G;
@@ -153,6 +132,48 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   launch_count(s->d, R, pa, a.run_anchor.p, a.run_count.p, a.run_dmask.p, a.stuck.p, c->st_cs);
   launch_scan_runs(a.run_count.p, a.run_off.p, R, int32_t(G), a.scan_tmp.p, a.offsets.p, a.res_dev, a.stuck.p,
                    a.block_run.p, cap, c->st_cs);
+  a.R = R;
+  a.cap = cap;
+  *empty = false;
+  return CG_OK;
+}
+
+extern "C" {
+
+int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1) {
+  if (!c || !s || !z) return cg_fail(CG_EINVAL, "cg_expand_device_async: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
+    return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON (40 years)");
+  const int64_t cap = int64_t(c->times.cap);
+  if (cap == 0)
+    return cg_fail(CG_ECAPACITY, "cg_expand_device_async: no output capacity yet (run cg_expand_device once)");
+  int rc = ensure_async(c);
+  if (rc) return rc;
+  const int k = c->as_next;
+  AsyncSet& a = c->as[k];
+  // the set was last used kAsyncSets calls ago: its writer must be done
+  // before the host restages its plan or the count stream rewrites its runs
+  HIPCHK(hipEventSynchronize(a.written));
+  check_set(c, a);
+  const int64_t R = int64_t(s->n);
+  bool empty = false;
+  if ((rc = async_count_scan(c, a, s, z, t0, t1, cap, &empty))) return rc;
+  if (empty) {  // nothing to count: zero offsets, an empty result
+    HIPCHK(hipMemsetAsync(a.offsets.p, 0, (R + 1) * 8, c->st));
+    a.res_host[0] = 0;
+    a.res_host[1] = -1;
+    a.R = R;
+    c->as_next = (k + 1) % cg_ctx::kAsyncSets;
+    c->as_last = k;
+    c->last_R = R;
+    c->last_E = 0;
+    return CG_OK;
+  }
+  const PlanArgs& pa = a.pa;
+  const int64_t nruns = R * int64_t(pa.G);
   HIPCHK(hipEventRecord(c->cs_done[k], c->st_cs));
   // the writer after the previous call's writer, once this call's scan is done
   HIPCHK(hipStreamWaitEvent(c->st, c->cs_done[k], 0));

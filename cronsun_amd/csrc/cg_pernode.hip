@@ -277,7 +277,7 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
 constexpr int kApRules = 256;
 __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ rule_off,
                                                     const int64_t* __restrict__ times, int64_t R, int64_t t0,
-                                                    int32_t B, RuleInfo* __restrict__ info,
+                                                    int32_t B, int64_t cap, RuleInfo* __restrict__ info,
                                                     int64_t* __restrict__ err) {
   __shared__ int64_t off[kApRules + 1];
   __shared__ int64_t step[kApRules];
@@ -285,6 +285,10 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
   const int64_t r0 = int64_t(blockIdx.x) * kApRules;
   const int nr = int(R - r0 < kApRules ? R - r0 : kApRules);
   const int tid = threadIdx.x;
+  if (rule_off[R] > cap) {  // a pipelined window past the fire-time capacity: no fires read, none written
+    if (tid < nr) info[r0 + tid] = RuleInfo{0, 0, 0, 0};
+    return;
+  }
   const int64_t band_lo = rule_off[(r0 / B) * B];  // B is a multiple of kApRules
   // the writer's 32-bit band-relative indices and k_seg_records' int32
   // scans need a band to hold < 2^30 events (else the call fails)
@@ -864,6 +868,16 @@ int transpose_locked(cg_ctx* c, int64_t nnz, int32_t N) {
 #ifndef CG_BAND_BYTES
 #define CG_BAND_BYTES (1536 * 1024)
 #endif
+// largest fire-list span of a band of B rules (rule-major offsets): *out = max_k
+// off[min((k+1)B, R)] - off[kB] (atomicMax; *out zeroed by the caller)
+__global__ void k_band_max(const int64_t* __restrict__ off, int64_t R, int32_t B, unsigned long long* out) {
+  const int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  const int64_t a = k * B;
+  if (a >= R) return;
+  const int64_t b = a + B < R ? a + B : R;
+  atomicMax(out, (unsigned long long)(off[b] - off[a]));
+}
+
 int32_t band_rules(int64_t R, int64_t E) {
   const double per_rule = double(std::max<int64_t>(E, 1)) * 8.0 / double(std::max<int64_t>(R, 1));
   int64_t B = int64_t(double(CG_BAND_BYTES) / per_rule);
@@ -895,8 +909,24 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   }
   (void)hipEventRecord(c->pev[1], st);
   if (!cached && (rc = transpose_locked(c, nnz, N))) return rc;
-  // segments (node, rule band): bounds cached per band width
-  const int32_t B = band_rules(R, E);
+  // segments (node, rule band): bounds cached per band width.  The writer's
+  // band-relative indices are 32-bit: when the window holds more than 2^30
+  // fires, bands whose fire lists pass 2^30 are halved (down to kApRules
+  // rules; e.g. 1024 every-second rules over 13 days)
+  int32_t B = band_rules(R, E);
+  if (E > (int64_t(1) << 30) && R > 0) {
+    if ((rc = c->cksum.ensure(1))) return rc;
+    for (;;) {
+      HIPCHK(hipMemsetAsync(c->cksum.p, 0, 8, st));
+      hipLaunchKernelGGL(k_band_max, dim3(gridn((R + B - 1) / B, 256, 1 << 30)), dim3(256), 0, st, c->offsets.p, R,
+                         B, c->cksum.p);
+      unsigned long long mx = 0;
+      HIPCHK(hipMemcpyAsync(&mx, c->cksum.p, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if (mx <= (1ull << 30) || B <= kApRules) break;
+      B /= 2;
+    }
+  }
   const int32_t K = int32_t(std::max<int64_t>(1, (R + B - 1) / B));
   const int64_t NK = int64_t(N) * K;
   if ((rc = c->seg_pair.ensure(NK + 1)) || (rc = c->seg_cnt.ensure(std::max<int64_t>(NK, 1))) ||
@@ -922,7 +952,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_res_host[1] = 0;  // error flag (nothing of this ctx is in flight here)
   if (R > 0)
     hipLaunchKernelGGL(k_rule_info, dim3(unsigned((R + kApRules - 1) / kApRules)), dim3(256), 0, st,
-                       c->offsets.p, c->times.p, R, t0, B, c->rule_info.p, c->pn_res_dev + 1);
+                       c->offsets.p, c->times.p, R, t0, B, int64_t(c->times.cap), c->rule_info.p, c->pn_res_dev + 1);
   if (NK > 0)
     hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
                        c->nt_rule.p, c->offsets.p, c->rule_info.p, N, K, B, R, c->seg_cnt.p, c->seg_nrec.p,
@@ -975,8 +1005,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
     En = c->pn_res_host[0];
     if (c->pn_res_host[1] != 0)
-      return cg_fail(CG_ERANGE, "per-node output: a (node, rule band) segment or a band's fire "
-                                "lists exceed 2^30 events (narrow the time window)");
+      return cg_fail(CG_ERANGE, "per-node output: " + std::to_string(B) + " consecutive rules fire more than 2^30 "
+                                "times in this window (the writer's 32-bit band indices; narrow the time window)");
     if (En <= cap) break;
     // grow the output, reset the tickets the first launch consumed, rerun
     if ((rc = c->node_time.ensure(En)) || (rc = c->node_rule.ensure(En))) return rc;
@@ -987,7 +1017,6 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   (void)hipEventElapsedTime(&c->kt[7], c->pev[1], c->pev[2]);
   (void)hipEventElapsedTime(&c->kt[8], c->pev[2], c->pev[3]);
   c->pn_E = En;
-  c->pn_recs_valid = true;
   c->pn_nnz = nnz;
   c->pn_N = N;
   c->pn_t0 = t0;
@@ -1000,6 +1029,226 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
 }
 
 }  // namespace
+
+// ---- pipelined per-node windows -------------------------------------------
+// A node scheduler's tick loop (node/node.go:121-158 filtering every job,
+// node/cron/cron.go:210-275 firing them) asks for consecutive windows of every
+// node's list.  The synchronous entry point runs a window's expansion, records
+// and writer in series with two host syncs; here window k+1's rule-major
+// expansion, rule infos, segment records and node offsets run on the second
+// stream (into set (k+1) % 3) while window k's k_node_write streams on the
+// first.  The rule->node join, its transpose, the band width and the segment
+// bounds come from an earlier synchronous call on the same rule set and mode.
+
+namespace {
+
+void pn_check_set(cg_ctx* c, PnAsyncSet& a) {
+  if (!a.pending) return;
+  a.pending = false;
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, a.nw0, a.nw1) == hipSuccess) {
+    c->nw_ms_sum += ms;
+    c->nw_n++;
+  }
+  const int64_t E = a.rm.res_host[0], En = a.res_host[0];
+  c->pa_en_sum += En;
+  if (c->pa_rc) return;  // keep the first error
+  const unsigned long long stuck = static_cast<unsigned long long>(a.rm.res_host[1]);
+  if (stuck != ~0ULL) {
+    c->pa_rc = CG_ERANGE;
+    c->pa_msg = "rule " + std::to_string(stuck) +
+                ": the reference Next loop never terminates inside this horizon "
+                "(Next does not return, or returns a time <= its input and cycles)";
+  } else if (E > a.rm_cap) {
+    c->pa_rc = CG_ECAPACITY;
+    c->pa_msg = "per-node async window (" + std::to_string(a.t0) + ", " + std::to_string(a.t1) + "]: " +
+                std::to_string(E) + " rule-major events exceed the capacity " + std::to_string(a.rm_cap) +
+                " (run a synchronous per-node call on a window this large first)";
+  } else if (a.res_host[1] != 0) {
+    c->pa_rc = CG_ERANGE;
+    c->pa_msg = "per-node output: a (node, rule band) segment or a band's fire lists exceed 2^30 events";
+  } else if (En > a.node_cap) {
+    c->pa_rc = CG_ECAPACITY;
+    c->pa_msg = "per-node async window (" + std::to_string(a.t0) + ", " + std::to_string(a.t1) + "]: " +
+                std::to_string(En) + " node events exceed the output capacity " + std::to_string(a.node_cap) +
+                " (run a synchronous per-node call on a window this large first)";
+  }
+}
+
+int pn_ensure_async(cg_ctx* c) {
+  int rc = ensure_async(c);  // the second stream
+  if (rc) return rc;
+  for (PnAsyncSet& a : c->pns) {
+    if (a.written) continue;
+    HIPCHK(hipEventCreateWithFlags(&a.side_done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&a.written, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&a.nw0, hipEventDisableSystemFence));
+    HIPCHK(hipEventCreateWithFlags(&a.nw1, hipEventDisableSystemFence));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&a.res_host), 16, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.res_dev), a.res_host, 0));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&a.rm.res_host), 16, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.rm.res_dev), a.rm.res_host, 0));
+    a.res_host[0] = a.res_host[1] = 0;
+    a.rm.res_host[0] = 0;
+    a.rm.res_host[1] = -1;
+  }
+  return CG_OK;
+}
+
+}  // namespace
+
+bool pn_async_pending(const cg_ctx* c) {
+  for (const PnAsyncSet& a : c->pns)
+    if (a.pending) return true;
+  return false;
+}
+
+int pn_async_drain(cg_ctx* c) {
+  if (!pn_async_pending(c)) return CG_OK;
+  HIPCHK(hipStreamSynchronize(c->st));
+  for (PnAsyncSet& a : c->pns) pn_check_set(c, a);
+  return CG_OK;
+}
+
+extern "C" {
+
+int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, int64_t t1,
+                                          const cg_rules* rules, int mode) {
+  if (!c || !s || !z || !rules) return cg_fail(CG_EINVAL, "cg_expand_per_node_rules_device_async: null");
+  if (rules->ctx != c) return cg_fail(CG_EINVAL, "rule set uploaded on another context");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  const RulesStore& in = rules->st;
+  if (int64_t(s->n) != in.n_rules) return cg_fail(CG_EINVAL, "specs count != rules n_rules");
+  if (!(in.serial != 0 && in.serial == c->pn_cache_serial && mode == c->pn_cache_mode && c->pn_K > 0))
+    return cg_fail(CG_EINVAL, "cg_expand_per_node_rules_device_async: run cg_expand_per_node_rules_device once "
+                              "on this rule set and exclude mode first (rule->node join, bands, capacity)");
+  if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
+    return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON (40 years)");
+  const int64_t rm_cap = int64_t(c->times.cap);
+  const int64_t node_cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
+  if (rm_cap == 0 || node_cap == 0) return cg_fail(CG_ECAPACITY, "no output capacity yet (run a synchronous call)");
+  int rc = pn_ensure_async(c);
+  if (rc) return rc;
+  // the rule-major result and the time-order records no longer describe a result
+  c->as_last = -1;
+  c->last_R = 0;
+  c->last_E = 0;
+  const int k = c->pa_next;
+  PnAsyncSet& a = c->pns[k];
+  // the set was last used kPnSets calls ago: its writer must be done
+  HIPCHK(hipEventSynchronize(a.written));
+  pn_check_set(c, a);
+  const int32_t N = in.n_nodes, K = c->pn_K, B = c->pn_B;
+  const int64_t R = in.n_rules, NK = int64_t(N) * K, nnz = c->pn_nnz;
+  hipStream_t sc = c->st_cs, st = c->st;
+  bool empty = false;
+  if ((rc = async_count_scan(c, a.rm, s, z, t0, t1, rm_cap, &empty))) return rc;
+  if ((rc = a.times.ensure(std::max<int64_t>(rm_cap, 1))) || (rc = a.rule_info.ensure(std::max<int64_t>(R, 1))) ||
+      (rc = a.seg_cnt.ensure(std::max<int64_t>(NK, 1))) || (rc = a.seg_pos.ensure(NK + 1)) ||
+      (rc = a.seg_nrec.ensure(std::max<int64_t>(NK, 1))) || (rc = a.recs.ensure(std::max<int64_t>(nnz, 1))) ||
+      (rc = a.tickets.ensure(kTicketGroups * kTicketStride)) || (rc = a.node_off.ensure(int64_t(N) + 1)) ||
+      (rc = a.seg_tmp.ensure(scan_temp_bytes(std::max<int64_t>(NK, 1)))))
+    return rc;
+  a.res_host[0] = 0;
+  a.res_host[1] = 0;
+  if (empty) {  // no rules: every list empty
+    a.rm.res_host[0] = 0;
+    a.rm.res_host[1] = -1;
+    HIPCHK(hipMemsetAsync(a.seg_pos.p, 0, (NK + 1) * 8, sc));
+    HIPCHK(hipMemsetAsync(a.rule_info.p, 0, std::max<int64_t>(R, 1) * sizeof(RuleInfo), sc));
+  } else {
+    const PlanArgs& pa = a.rm.pa;
+    const int64_t nruns = R * int64_t(pa.G);
+    // a quarter of the persistent writer grid: the window's rule-major fires
+    // are few, and the previous window's per-node writer keeps the CUs
+    launch_write_cf(s->d, pa, a.rm.run_anchor.p, a.rm.run_count.p, a.rm.run_dmask.p, a.rm.run_off.p, nruns,
+                    a.rm.block_run.p, rm_cap, a.times.p, std::max(1, c->write_blocks / 4), sc);
+    if ((a.rm.plan.flags & (kPlanT0Walk | kPlanWalkSegs)) != 0)
+      launch_write_walk(s->d, R, pa, a.rm.run_anchor.p, a.rm.run_count.p, a.rm.run_dmask.p, a.rm.run_off.p, rm_cap,
+                        a.times.p, sc);
+    if (R > 0)
+      hipLaunchKernelGGL(k_rule_info, dim3(unsigned((R + kApRules - 1) / kApRules)), dim3(256), 0, sc,
+                         a.rm.offsets.p, a.times.p, R, t0, B, rm_cap, a.rule_info.p, a.res_dev + 1);
+  }
+  if (NK > 0) {
+    if (!empty)
+      hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, sc, c->seg_pair.p, c->nt_rule.p,
+                         a.rm.offsets.p, a.rule_info.p, N, K, B, R, a.seg_cnt.p, a.seg_nrec.p, a.recs.p,
+                         a.tickets.p, a.res_dev + 1);
+    else
+      HIPCHK(hipMemsetAsync(a.seg_cnt.p, 0, NK * 8, sc));
+    launch_scan64(a.seg_cnt.p, a.seg_pos.p, NK, a.seg_tmp.p, sc);
+  }
+  hipLaunchKernelGGL(k_node_off_from_seg, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, sc, a.seg_pos.p,
+                     N, K, a.node_off.p, a.res_dev);
+  HIPCHK(hipEventRecord(a.side_done, sc));
+  // the writer after the previous window's writer, once this window's records are built
+  HIPCHK(hipStreamWaitEvent(st, a.side_done, 0));
+  (void)hipEventRecord(a.nw0, st);
+  if (NK > 0 && !empty) {
+    // two block slots per CU fewer than the synchronous path's persistent
+    // grid: the next window's count, records and offsets (second stream) get
+    // wave slots beside this writer instead of waiting for it to retire
+    static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
+    const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
+    hipLaunchKernelGGL(k_node_write<0>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), 0, st,
+                       c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N, K, B,
+                       node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
+  }
+  (void)hipEventRecord(a.nw1, st);
+  HIPCHK(hipEventRecord(a.written, st));
+  HIPCHK(hipGetLastError());
+  a.pending = true;
+  a.t0 = t0;
+  a.t1 = t1;
+  a.rm_cap = rm_cap;
+  a.node_cap = node_cap;
+  a.N = N;
+  c->pa_next = (k + 1) % cg_ctx::kPnSets;
+  c->pa_last = k;
+  c->pn_E = 0;  // nothing readable until cg_expand_per_node_wait
+  return CG_OK;
+}
+
+int cg_expand_per_node_wait(cg_ctx* c, int64_t* n_events, int64_t* n_events_all) {
+  if (!c) return cg_fail(CG_EINVAL, "cg_expand_per_node_wait: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  int rc = pn_async_drain(c);
+  if (rc) return rc;
+  if (c->nw_n > 0) c->kt[8] = float(c->nw_ms_sum / c->nw_n);  // mean per-node writer time of the calls checked
+  c->nw_ms_sum = 0;
+  c->nw_n = 0;
+  const int rc_async = c->pa_rc;
+  const std::string msg = c->pa_msg;
+  c->pa_rc = 0;
+  c->pa_msg.clear();
+  int64_t En = 0;
+  if (c->pa_last >= 0) {
+    PnAsyncSet& a = c->pns[c->pa_last];
+    En = a.res_host[0];
+    if (!rc_async) {  // the last window becomes the readable per-node result
+      if ((rc = c->node_off.ensure(int64_t(a.N) + 1))) return rc;
+      HIPCHK(hipMemcpyAsync(c->node_off.p, a.node_off.p, (int64_t(a.N) + 1) * 8, hipMemcpyDeviceToDevice, c->st));
+      HIPCHK(hipStreamSynchronize(c->st));
+      c->pn_E = En;
+      c->pn_N = a.N;
+      c->pn_t0 = a.t0;
+      c->pn_t1 = a.t1;
+    }
+    c->pa_last = -1;
+  }
+  if (n_events) *n_events = rc_async ? 0 : En;
+  if (n_events_all) *n_events_all = c->pa_en_sum;
+  c->pa_en_sum = 0;
+  if (rc_async) return cg_fail(rc_async, msg);
+  return CG_OK;
+}
+
+}  // extern "C"
 
 extern "C" {
 
@@ -1108,6 +1357,9 @@ int cg_expand_per_node(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t
 int cg_node_result_device(cg_ctx* c, const int64_t** d_node_off, const int64_t** d_time,
                           const int32_t** d_rule, int64_t* n_events) {
   if (!c) return cg_fail(CG_EINVAL, "cg_node_result_device: null");
+  std::lock_guard<std::mutex> g(c->mu);
+  if (pn_async_pending(c))
+    return cg_fail(CG_EINVAL, "pipelined per-node windows pending (call cg_expand_per_node_wait first)");
   if (d_node_off) *d_node_off = c->node_off.p;
   if (d_time) *d_time = c->node_time.p;
   if (d_rule) *d_rule = c->node_rule.p;
@@ -1118,6 +1370,8 @@ int cg_node_result_device(cg_ctx* c, const int64_t** d_node_off, const int64_t**
 int cg_node_result_copy(cg_ctx* c, int64_t* node_off, int64_t* time, int32_t* rule, int64_t cap) {
   if (!c) return cg_fail(CG_EINVAL, "cg_node_result_copy: null");
   std::lock_guard<std::mutex> g(c->mu);
+  if (pn_async_pending(c))
+    return cg_fail(CG_EINVAL, "pipelined per-node windows pending (call cg_expand_per_node_wait first)");
   (void)hipGetLastError();
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
@@ -1141,6 +1395,8 @@ int cg_node_result_copy(cg_ctx* c, int64_t* node_off, int64_t* time, int32_t* ru
 int cg_node_result_copy_range(cg_ctx* c, int64_t first, int64_t count, int64_t* time, int32_t* rule) {
   if (!c || (count && !time && !rule)) return cg_fail(CG_EINVAL, "cg_node_result_copy_range: null");
   std::lock_guard<std::mutex> g(c->mu);
+  if (pn_async_pending(c))
+    return cg_fail(CG_EINVAL, "pipelined per-node windows pending (call cg_expand_per_node_wait first)");
   (void)hipGetLastError();
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;
@@ -1177,6 +1433,8 @@ int cg_node_csr_place(cg_ctx* c, int32_t n_nodes, const int64_t* d_src_node_off,
 int cg_node_counts_to_device(cg_ctx* c, int64_t* d_counts) {
   if (!c || !d_counts) return cg_fail(CG_EINVAL, "cg_node_counts_to_device: null");
   std::lock_guard<std::mutex> g(c->mu);
+  if (pn_async_pending(c))
+    return cg_fail(CG_EINVAL, "pipelined per-node windows pending (call cg_expand_per_node_wait first)");
   (void)hipGetLastError();  // clear a stale error so launch checks see only their own
   int rc = cg_hip_check(hipSetDevice(c->device), "hipSetDevice");
   if (rc) return rc;

@@ -405,6 +405,21 @@ class Engine:
                                                     C.byref(En), C.byref(nnz)))
         return En.value, nnz.value
 
+    def expand_per_node_async(self, specs, loc, t0, t1, drules, mode=_lib.EXCLUDE_NONE):
+        """Enqueue one per-node window (cg_expand_per_node_rules_device_async):
+        the next window's expansion and records overlap this one's writer.
+        Results and errors come with expand_per_node_wait()."""
+        check(lib().cg_expand_per_node_rules_device_async(self._h, specs._h, self._loc(loc).handle, int(t0),
+                                                          int(t1), drules._h, mode))
+
+    def expand_per_node_wait(self, with_total=False):
+        """Wait for the pipelined per-node windows; returns the last window's
+        node-event total (its result is then the readable per-node result),
+        and with with_total also the node events of every window waited for."""
+        n, tot = C.c_int64(), C.c_int64()
+        check(lib().cg_expand_per_node_wait(self._h, C.byref(n), C.byref(tot)))
+        return (n.value, tot.value) if with_total else n.value
+
     def node_result_device(self):
         """Device pointers of the last per-node result: (node_off, time, rule, n_events)."""
         o, t, r, n = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_int64()

@@ -427,6 +427,27 @@ void cg_rules_free(cg_rules* rules);
 int cg_expand_per_node_rules_device(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z,
                                     int64_t t0, int64_t t1, const cg_rules* rules, int mode,
                                     int64_t* n_events, int64_t* nnz);
+/* Pipelined per-node windows for a node scheduler's tick loop
+ * (node/node.go:121-158 filtering every job, node/cron/cron.go:210-275 firing
+ * them, window after window): enqueues window (t0, t1] and returns.  Window
+ * k+1's rule-major expansion, rule infos, segment records and node offsets
+ * run on the ctx's second stream while window k's per-node writer streams.
+ * Needs an earlier cg_expand_per_node_rules_device on the same rule set and
+ * exclude mode (the rule->node join, its transpose and the band width are
+ * reused) whose rule-major and per-node results were at least as large as
+ * every window's: a window that would exceed them writes nothing and
+ * cg_expand_per_node_wait returns CG_ECAPACITY.  Every window writes the same
+ * per-node output: after the wait only the LAST window's result is readable
+ * (cg_node_result_*), and a returned error may belong to any window since the
+ * previous wait.  The per-node result accessors refuse (CG_EINVAL) while
+ * windows are pending; a synchronous call drains them and discards their
+ * results and errors.  cg_last_kernel_times [8] = the mean per-node writer
+ * time of the waited windows. */
+int cg_expand_per_node_rules_device_async(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
+                                          int64_t t1, const cg_rules* rules, int mode);
+/* *n_events: the last window's node events (its result is then readable);
+ * *n_events_all (may be NULL): the node events of every window waited for. */
+int cg_expand_per_node_wait(cg_ctx* ctx, int64_t* n_events, int64_t* n_events_all);
 
 /* rule -> node CSR only (GPU join), host output */
 int cg_rule_nodes(cg_ctx* ctx, const cg_rules_in* rules, int mode, int64_t* rn_off /*[R+1]*/,

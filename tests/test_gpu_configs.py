@@ -206,9 +206,10 @@ def test_config3_sharded_ranges_place_to_unsharded(config3):
             out_t.fill_(-1)
             for g, ((lo, hi), (view, dr_g)) in enumerate(zip(ranges, parts)):
                 B.expand_per_node_rules_device(view, utc, t0, t1, dr_g, _lib.EXCLUDE_NONE)
-                o, t, r, n = B.node_result_device()
+                n_off, n_time, n_rule = B.node_result_tensors(N)  # zero-copy views of B's result
                 starts, node_base = shard.node_slice_starts(allc, g)
-                B.node_csr_place(N, o, t, r, lo, starts.contiguous().data_ptr(), out_t.data_ptr(), out_r.data_ptr())
+                # the product path of shard.gather_node_csr: torch's stream synchronised, then the kernel
+                shard.place_node_slice(n_off, n_time, n_rule, lo, starts, out_t, out_r, engine=B)
                 view.free()
                 dr_g.free()
             torch.cuda.synchronize(dev)

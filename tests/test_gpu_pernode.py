@@ -233,3 +233,114 @@ def test_per_node_progressions_vs_oracle(eng, zone, t0):
         exp_t, exp_r = O.node_list(eo, et, per_node[n])
         assert np.array_equal(time[node_off[n]:node_off[n + 1]], exp_t), n
         assert np.array_equal(rule[node_off[n]:node_off[n + 1]], exp_r), n
+
+
+@pytest.mark.parametrize("zone", ["UTC", "America/New_York"])
+def test_per_node_async_windows(zone):
+    """cg_expand_per_node_rules_device_async / cg_expand_per_node_wait: a node
+    scheduler's consecutive windows (node/node.go:121-158 + cron.go:210-275),
+    pipelined.  The last window's per-node CSR equals the synchronous result of
+    that window and the oracle; the all-window total equals the sum of the
+    windows' synchronous totals; accessors refuse while windows are pending; a
+    window beyond the capacity reports CG_ECAPACITY at the wait; a synchronous
+    call in between discards pending windows."""
+    from cronsun_amd.engine import Engine
+    from cronsun_amd._lib import check, lib
+    e2 = Engine(0)
+    rin = synth.multi_rule_jobs(2000, seed=31)
+    specs = synth.spec_mix(rin.n_rules, seed=9, mix=synth.MIX_CONFIG2)
+    arr, status = cron.parse_batch(specs)
+    assert (status == 0).all()
+    sp = e2.upload_c(arr, rin.n_rules)
+    dr = e2.upload_rules(rin)
+    z = product_zone(zone)
+    t0 = 1772953200 - 5 * 3600 if zone != "UTC" else synth.T0_2026 + 3 * 3600 + 17
+    e2.expand_per_node_rules_device(sp, z, t0, t0 + 3 * 3600, dr, _lib.EXCLUDE_NONE)  # sizes the outputs
+    wins = [(t0 + 1800 * i, t0 + 1800 * i + 3600) for i in range(8)]
+    for a, b in wins:
+        e2.expand_per_node_async(sp, z, a, b, dr, _lib.EXCLUDE_NONE)
+    with pytest.raises(_lib.CgError) as err:
+        e2.node_copy_range(0, 1)
+    assert err.value.code == _lib.CG_EINVAL
+    En, tot = e2.expand_per_node_wait(with_total=True)
+    off = np.empty(rin.n_nodes + 1, np.int64)
+    check(lib().cg_node_result_copy(e2._h, off.ctypes.data, None, None, 0))
+    got_t, got_r = e2.node_copy_range(0, En)
+    sync_tot = 0
+    for a, b in wins:
+        Ew, _ = e2.expand_per_node_rules_device(sp, z, a, b, dr, _lib.EXCLUDE_NONE)
+        sync_tot += Ew
+    assert tot == sync_tot
+    assert En == Ew
+    off_s = np.empty_like(off)
+    check(lib().cg_node_result_copy(e2._h, off_s.ctypes.data, None, None, 0))
+    st_t, st_r = e2.node_copy_range(0, Ew)
+    assert np.array_equal(off, off_s) and np.array_equal(got_t, st_t) and np.array_equal(got_r, st_r)
+    # the oracle, every node, last window
+    a, b = wins[-1]
+    eo, et = O.expand_batch(O.sched_array(oracle_parse_all(specs)), a, b, oracle_zone(zone))
+    rn = oracle_rule_nodes(rin, _lib.EXCLUDE_NONE)
+    per_node = [[] for _ in range(rin.n_nodes)]
+    for r in range(rin.n_rules):
+        for n in rn[r]:
+            per_node[n].append(r)
+    for n in range(rin.n_nodes):
+        if not per_node[n]:
+            assert off[n + 1] == off[n]
+            continue
+        exp_t, exp_r = O.node_list(eo, et, per_node[n])
+        assert np.array_equal(got_t[off[n]:off[n + 1]], exp_t), n
+        assert np.array_equal(got_r[off[n]:off[n + 1]], exp_r), n
+    # a window far beyond the capacity: CG_ECAPACITY at the wait
+    e2.expand_per_node_async(sp, z, t0, t0 + 2 * DAY, dr, _lib.EXCLUDE_NONE)
+    with pytest.raises(_lib.CgError) as err:
+        e2.expand_per_node_wait()
+    assert err.value.code == _lib.CG_ECAPACITY
+    # a synchronous call discards pending windows (and their errors)
+    e2.expand_per_node_async(sp, z, t0, t0 + 2 * DAY, dr, _lib.EXCLUDE_NONE)
+    Es, _ = e2.expand_per_node_rules_device(sp, z, a, b, dr, _lib.EXCLUDE_NONE)
+    e2.expand_per_node_async(sp, z, a, b, dr, _lib.EXCLUDE_NONE)
+    assert e2.expand_per_node_wait() == Es
+    dr.free()
+    sp.free()
+    e2.close()
+
+
+def test_per_node_bands_past_2_30_fires():
+    """A window whose 1024-rule bands hold more than 2^30 fires (1024
+    every-second rules over 13 days: 1.15 G fires): the per-node path narrows
+    its bands instead of refusing, and sampled nodes' lists are bit-exact
+    against the oracle (job.go:591-614 composed with spec.go:55-145 over the
+    whole window)."""
+    from cronsun_amd.engine import Engine
+    e2 = Engine(0)
+    R, N = 1100, 48
+    specs = ["* * * * * *"] * 1024 + [PROGRESSION_MIX[1 + i % (len(PROGRESSION_MIX) - 1)] for i in range(R - 1024)]
+    rin = progression_rules(R, N)
+    arr, status = cron.parse_batch(specs)
+    assert (status == 0).all()
+    sp = e2.upload_c(arr, R)
+    dr = e2.upload_rules(rin)
+    t0 = synth.T0_2026 + 1234
+    t1 = t0 + 13 * DAY
+    En, nnz = e2.expand_per_node_rules_device(sp, cron.UTC(), t0, t1, dr, _lib.EXCLUDE_NONE)
+    assert En > 2 * (1 << 30)
+    from cronsun_amd._lib import check, lib
+    off = np.empty(N + 1, np.int64)
+    check(lib().cg_node_result_copy(e2._h, off.ctypes.data, None, None, 0))
+    rn = oracle_rule_nodes(rin, _lib.EXCLUDE_NONE)
+    per_node = [[] for _ in range(N)]
+    for r in range(R):
+        for n in rn[r]:
+            per_node[n].append(r)
+    for n in (5, 31):
+        rules = per_node[n]
+        arr_o = O.sched_array(oracle_parse_all([specs[r] for r in rules]))
+        eo, et = O.expand_batch(arr_o, t0, t1, oracle_zone("UTC"), threads=16)
+        exp_t, exp_r = O.node_list(eo, et, list(range(len(rules))))
+        got_t, got_r = e2.node_copy_range(off[n], off[n + 1] - off[n])
+        assert np.array_equal(got_t, exp_t), n
+        assert np.array_equal(got_r, np.array(rules, np.int32)[exp_r]), n
+    dr.free()
+    sp.free()
+    e2.close()
