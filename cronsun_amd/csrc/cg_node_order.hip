@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "../../include/cronsun_gpu.h"
 #include "cg_api_internal.h"
@@ -167,6 +168,465 @@ __global__ __launch_bounds__(256) void k_ts_scatter(const int64_t* __restrict__ 
   }
 }
 
+// ---- windows <= 4096 s (12-bit time offsets): tile sort + per-node merge ----
+//
+//   k_ot_tile   per tile (<= kTsTile events of one node, rule-major): a
+//               stable LDS counting sort by the time offset (two 6-bit
+//               passes over packed (offset << 12 | index) words), the tile
+//               written back in (time, rule) order with coalesced stores, and
+//               the tile's slab prefix pre[t][0..64] (slab = offset >> 6)
+//   k_ot_merge  one workgroup per node: the node's slabs in order; the
+//               portions (tile t, slab j) of a run of small slabs are
+//               gathered into LDS in (slab, tile) order, sorted stably by
+//               the offset and stored contiguously; a slab of more than one
+//               chunk (or of a node with more than kOtGroup tiles) is
+//               histogrammed by its low 6 bits first and then stored chunk
+//               by chunk at its digits' running bases
+// Each event is read and written twice (24 B + 24 B), all stores coalesced;
+// the LSD passes above scatter every event to its own address twice and
+// read the times a third and fourth time for the histograms.
+constexpr int kOtItems = kTsItems;          // per thread
+constexpr int kOtChunk = kTsTile;           // events per LDS chunk (index fits 12 bits)
+constexpr int kOtGroup = 256;               // portions per LDS portion list
+
+struct OtRank {
+  int32_t run[4][64];   // per wave: events of each digit so far
+  int32_t base[4][64];  // per wave: first position of its events of each digit
+  int32_t dbase[65];    // exclusive prefix of the digit totals; [64] = events
+};
+
+// Stable positions of the n valid items (item j of wave w, lane l = element
+// w*1024 + j*64 + l) by the 6-bit digit dg[j]: earlier elements with the same
+// digit keep their order.  Ends with the block synchronised, positions in pos.
+__device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, int32_t (&pos)[kOtItems],
+                                        OtRank& s) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  s.run[w][lane] = 0;
+  const int ebase = w * (64 * kOtItems);
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) {
+    const bool valid = ebase + j * 64 + lane < n;
+    const uint32_t d = dg[j];
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    // every lane reads the running count before the group's first lane adds
+    // the group size (a wave's LDS operations complete in program order)
+    const int32_t r0 = s.run[w][d];
+    pos[j] = r0 + __popcll(peers & lt);
+    if (valid && (peers & lt) == 0) s.run[w][d] = r0 + __popcll(peers);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int d = threadIdx.x;
+    const int32_t tot = s.run[0][d] + s.run[1][d] + s.run[2][d] + s.run[3][d];
+    int32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(inc, o, 64);
+      if (d >= o) inc += y;
+    }
+    int32_t acc = inc - tot;
+    s.dbase[d] = acc;
+    if (d == 63) s.dbase[64] = inc;
+#pragma unroll
+    for (int ww = 0; ww < 4; ww++) {
+      s.base[ww][d] = acc;
+      acc += s.run[ww][d];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) pos[j] += s.base[w][dg[j]];
+}
+
+// Stable sort of n packed words (offset << 12 | index) held as items, by
+// the offset's low 6 bits and, if both, then by its high 6 bits; the sorted
+// words end in pk[0..n).  Ends synchronised.
+__device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, bool both, uint32_t* pk, OtRank& s) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ebase = w * (64 * kOtItems);
+  uint32_t dg[kOtItems];
+  int32_t pos[kOtItems];
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) dg[j] = (key[j] >> 12) & 63u;
+  ot_rank(dg, n, pos, s);
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++)
+    if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
+  __syncthreads();
+  if (!both) return;
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) {
+    const int e = ebase + j * 64 + lane;
+    key[j] = e < n ? pk[e] : 0u;
+    dg[j] = (key[j] >> 18) & 63u;
+  }
+  ot_rank(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++)
+    if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_ot_tile(int64_t* __restrict__ time, int32_t* __restrict__ rule,
+                                                  const int32_t* __restrict__ tile_node,
+                                                  const int64_t* __restrict__ tile_base,
+                                                  const int64_t* __restrict__ node_off, int64_t t0,
+                                                  int32_t* __restrict__ pre) {
+  __shared__ OtRank s;
+  __shared__ uint32_t pk[kOtChunk];
+  __shared__ int32_t rl[kOtChunk];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t t = blockIdx.x;
+  const TileRange r = tile_range(t, tile_node, tile_base, node_off);
+  const int n = int(r.hi - r.lo);
+  const int ebase = w * (64 * kOtItems);
+  uint32_t key[kOtItems];
+  const uint32_t* __restrict__ tlo = reinterpret_cast<const uint32_t*>(time);  // low words: offsets < 4096
+  const uint32_t b = uint32_t(t0 + 1);
+  uint32_t tv[kOtItems];
+  int32_t rv[kOtItems];
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) {  // every load issued before any is used
+    const int e = ebase + j * 64 + lane;
+    const int64_t i = r.lo + (e < n ? e : n - 1);
+    tv[j] = tlo[2 * i];
+    rv[j] = rule[i];
+  }
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) {
+    const int e = ebase + j * 64 + lane;
+    key[j] = e < n ? ((tv[j] - b) << 12) | uint32_t(e) : 0u;
+    if (e < n) rl[e] = rv[j];
+  }
+  ot_sort(key, n, true, pk, s);
+  if (threadIdx.x <= 64) pre[t * 65 + threadIdx.x] = s.dbase[threadIdx.x];  // slab prefix of the last pass
+  for (int p = threadIdx.x; p < n; p += 256) {
+    const uint32_t v = pk[p];
+    __builtin_nontemporal_store(t0 + 1 + int64_t(v >> 12), time + r.lo + p);
+    __builtin_nontemporal_store(rl[v & 4095u], rule + r.lo + p);
+  }
+}
+
+// Block-wide exclusive scan of cnt(q) for q in [0, Q) (Q <= kOtGroup) into
+// ps[0..Q] (ps[Q] = total); src(q) into psrc.  Ends synchronised.
+template <class Portion>
+__device__ __forceinline__ void ot_portions(int Q, Portion&& portion, int32_t* ps, int64_t* psrc, int32_t* wsum) {
+  constexpr int PER = kOtGroup / 256;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int32_t c[PER], sum = 0;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int q = threadIdx.x * PER + i;
+    c[i] = 0;
+    if (q < Q) {
+      int64_t src;
+      c[i] = portion(q, &src);
+      psrc[q] = src;
+    }
+    sum += c[i];
+  }
+  int32_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int32_t run = inc - sum;
+  for (int ww = 0; ww < w; ww++) run += wsum[ww];
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int q = threadIdx.x * PER + i;
+    if (q < Q) ps[q] = run;
+    run += c[i];
+  }
+  if (threadIdx.x == 255) ps[Q] = run;
+  __syncthreads();
+}
+
+// the portion holding element e of the list (ps ascending, ps[0] = 0)
+__device__ __forceinline__ int ot_find(const int32_t* ps, int Q, int32_t e) {
+  int lo = 0, hi = Q - 1;  // the last q with ps[q] <= e
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (ps[mid] <= e) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// own[i] = the portion holding element c0 + i of the list, i < n_el <=
+// kOtChunk: every non-empty portion marks its first element and an inclusive
+// max-scan fills the rest (portion indices grow with position), so no
+// element searches.  Ends synchronised.
+__device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, int n_el, int32_t* own,
+                                          int32_t* wsum) {
+  constexpr int PER = kOtChunk / 256;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < n_el; i += 256) own[i] = -1;
+  __syncthreads();
+  for (int q = threadIdx.x; q < Q; q += 256) {
+    const int32_t a = ps[q];
+    if (a < ps[q + 1] && a >= c0 && a < c0 + n_el) own[a - c0] = q;
+  }
+  if (threadIdx.x == 0) own[0] = ot_find(ps, Q, c0);  // the portion the chunk starts in (the same q if it starts at c0)
+  __syncthreads();
+  int32_t v[PER], m = -1;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int idx = threadIdx.x * PER + i;
+    v[i] = idx < n_el ? own[idx] : -1;
+    m = v[i] > m ? v[i] : m;
+    v[i] = m;
+  }
+  int32_t inc = m;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc = y > inc ? y : inc;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  int32_t prev = __shfl_up(inc, 1, 64);
+  if (lane == 0) prev = -1;
+  for (int ww = 0; ww < w; ww++) prev = wsum[ww] > prev ? wsum[ww] : prev;
+#pragma unroll
+  for (int i = 0; i < PER; i++) {
+    const int idx = threadIdx.x * PER + i;
+    if (idx < n_el) own[idx] = v[i] > prev ? v[i] : prev;
+  }
+  __syncthreads();
+}
+
+// Items of elements c0 .. c0 + n_el of the portion list: key = (offset << 12
+// | chunk index), rule into rl[chunk index] (RULES).  All loads issued before
+// any is used (clamped indices).
+template <bool RULES>
+__device__ __forceinline__ void ot_gather(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
+                                          int64_t t0, const int32_t* ps, const int64_t* psrc, const int32_t* own,
+                                          int32_t c0, int n_el, uint32_t (&key)[kOtItems], int32_t* rl) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ebase = w * (64 * kOtItems);
+  // the low words of the times suffice: offsets are < 4096
+  const uint32_t* __restrict__ tlo = reinterpret_cast<const uint32_t*>(tin);
+  const uint32_t b = uint32_t(t0 + 1);
+  uint32_t tv[kOtItems];
+  int32_t rv[kOtItems];
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) {
+    const int e = ebase + j * 64 + lane;
+    const int ec = e < n_el ? e : n_el - 1;
+    const int q = own[ec];
+    const int64_t src = psrc[q] + (c0 + ec - ps[q]);
+    tv[j] = tlo[2 * src];
+    if (RULES) rv[j] = rin[src];
+  }
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++) {
+    const int e = ebase + j * 64 + lane;
+    key[j] = e < n_el ? ((tv[j] - b) << 12) | uint32_t(e) : 0u;
+    if (RULES && e < n_el) rl[e] = rv[j];
+  }
+}
+
+__global__ __launch_bounds__(256, 4) void k_ot_merge(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
+                                                   const int64_t* __restrict__ tile_base,
+                                                   const int64_t* __restrict__ node_off,
+                                                   const int32_t* __restrict__ pre, int32_t N, int64_t t0,
+                                                   int64_t* __restrict__ tout, int32_t* __restrict__ rout,
+                                                   int64_t* __restrict__ big, unsigned* __restrict__ big_n) {
+  __shared__ OtRank s;
+  __shared__ uint32_t pk[kOtChunk];  // the owner list while gathering, then the sorted words
+  __shared__ int32_t rl[kOtChunk];
+  __shared__ int32_t ps[kOtGroup + 1];
+  __shared__ int64_t psrc[kOtGroup];
+  __shared__ int64_t slab_off[65];  // node-relative first position of each slab; [64] = the node's events
+  __shared__ int32_t wsum[4];
+  int32_t* own = reinterpret_cast<int32_t*>(pk);
+  const int32_t n = blockIdx.x;
+  if (n >= N) return;
+  const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta, lo_n = node_off[n];
+  if (M == 0) return;
+  if (M == 1) {  // one tile: already in order
+    const int64_t e = node_off[n + 1] - lo_n;
+    for (int64_t p = threadIdx.x; p < e; p += 256) {
+      __builtin_nontemporal_store(tin[lo_n + p], tout + lo_n + p);
+      __builtin_nontemporal_store(rin[lo_n + p], rout + lo_n + p);
+    }
+    return;
+  }
+  if (threadIdx.x < 64) {  // slab totals over the node's tiles, exclusive prefix
+    const int d = threadIdx.x;
+    int64_t tot = 0;
+    for (int64_t t = ta; t < ta + M; t++) tot += pre[t * 65 + d + 1] - pre[t * 65 + d];
+    int64_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int64_t y = __shfl_up(inc, o, 64);
+      if (d >= o) inc += y;
+    }
+    slab_off[d] = inc - tot;
+    if (d == 63) slab_off[64] = inc;
+  }
+  __syncthreads();
+  // the portion list of slabs [ja, jb): per tile its sorted events of those
+  // slabs, one contiguous range (tile order; the sort by offset then keeps
+  // tile order, i.e. rule order, for equal offsets)
+  auto list = [&](int ja, int jb) {
+    const int Q = int(M);
+    ot_portions(
+        Q,
+        [&](int q, int64_t* src) {
+          const int64_t t = ta + q;
+          const int32_t a = pre[t * 65 + ja];
+          *src = lo_n + int64_t(q) * kTsTile + a;
+          return pre[t * 65 + jb] - a;
+        },
+        ps, psrc, wsum);
+    return Q;
+  };
+  uint32_t key[kOtItems];
+  int ja = 0;
+  while (ja < 64) {
+    // a run of whole slabs [ja, jb) that fits one chunk (nodes of at most
+    // kOtGroup tiles)
+    int jb = ja;
+    while (M <= kOtGroup && jb < 64 && slab_off[jb + 1] - slab_off[ja] <= kOtChunk) jb++;
+    if (jb > ja) {
+      const int n_el = int(slab_off[jb] - slab_off[ja]);
+      if (n_el > 0) {
+        const int Q = list(ja, jb);
+        ot_owners(ps, Q, 0, n_el, own, wsum);
+        ot_gather<true>(tin, rin, t0, ps, psrc, own, 0, n_el, key, rl);
+        ot_sort(key, n_el, jb - ja > 1, pk, s);
+        const int64_t o = lo_n + slab_off[ja];
+        for (int p = threadIdx.x; p < n_el; p += 256) {
+          const uint32_t v = pk[p];
+          __builtin_nontemporal_store(t0 + 1 + int64_t(v >> 12), tout + o + p);
+          __builtin_nontemporal_store(rl[v & 4095u], rout + o + p);
+        }
+        __syncthreads();
+      }
+      ja = jb;
+      continue;
+    }
+    // slab ja alone (more than a chunk, or more tiles than a portion list):
+    // k_ot_big
+    if (threadIdx.x == 0) {
+      const unsigned k = atomicAdd(big_n, 1u);
+      big[k] = (int64_t(n) << 8) | ja;
+    }
+    ja++;
+  }
+}
+
+// The slabs k_ot_merge leaves (more events than a chunk, or a node of more
+// than kOtGroup tiles), one per workgroup turn: the slab's low-6-bit
+// histogram over all its portions first, then its chunks in order, each
+// sorted in LDS and stored at its digits' running bases.
+__global__ __launch_bounds__(256, 4) void k_ot_big(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
+                                                    const int64_t* __restrict__ tile_base,
+                                                    const int64_t* __restrict__ node_off,
+                                                    const int32_t* __restrict__ pre, int64_t t0,
+                                                    int64_t* __restrict__ tout, int32_t* __restrict__ rout,
+                                                    const int64_t* __restrict__ big, const unsigned* __restrict__ big_n) {
+  __shared__ OtRank s;
+  __shared__ uint32_t pk[kOtChunk];
+  __shared__ int32_t rl[kOtChunk];
+  __shared__ int32_t ps[kOtGroup + 1];
+  __shared__ int64_t psrc[kOtGroup];
+  __shared__ int64_t gbase[64];
+  __shared__ int32_t hist[64];
+  __shared__ int32_t wsum[4];
+  __shared__ int64_t red[4];
+  int32_t* own = reinterpret_cast<int32_t*>(pk);
+  const unsigned nb = *big_n;
+  for (unsigned task = blockIdx.x; task < nb; task += gridDim.x) {
+    const int32_t n = int32_t(big[task] >> 8);
+    const int j = int(big[task] & 255);
+    const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta, lo_n = node_off[n];
+    auto list = [&](int j0, int nj, int64_t g0, int64_t gm) {
+      const int Q = int(nj * gm);
+      ot_portions(
+          Q,
+          [&](int q, int64_t* src) {
+            const int jq = j0 + int(q / gm);
+            const int64_t t = ta + g0 + q % gm;
+            *src = lo_n + (t - ta) * int64_t(kTsTile) + pre[t * 65 + jq];
+            return pre[t * 65 + jq + 1] - pre[t * 65 + jq];
+          },
+          ps, psrc, wsum);
+      return Q;
+    };
+    // the slab's first position: events of earlier slabs over the node's tiles
+    int64_t before = 0;
+    for (int64_t t = ta + threadIdx.x; t < ta + M; t += 256) before += pre[t * 65 + j];
+#pragma unroll
+    for (int o = 32; o; o >>= 1) before += __shfl_xor(before, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = before;
+    __syncthreads();
+    const int64_t slab_lo = lo_n + red[0] + red[1] + red[2] + red[3];
+    uint32_t key[kOtItems];
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int64_t ga = 0; ga < M; ga += kOtGroup) {  // histogram of the low 6 bits
+      const int Q = list(j, 1, ga, M - ga < kOtGroup ? M - ga : kOtGroup);
+      const int32_t n_grp = ps[Q];
+      for (int32_t c0 = 0; c0 < n_grp; c0 += kOtChunk) {
+        const int n_el = n_grp - c0 < kOtChunk ? int(n_grp - c0) : kOtChunk;
+        ot_owners(ps, Q, c0, n_el, own, wsum);
+        ot_gather<false>(tin, rin, t0, ps, psrc, own, c0, n_el, key, rl);
+        const int ebase = (threadIdx.x >> 6) * (64 * kOtItems);
+#pragma unroll
+        for (int jj = 0; jj < kOtItems; jj++)
+          if (ebase + jj * 64 + (threadIdx.x & 63) < n_el) atomicAdd(&hist[(key[jj] >> 12) & 63u], 1);
+        __syncthreads();
+      }
+    }
+    if (threadIdx.x < 64) {
+      const int d = threadIdx.x;
+      const int64_t c = hist[d];
+      int64_t inc = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(inc, o, 64);
+        if (d >= o) inc += y;
+      }
+      gbase[d] = slab_lo + inc - c;
+    }
+    __syncthreads();
+    for (int64_t ga = 0; ga < M; ga += kOtGroup) {  // chunks in order, each digit at its running base
+      const int Q = list(j, 1, ga, M - ga < kOtGroup ? M - ga : kOtGroup);
+      const int32_t n_grp = ps[Q];
+      for (int32_t c0 = 0; c0 < n_grp; c0 += kOtChunk) {
+        const int n_el = n_grp - c0 < kOtChunk ? int(n_grp - c0) : kOtChunk;
+        ot_owners(ps, Q, c0, n_el, own, wsum);
+        ot_gather<true>(tin, rin, t0, ps, psrc, own, c0, n_el, key, rl);
+        ot_sort(key, n_el, false, pk, s);
+        for (int p = threadIdx.x; p < n_el; p += 256) {
+          const uint32_t v = pk[p];
+          const uint32_t d = (v >> 12) & 63u;
+          const int64_t dst = gbase[d] + (p - s.dbase[d]);
+          tout[dst] = t0 + 1 + int64_t(v >> 12);
+          rout[dst] = rl[v & 4095u];
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) gbase[threadIdx.x] += s.dbase[threadIdx.x + 1] - s.dbase[threadIdx.x];
+        __syncthreads();
+      }
+    }
+    __syncthreads();  // red, gbase and the lists are rewritten by the next task
+  }
+}
+
 int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads - 1) / threads)); }
 
 }  // namespace
@@ -196,11 +656,34 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   if ((rc = cg_hip_check(hipMemcpyAsync(&T, c->ts_base.p + N, 8, hipMemcpyDeviceToHost, st), "tiles")) ||
       (rc = cg_hip_check(hipStreamSynchronize(st), "sync")))
     return rc;
-  if ((rc = c->ts_tile_node.ensure(T)) || (rc = c->ts_hist.ensure(T * kTsDigits)) ||
-      (rc = c->ts_off.ensure(T * kTsDigits)) || (rc = c->node_time2.ensure(En)) || (rc = c->node_rule2.ensure(En)))
+  const bool merge = bits <= 12 && !getenv("CG_ORDER_LSD");
+  if ((rc = c->ts_tile_node.ensure(T)) || (rc = c->ts_hist.ensure(T * (merge ? 65 : kTsDigits))) ||
+      (!merge && (rc = c->ts_off.ensure(T * kTsDigits))) || (rc = c->node_time2.ensure(En)) ||
+      (rc = c->node_rule2.ensure(En)))
     return rc;
   (void)hipEventRecord(c->pev[0], st);
   hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
+  if (merge) {
+    hipLaunchKernelGGL(k_ot_tile, dim3(unsigned(T)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
+                       c->ts_tile_node.p, c->ts_base.p, c->node_off.p, c->pn_t0, c->ts_hist.p);
+    // big-slab tasks: at most 64 per node, after one counter word
+    if ((rc = c->ts_off.ensure(int64_t(N) * 64 + 1))) return rc;
+    unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * 64);
+    if ((rc = cg_hip_check(hipMemsetAsync(big_n, 0, 8, st), "memset"))) return rc;
+    hipLaunchKernelGGL(k_ot_merge, dim3(unsigned(N)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
+                       c->ts_base.p, c->node_off.p, c->ts_hist.p, N, c->pn_t0, c->node_time2.p, c->node_rule2.p,
+                       c->ts_off.p, big_n);
+    hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, c->node_time.p,
+                       c->node_rule.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, c->pn_t0, c->node_time2.p,
+                       c->node_rule2.p, c->ts_off.p, big_n);
+    (void)hipEventRecord(c->pev[1], st);
+    if ((rc = cg_hip_check(hipGetLastError(), "time-order kernels"))) return rc;
+    std::swap(c->node_time, c->node_time2);
+    std::swap(c->node_rule, c->node_rule2);
+    if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+    (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);
+    return CG_OK;
+  }
   int64_t* tin = c->node_time.p;
   int32_t* rin = c->node_rule.p;
   int64_t* tout = c->node_time2.p;

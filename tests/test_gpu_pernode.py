@@ -204,6 +204,42 @@ def progression_rules(R, n_nodes):
                    job_pause=np.zeros(R, np.uint8))
 
 
+@pytest.mark.parametrize("R,N,secs,star_every", [(1200, 3, 3600, 13), (2600, 2, 4096, 2), (64, 1, 61, 3)])
+def test_per_node_time_ordered_big_nodes(eng, R, N, secs, star_every):
+    """The one-pass time order on nodes far larger than one LDS chunk:
+    every-second rules put > 4096 events into one 64-s slab (the slab is
+    histogrammed, then stored chunk by chunk at its digits' running bases),
+    and at 2600 rules on 2 nodes over 4096 s each node holds > 5 M events,
+    more than 1024 tiles (portion lists in groups); 61 s: one tile per node.
+    Against the oracle's lists sorted by (time, rule)."""
+    specs = [PROGRESSION_MIX[0] if i % star_every == 0 else PROGRESSION_MIX[1 + i % (len(PROGRESSION_MIX) - 1)]
+             for i in range(R)]
+    rin = progression_rules(R, N)
+    scheds = [cron.Parse(s) for s in specs]
+    t0 = synth.T0_2026 + 9 * DAY + 777
+    t1 = t0 + secs
+    node_off, time, rule = eng.expand_per_node(scheds, product_zone("UTC"), t0, t1, rin, _lib.EXCLUDE_NONE)
+    eng.node_order_by_time()
+    off2, time2, rule2 = eng.node_result(rin.n_nodes, len(time))
+    assert np.array_equal(off2, node_off)
+    arr = O.sched_array(oracle_parse_all(specs))
+    eo, et = O.expand_batch(arr, t0, t1, oracle_zone("UTC"))
+    rn = oracle_rule_nodes(rin, _lib.EXCLUDE_NONE)
+    per_node = [[] for _ in range(N)]
+    for r in range(R):
+        for n in rn[r]:
+            per_node[n].append(r)
+    for n in range(N):
+        exp_t, exp_r = O.node_list(eo, et, per_node[n])
+        order = np.lexsort((exp_r, exp_t))
+        a, b = node_off[n], node_off[n + 1]
+        assert b - a == len(exp_t), n
+        assert np.array_equal(time2[a:b], exp_t[order]), n
+        assert np.array_equal(rule2[a:b], exp_r[order]), n
+    if secs == 4096:
+        assert (np.diff(node_off) > 1024 * 4096).all()
+
+
 @pytest.mark.parametrize("zone,t0", [("UTC", synth.T0_2026 + 64 * DAY + 1234),
                                      ("America/New_York", 1772953200 - 36 * 3600)])
 def test_per_node_progressions_vs_oracle(eng, zone, t0):
