@@ -37,10 +37,10 @@ constexpr int kTsTile = 256 * kTsItems;  // events per tile (4 waves x 16 items 
 constexpr int kTsBits = 6;
 constexpr int kTsDigits = 1 << kTsBits;
 
-__global__ void k_ts_tile_count(const int64_t* __restrict__ node_off, int32_t N, int32_t* __restrict__ cnt) {
+__global__ void k_ts_tile_count(const int64_t* __restrict__ node_off, int32_t N, int tile, int32_t* __restrict__ cnt) {
   const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
   if (n >= N) return;
-  cnt[n] = int32_t((node_off[n + 1] - node_off[n] + kTsTile - 1) / kTsTile);
+  cnt[n] = int32_t((node_off[n + 1] - node_off[n] + tile - 1) / tile);
 }
 
 __global__ void k_ts_tiles(const int64_t* __restrict__ tile_base, int32_t N, int32_t* __restrict__ tile_node) {
@@ -53,11 +53,11 @@ struct TileRange {
   int64_t lo, hi;
 };
 __device__ __forceinline__ TileRange tile_range(int64_t t, const int32_t* tile_node, const int64_t* tile_base,
-                                                const int64_t* node_off) {
+                                                const int64_t* node_off, int tile = kTsTile) {
   const int32_t n = tile_node[t];
   TileRange r;
-  r.lo = node_off[n] + (t - tile_base[n]) * kTsTile;
-  r.hi = min(r.lo + int64_t(kTsTile), node_off[n + 1]);
+  r.lo = node_off[n] + (t - tile_base[n]) * tile;
+  r.hi = min(r.lo + int64_t(tile), node_off[n + 1]);
   return r;
 }
 
@@ -170,36 +170,64 @@ __global__ __launch_bounds__(256) void k_ts_scatter(const int64_t* __restrict__ 
 
 // ---- windows <= 4096 s (12-bit time offsets): tile sort + per-node merge ----
 //
-//   k_ot_tile   per tile (<= kTsTile events of one node, rule-major): a
+//   k_ot_tile   per tile (<= kOtTile events of one node, rule-major): a
 //               stable LDS counting sort by the time offset (two 6-bit
 //               passes over packed (offset << 12 | index) words), the tile
 //               written back in (time, rule) order with coalesced stores, and
-//               the tile's slab prefix pre[t][0..64] (slab = offset >> 6)
-//   k_ot_merge  one workgroup per node: the node's slabs in order; the
-//               portions (tile t, slab j) of a run of small slabs are
-//               gathered into LDS in (slab, tile) order, sorted stably by
-//               the offset and stored contiguously; a slab of more than one
-//               chunk (or of a node with more than kOtGroup tiles) is
-//               histogrammed by its low 6 bits first and then stored chunk
-//               by chunk at its digits' running bases
-// Each event is read and written twice (24 B + 24 B), all stores coalesced;
-// the LSD passes above scatter every event to its own address twice and
-// read the times a third and fourth time for the histograms.
-constexpr int kOtItems = kTsItems;          // per thread
-constexpr int kOtChunk = kTsTile;           // events per LDS chunk (index fits 12 bits)
-constexpr int kOtGroup = 256;               // portions per LDS portion list
+//               its slab prefix pre[t][0..256] (slab = offset >> 4: 16 s)
+//   k_ot_merge  one wave per node (many independent nodes in flight): runs
+//               of whole slabs holding <= kOtChunk1 events are gathered from
+//               every tile (one contiguous range per tile: its sorted events
+//               of those slabs; tile order = rule order), sorted by offset in
+//               LDS (one pass over the low 4 bits for a single slab) and
+//               stored contiguously; a larger slab, or every slab of a node
+//               of more than kOtMaxTiles tiles, is queued for k_ot_big
+//   k_ot_big    per queued slab: the histogram of its 16 seconds over all its
+//               portions, then its chunks in order, each sorted in LDS and
+//               stored at its seconds' running bases
+// Each event is read and written twice (24 B + 24 B) and every store is
+// coalesced, where the LSD passes above scatter each event to its own
+// address per pass and read the times again for every histogram.
+constexpr int kOtItems = 16;                  // per thread
+constexpr int kOtTile = 4 * 64 * kOtItems;    // 4096 events: the tile sort's 4-wave chunk
+#ifndef CG_OT_MERGE_WAVES
+#define CG_OT_MERGE_WAVES 4
+#endif
+constexpr int kOtMergeWaves = CG_OT_MERGE_WAVES;  // k_ot_merge: waves per node
+constexpr int kOtIdxBits = 12;                // chunk index bits of a packed word
+constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
+#ifndef CG_OT_SLAB_BITS
+#define CG_OT_SLAB_BITS 6
+#endif
+constexpr int kOtSlabBits = CG_OT_SLAB_BITS;  // slab = offset >> kOtSlabBits (64 s)
+constexpr int kOtSlabs = 4096 >> kOtSlabBits;
+constexpr int kOtPre = kOtSlabs + 1;          // pre row per tile
+constexpr int kOtMaxTiles = 256;              // portion list capacity
 
+template <int NW>
+__device__ __forceinline__ void ot_sync() {
+  if constexpr (NW > 1) {
+    __syncthreads();
+  } else {  // one wave: its LDS operations complete in order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+template <int NW>
 struct OtRank {
-  int32_t run[4][64];   // per wave: events of each digit so far
-  int32_t base[4][64];  // per wave: first position of its events of each digit
-  int32_t dbase[65];    // exclusive prefix of the digit totals; [64] = events
+  int32_t run[NW][64];   // per wave: events of each digit so far
+  int32_t base[NW][64];  // per wave: first position of its events of each digit
+  int32_t dbase[65];     // exclusive prefix of the digit totals; [64] = events
 };
 
 // Stable positions of the n valid items (item j of wave w, lane l = element
-// w*1024 + j*64 + l) by the 6-bit digit dg[j]: earlier elements with the same
-// digit keep their order.  Ends with the block synchronised, positions in pos.
+// w*64*kOtItems + j*64 + l) by the digit dg[j] < 64: earlier elements with
+// the same digit keep their order.  Ends synchronised.
+template <int NW>
 __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, int32_t (&pos)[kOtItems],
-                                        OtRank& s) {
+                                        OtRank<NW>& s) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t lt = (1ull << lane) - 1ull;
   s.run[w][lane] = 0;
@@ -221,10 +249,12 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, i
     pos[j] = r0 + __popcll(peers & lt);
     if (valid && (peers & lt) == 0) s.run[w][d] = r0 + __popcll(peers);
   }
-  __syncthreads();
+  ot_sync<NW>();
   if (threadIdx.x < 64) {
     const int d = threadIdx.x;
-    const int32_t tot = s.run[0][d] + s.run[1][d] + s.run[2][d] + s.run[3][d];
+    int32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < NW; ww++) tot += s.run[ww][d];
     int32_t inc = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -235,43 +265,47 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, i
     s.dbase[d] = acc;
     if (d == 63) s.dbase[64] = inc;
 #pragma unroll
-    for (int ww = 0; ww < 4; ww++) {
+    for (int ww = 0; ww < NW; ww++) {
       s.base[ww][d] = acc;
       acc += s.run[ww][d];
     }
   }
-  __syncthreads();
+  ot_sync<NW>();
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) pos[j] += s.base[w][dg[j]];
 }
 
-// Stable sort of n packed words (offset << 12 | index) held as items, by
-// the offset's low 6 bits and, if both, then by its high 6 bits; the sorted
-// words end in pk[0..n).  Ends synchronised.
-__device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, bool both, uint32_t* pk, OtRank& s) {
+// Stable sort of n packed words (offset << 12 | index) held as items; the
+// sorted words end in pk[0..n).  full: by the whole offset (low 6 bits, then
+// high 6 bits); else by its low kOtSlabBits bits (the words of one slab).
+// Ends synchronised.
+template <int NW>
+__device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, bool full, uint32_t* pk,
+                                        OtRank<NW>& s) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * kOtItems);
+  const uint32_t m0 = full ? 63u : (1u << kOtSlabBits) - 1u;
   uint32_t dg[kOtItems];
   int32_t pos[kOtItems];
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) dg[j] = (key[j] >> 12) & 63u;
-  ot_rank(dg, n, pos, s);
+  for (int j = 0; j < kOtItems; j++) dg[j] = (key[j] >> kOtIdxBits) & m0;
+  ot_rank<NW>(dg, n, pos, s);
 #pragma unroll
   for (int j = 0; j < kOtItems; j++)
     if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
-  __syncthreads();
-  if (!both) return;
+  ot_sync<NW>();
+  if (!full) return;
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
     key[j] = e < n ? pk[e] : 0u;
-    dg[j] = (key[j] >> 18) & 63u;
+    dg[j] = (key[j] >> (kOtIdxBits + 6)) & 63u;
   }
-  ot_rank(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
+  ot_rank<NW>(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
 #pragma unroll
   for (int j = 0; j < kOtItems; j++)
     if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
-  __syncthreads();
+  ot_sync<NW>();
 }
 
 __global__ __launch_bounds__(256) void k_ot_tile(int64_t* __restrict__ time, int32_t* __restrict__ rule,
@@ -279,18 +313,17 @@ __global__ __launch_bounds__(256) void k_ot_tile(int64_t* __restrict__ time, int
                                                   const int64_t* __restrict__ tile_base,
                                                   const int64_t* __restrict__ node_off, int64_t t0,
                                                   int32_t* __restrict__ pre) {
-  __shared__ OtRank s;
-  __shared__ uint32_t pk[kOtChunk];
-  __shared__ int32_t rl[kOtChunk];
+  __shared__ OtRank<4> s;
+  __shared__ uint32_t pk[kOtTile];
+  __shared__ int32_t rl[kOtTile];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t t = blockIdx.x;
-  const TileRange r = tile_range(t, tile_node, tile_base, node_off);
+  const TileRange r = tile_range(t, tile_node, tile_base, node_off, kOtTile);
   const int n = int(r.hi - r.lo);
   const int ebase = w * (64 * kOtItems);
-  uint32_t key[kOtItems];
   const uint32_t* __restrict__ tlo = reinterpret_cast<const uint32_t*>(time);  // low words: offsets < 4096
   const uint32_t b = uint32_t(t0 + 1);
-  uint32_t tv[kOtItems];
+  uint32_t key[kOtItems], tv[kOtItems];
   int32_t rv[kOtItems];
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {  // every load issued before any is used
@@ -302,23 +335,33 @@ __global__ __launch_bounds__(256) void k_ot_tile(int64_t* __restrict__ time, int
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
-    key[j] = e < n ? ((tv[j] - b) << 12) | uint32_t(e) : 0u;
+    key[j] = e < n ? ((tv[j] - b) << kOtIdxBits) | uint32_t(e) : 0u;
     if (e < n) rl[e] = rv[j];
   }
-  ot_sort(key, n, true, pk, s);
-  if (threadIdx.x <= 64) pre[t * 65 + threadIdx.x] = s.dbase[threadIdx.x];  // slab prefix of the last pass
+  ot_sort<4>(key, n, true, pk, s);
+  int32_t* __restrict__ pt = pre + t * kOtPre;
+  if constexpr (kOtSlabBits == 6) {  // slabs = the last pass's digits
+    if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];
+  }
   for (int p = threadIdx.x; p < n; p += 256) {
     const uint32_t v = pk[p];
-    __builtin_nontemporal_store(t0 + 1 + int64_t(v >> 12), time + r.lo + p);
-    __builtin_nontemporal_store(rl[v & 4095u], rule + r.lo + p);
+    __builtin_nontemporal_store(t0 + 1 + int64_t(v >> kOtIdxBits), time + r.lo + p);
+    __builtin_nontemporal_store(rl[v & kOtIdxMask], rule + r.lo + p);
+    if constexpr (kOtSlabBits != 6) {  // slab prefix: the slabs that start at p (and past the last event, n)
+      const int sp = int(v >> (kOtIdxBits + kOtSlabBits));
+      const int sq = p > 0 ? int(pk[p - 1] >> (kOtIdxBits + kOtSlabBits)) : -1;
+      for (int k = sq + 1; k <= sp; k++) pt[k] = p;
+      if (p == n - 1)
+        for (int k = sp + 1; k <= kOtSlabs; k++) pt[k] = n;
+    }
   }
 }
 
-// Block-wide exclusive scan of cnt(q) for q in [0, Q) (Q <= kOtGroup) into
-// ps[0..Q] (ps[Q] = total); src(q) into psrc.  Ends synchronised.
-template <class Portion>
-__device__ __forceinline__ void ot_portions(int Q, Portion&& portion, int32_t* ps, int64_t* psrc, int32_t* wsum) {
-  constexpr int PER = kOtGroup / 256;
+// Exclusive scan of cnt(q) for q in [0, Q) (Q <= kOtMaxTiles) into ps[0..Q]
+// (ps[Q] = total); src(q) into psrc.  Ends synchronised.
+template <int NW, class Portion>
+__device__ __forceinline__ void ot_portions(int Q, Portion&& portion, int32_t* ps, int32_t* psrc, int32_t* wsum) {
+  constexpr int PER = (kOtMaxTiles + 64 * NW - 1) / (64 * NW);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int32_t c[PER], sum = 0;
 #pragma unroll
@@ -326,7 +369,7 @@ __device__ __forceinline__ void ot_portions(int Q, Portion&& portion, int32_t* p
     const int q = threadIdx.x * PER + i;
     c[i] = 0;
     if (q < Q) {
-      int64_t src;
+      int32_t src;
       c[i] = portion(q, &src);
       psrc[q] = src;
     }
@@ -338,18 +381,20 @@ __device__ __forceinline__ void ot_portions(int Q, Portion&& portion, int32_t* p
     const int32_t y = __shfl_up(inc, o, 64);
     if (lane >= o) inc += y;
   }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
   int32_t run = inc - sum;
-  for (int ww = 0; ww < w; ww++) run += wsum[ww];
+  if constexpr (NW > 1) {
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    for (int ww = 0; ww < w; ww++) run += wsum[ww];
+  }
 #pragma unroll
   for (int i = 0; i < PER; i++) {
     const int q = threadIdx.x * PER + i;
     if (q < Q) ps[q] = run;
     run += c[i];
   }
-  if (threadIdx.x == 255) ps[Q] = run;
-  __syncthreads();
+  if (threadIdx.x == 64 * NW - 1) ps[Q] = run;
+  ot_sync<NW>();
 }
 
 // the portion holding element e of the list (ps ascending, ps[0] = 0)
@@ -363,27 +408,30 @@ __device__ __forceinline__ int ot_find(const int32_t* ps, int Q, int32_t e) {
   return lo;
 }
 
-// own[i] = the portion holding element c0 + i of the list, i < n_el <=
-// kOtChunk: every non-empty portion marks its first element and an inclusive
+// own[i] = the portion holding element c0 + i of the list, i < n_el <= the
+// chunk: every non-empty portion marks its first element and an inclusive
 // max-scan fills the rest (portion indices grow with position), so no
-// element searches.  Ends synchronised.
+// element searches.  own is padded (element i at i + i / 32) so the scan's
+// per-thread runs of kOtItems do not collide in the LDS banks.  Ends
+// synchronised.
+__device__ __forceinline__ int ot_pad(int i) { return i + (i >> 5); }
+template <int NW>
 __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, int n_el, int32_t* own,
                                           int32_t* wsum) {
-  constexpr int PER = kOtChunk / 256;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int i = threadIdx.x; i < n_el; i += 256) own[i] = -1;
-  __syncthreads();
-  for (int q = threadIdx.x; q < Q; q += 256) {
+  for (int i = threadIdx.x; i < n_el; i += 64 * NW) own[ot_pad(i)] = -1;
+  ot_sync<NW>();
+  for (int q = threadIdx.x; q < Q; q += 64 * NW) {
     const int32_t a = ps[q];
-    if (a < ps[q + 1] && a >= c0 && a < c0 + n_el) own[a - c0] = q;
+    if (a < ps[q + 1] && a >= c0 && a < c0 + n_el) own[ot_pad(a - c0)] = q;
   }
   if (threadIdx.x == 0) own[0] = ot_find(ps, Q, c0);  // the portion the chunk starts in (the same q if it starts at c0)
-  __syncthreads();
-  int32_t v[PER], m = -1;
+  ot_sync<NW>();
+  int32_t v[kOtItems], m = -1;
 #pragma unroll
-  for (int i = 0; i < PER; i++) {
-    const int idx = threadIdx.x * PER + i;
-    v[i] = idx < n_el ? own[idx] : -1;
+  for (int i = 0; i < kOtItems; i++) {
+    const int idx = threadIdx.x * kOtItems + i;
+    v[i] = idx < n_el ? own[ot_pad(idx)] : -1;
     m = v[i] > m ? v[i] : m;
     v[i] = m;
   }
@@ -393,29 +441,31 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
     const int32_t y = __shfl_up(inc, o, 64);
     if (lane >= o) inc = y > inc ? y : inc;
   }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
   int32_t prev = __shfl_up(inc, 1, 64);
   if (lane == 0) prev = -1;
-  for (int ww = 0; ww < w; ww++) prev = wsum[ww] > prev ? wsum[ww] : prev;
-#pragma unroll
-  for (int i = 0; i < PER; i++) {
-    const int idx = threadIdx.x * PER + i;
-    if (idx < n_el) own[idx] = v[i] > prev ? v[i] : prev;
+  if constexpr (NW > 1) {
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    for (int ww = 0; ww < w; ww++) prev = wsum[ww] > prev ? wsum[ww] : prev;
   }
-  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kOtItems; i++) {
+    const int idx = threadIdx.x * kOtItems + i;
+    if (idx < n_el) own[ot_pad(idx)] = v[i] > prev ? v[i] : prev;
+  }
+  ot_sync<NW>();
 }
 
-// Items of elements c0 .. c0 + n_el of the portion list: key = (offset << 12
-// | chunk index), rule into rl[chunk index] (RULES).  All loads issued before
-// any is used (clamped indices).
+// Items of elements c0 .. c0 + n_el of the portion list (sources relative
+// to tin / rin, < 2^31): key = (offset << 12 | chunk index), rule into
+// rl[chunk index] (RULES).  All loads issued before any is used (clamped
+// indices); the low words of the times suffice.
 template <bool RULES>
 __device__ __forceinline__ void ot_gather(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
-                                          int64_t t0, const int32_t* ps, const int64_t* psrc, const int32_t* own,
+                                          int64_t t0, const int32_t* ps, const int32_t* psrc, const int32_t* own,
                                           int32_t c0, int n_el, uint32_t (&key)[kOtItems], int32_t* rl) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * kOtItems);
-  // the low words of the times suffice: offsets are < 4096
   const uint32_t* __restrict__ tlo = reinterpret_cast<const uint32_t*>(tin);
   const uint32_t b = uint32_t(t0 + 1);
   uint32_t tv[kOtItems];
@@ -424,32 +474,76 @@ __device__ __forceinline__ void ot_gather(const int64_t* __restrict__ tin, const
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
     const int ec = e < n_el ? e : n_el - 1;
-    const int q = own[ec];
-    const int64_t src = psrc[q] + (c0 + ec - ps[q]);
-    tv[j] = tlo[2 * src];
+    const int q = own[ot_pad(ec)];
+    const uint32_t src = uint32_t(psrc[q] + (c0 + ec - ps[q]));
+    tv[j] = tlo[2u * src];
     if (RULES) rv[j] = rin[src];
   }
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
-    key[j] = e < n_el ? ((tv[j] - b) << 12) | uint32_t(e) : 0u;
+    key[j] = e < n_el ? ((tv[j] - b) << kOtIdxBits) | uint32_t(e) : 0u;
     if (RULES && e < n_el) rl[e] = rv[j];
   }
 }
 
-__global__ __launch_bounds__(256, 4) void k_ot_merge(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
-                                                   const int64_t* __restrict__ tile_base,
-                                                   const int64_t* __restrict__ node_off,
-                                                   const int32_t* __restrict__ pre, int32_t N, int64_t t0,
-                                                   int64_t* __restrict__ tout, int32_t* __restrict__ rout,
-                                                   int64_t* __restrict__ big, unsigned* __restrict__ big_n) {
-  __shared__ OtRank s;
-  __shared__ uint32_t pk[kOtChunk];  // the owner list while gathering, then the sorted words
-  __shared__ int32_t rl[kOtChunk];
-  __shared__ int32_t ps[kOtGroup + 1];
-  __shared__ int64_t psrc[kOtGroup];
-  __shared__ int64_t slab_off[65];  // node-relative first position of each slab; [64] = the node's events
-  __shared__ int32_t wsum[4];
+// Per node: the first node-relative position of each slab (events of the
+// earlier slabs over all its tiles), slab_off[n][0..kOtSlabs].  One wave per
+// node, kOtSlabs / 64 slabs per lane.
+__global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ tile_base,
+                                                  const int32_t* __restrict__ pre, int32_t N,
+                                                  int64_t* __restrict__ slab_off) {
+  constexpr int kSpl = kOtSlabs / 64;
+  const int lane = threadIdx.x;
+  const int32_t n = blockIdx.x;
+  if (n >= N) return;
+  const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta;
+  int64_t c[kSpl];
+#pragma unroll
+  for (int i = 0; i < kSpl; i++) c[i] = 0;
+  for (int64_t t = ta; t < ta + M; t++) {
+    const int32_t* pt = pre + t * kOtPre + kSpl * lane;
+    int32_t p[kSpl + 1];
+#pragma unroll
+    for (int i = 0; i <= kSpl; i++) p[i] = pt[i];
+#pragma unroll
+    for (int i = 0; i < kSpl; i++) c[i] += p[i + 1] - p[i];
+  }
+  int64_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < kSpl; i++) sum += c[i];
+  int64_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
+  }
+  int64_t run = inc - sum;
+  int64_t* so = slab_off + int64_t(n) * kOtPre;
+#pragma unroll
+  for (int i = 0; i < kSpl; i++) {
+    so[kSpl * lane + i] = run;
+    run += c[i];
+  }
+  if (lane == 63) so[kOtSlabs] = run;
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
+                                                       const int64_t* __restrict__ tile_base,
+                                                       const int64_t* __restrict__ node_off,
+                                                       const int32_t* __restrict__ pre, int32_t N, int64_t t0,
+                                                       const int64_t* __restrict__ slab_tab,
+                                                       int64_t* __restrict__ tout, int32_t* __restrict__ rout,
+                                                       int64_t* __restrict__ big, unsigned* __restrict__ big_n) {
+  constexpr int kThreads = 64 * NW, kChunk = kThreads * kOtItems;
+  __shared__ OtRank<NW> s;
+  __shared__ uint32_t pk[kChunk + kChunk / 32];  // the owner list while gathering (padded), then the sorted words
+  __shared__ int32_t rl[kChunk];
+  __shared__ int32_t ps[kOtMaxTiles + 1];
+  __shared__ int32_t psrc[kOtMaxTiles];       // node-relative (M <= kOtMaxTiles: < 2^20)
+  __shared__ int64_t slab_off[kOtSlabs + 1];  // node-relative first position of each slab
+  __shared__ int32_t wsum[NW];
   int32_t* own = reinterpret_cast<int32_t*>(pk);
   const int32_t n = blockIdx.x;
   if (n >= N) return;
@@ -457,137 +551,114 @@ __global__ __launch_bounds__(256, 4) void k_ot_merge(const int64_t* __restrict__
   if (M == 0) return;
   if (M == 1) {  // one tile: already in order
     const int64_t e = node_off[n + 1] - lo_n;
-    for (int64_t p = threadIdx.x; p < e; p += 256) {
+    for (int64_t p = threadIdx.x; p < e; p += kThreads) {
       __builtin_nontemporal_store(tin[lo_n + p], tout + lo_n + p);
       __builtin_nontemporal_store(rin[lo_n + p], rout + lo_n + p);
     }
     return;
   }
-  if (threadIdx.x < 64) {  // slab totals over the node's tiles, exclusive prefix
-    const int d = threadIdx.x;
-    int64_t tot = 0;
-    for (int64_t t = ta; t < ta + M; t++) tot += pre[t * 65 + d + 1] - pre[t * 65 + d];
-    int64_t inc = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int64_t y = __shfl_up(inc, o, 64);
-      if (d >= o) inc += y;
-    }
-    slab_off[d] = inc - tot;
-    if (d == 63) slab_off[64] = inc;
+  if (M > kOtMaxTiles) {  // every slab to k_ot_big
+    for (int j = threadIdx.x; j < kOtSlabs; j += kThreads) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | j;
+    return;
   }
-  __syncthreads();
-  // the portion list of slabs [ja, jb): per tile its sorted events of those
-  // slabs, one contiguous range (tile order; the sort by offset then keeps
-  // tile order, i.e. rule order, for equal offsets)
-  auto list = [&](int ja, int jb) {
-    const int Q = int(M);
-    ot_portions(
-        Q,
-        [&](int q, int64_t* src) {
-          const int64_t t = ta + q;
-          const int32_t a = pre[t * 65 + ja];
-          *src = lo_n + int64_t(q) * kTsTile + a;
-          return pre[t * 65 + jb] - a;
-        },
-        ps, psrc, wsum);
-    return Q;
-  };
+  for (int j = threadIdx.x; j <= kOtSlabs; j += kThreads) slab_off[j] = slab_tab[int64_t(n) * kOtPre + j];
+  ot_sync<NW>();
   uint32_t key[kOtItems];
   int ja = 0;
-  while (ja < 64) {
-    // a run of whole slabs [ja, jb) that fits one chunk (nodes of at most
-    // kOtGroup tiles)
+  while (ja < kOtSlabs) {
+    // the longest run of whole slabs [ja, jb) that fits one chunk
     int jb = ja;
-    while (M <= kOtGroup && jb < 64 && slab_off[jb + 1] - slab_off[ja] <= kOtChunk) jb++;
-    if (jb > ja) {
-      const int n_el = int(slab_off[jb] - slab_off[ja]);
-      if (n_el > 0) {
-        const int Q = list(ja, jb);
-        ot_owners(ps, Q, 0, n_el, own, wsum);
-        ot_gather<true>(tin, rin, t0, ps, psrc, own, 0, n_el, key, rl);
-        ot_sort(key, n_el, jb - ja > 1, pk, s);
-        const int64_t o = lo_n + slab_off[ja];
-        for (int p = threadIdx.x; p < n_el; p += 256) {
-          const uint32_t v = pk[p];
-          __builtin_nontemporal_store(t0 + 1 + int64_t(v >> 12), tout + o + p);
-          __builtin_nontemporal_store(rl[v & 4095u], rout + o + p);
-        }
-        __syncthreads();
-      }
-      ja = jb;
+    while (jb < kOtSlabs && slab_off[jb + 1] - slab_off[ja] <= kChunk) jb++;
+    if (jb == ja) {  // one slab of more than a chunk
+      if (threadIdx.x == 0) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | ja;
+      ja++;
       continue;
     }
-    // slab ja alone (more than a chunk, or more tiles than a portion list):
-    // k_ot_big
-    if (threadIdx.x == 0) {
-      const unsigned k = atomicAdd(big_n, 1u);
-      big[k] = (int64_t(n) << 8) | ja;
+    const int n_el = int(slab_off[jb] - slab_off[ja]);
+    if (n_el > 0) {
+      // per tile its sorted events of slabs [ja, jb): one contiguous range
+      ot_portions<NW>(
+          int(M),
+          [&](int q, int32_t* src) {
+            const int32_t* pt = pre + (ta + q) * kOtPre;
+            const int32_t a = pt[ja];
+            *src = q * kOtTile + a;
+            return pt[jb] - a;
+          },
+          ps, psrc, wsum);
+      ot_owners<NW>(ps, int(M), 0, n_el, own, wsum);
+      ot_gather<true>(tin + lo_n, rin + lo_n, t0, ps, psrc, own, 0, n_el, key, rl);
+      ot_sort<NW>(key, n_el, jb - ja > 1, pk, s);
+      const int64_t o = lo_n + slab_off[ja];
+      for (int p = threadIdx.x; p < n_el; p += kThreads) {
+        const uint32_t v = pk[p];
+        __builtin_nontemporal_store(t0 + 1 + int64_t(v >> kOtIdxBits), tout + o + p);
+        __builtin_nontemporal_store(rl[v & kOtIdxMask], rout + o + p);
+      }
+      ot_sync<NW>();
     }
-    ja++;
+    ja = jb;
   }
 }
 
-// The slabs k_ot_merge leaves (more events than a chunk, or a node of more
-// than kOtGroup tiles), one per workgroup turn: the slab's low-6-bit
-// histogram over all its portions first, then its chunks in order, each
-// sorted in LDS and stored at its digits' running bases.
-__global__ __launch_bounds__(256, 4) void k_ot_big(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
-                                                    const int64_t* __restrict__ tile_base,
-                                                    const int64_t* __restrict__ node_off,
-                                                    const int32_t* __restrict__ pre, int64_t t0,
-                                                    int64_t* __restrict__ tout, int32_t* __restrict__ rout,
-                                                    const int64_t* __restrict__ big, const unsigned* __restrict__ big_n) {
-  __shared__ OtRank s;
-  __shared__ uint32_t pk[kOtChunk];
-  __shared__ int32_t rl[kOtChunk];
-  __shared__ int32_t ps[kOtGroup + 1];
-  __shared__ int64_t psrc[kOtGroup];
+// The slabs k_ot_merge queued, one per workgroup turn: the slab's
+// histogram of its 16 seconds over all its portions first, then its chunks
+// in order, each sorted in LDS and stored at its seconds' running bases.
+__global__ __launch_bounds__(256) void k_ot_big(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
+                                                 const int64_t* __restrict__ tile_base,
+                                                 const int64_t* __restrict__ node_off,
+                                                 const int32_t* __restrict__ pre, int64_t t0,
+                                                 int64_t* __restrict__ tout, int32_t* __restrict__ rout,
+                                                 const int64_t* __restrict__ big, const unsigned* __restrict__ big_n) {
+  __shared__ OtRank<4> s;
+  __shared__ uint32_t pk[kOtTile + kOtTile / 32];
+  __shared__ int32_t rl[kOtTile];
+  __shared__ int32_t ps[kOtMaxTiles + 1];
+  __shared__ int32_t psrc[kOtMaxTiles];  // relative to the group's first tile
   __shared__ int64_t gbase[64];
   __shared__ int32_t hist[64];
   __shared__ int32_t wsum[4];
   __shared__ int64_t red[4];
   int32_t* own = reinterpret_cast<int32_t*>(pk);
+  const int lane = threadIdx.x & 63, ebase = (threadIdx.x >> 6) * (64 * kOtItems);
+  constexpr uint32_t kSec = (1u << kOtSlabBits) - 1u;
   const unsigned nb = *big_n;
   for (unsigned task = blockIdx.x; task < nb; task += gridDim.x) {
     const int32_t n = int32_t(big[task] >> 8);
     const int j = int(big[task] & 255);
     const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta, lo_n = node_off[n];
-    auto list = [&](int j0, int nj, int64_t g0, int64_t gm) {
-      const int Q = int(nj * gm);
-      ot_portions(
-          Q,
-          [&](int q, int64_t* src) {
-            const int jq = j0 + int(q / gm);
-            const int64_t t = ta + g0 + q % gm;
-            *src = lo_n + (t - ta) * int64_t(kTsTile) + pre[t * 65 + jq];
-            return pre[t * 65 + jq + 1] - pre[t * 65 + jq];
+    // portions of tiles [ga, ga + gm): per tile its events of slab j
+    auto list = [&](int64_t ga, int64_t gm) {
+      ot_portions<4>(
+          int(gm),
+          [&](int q, int32_t* src) {
+            const int32_t* pt = pre + (ta + ga + q) * kOtPre;
+            *src = q * kOtTile + pt[j];
+            return pt[j + 1] - pt[j];
           },
           ps, psrc, wsum);
-      return Q;
+      return int(gm);
     };
     // the slab's first position: events of earlier slabs over the node's tiles
     int64_t before = 0;
-    for (int64_t t = ta + threadIdx.x; t < ta + M; t += 256) before += pre[t * 65 + j];
+    for (int64_t t = ta + threadIdx.x; t < ta + M; t += 256) before += pre[t * kOtPre + j];
 #pragma unroll
     for (int o = 32; o; o >>= 1) before += __shfl_xor(before, o, 64);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = before;
+    if (lane == 0) red[threadIdx.x >> 6] = before;
+    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
     __syncthreads();
     const int64_t slab_lo = lo_n + red[0] + red[1] + red[2] + red[3];
     uint32_t key[kOtItems];
-    if (threadIdx.x < 64) hist[threadIdx.x] = 0;
-    __syncthreads();
-    for (int64_t ga = 0; ga < M; ga += kOtGroup) {  // histogram of the low 6 bits
-      const int Q = list(j, 1, ga, M - ga < kOtGroup ? M - ga : kOtGroup);
+    for (int64_t ga = 0; ga < M; ga += kOtMaxTiles) {  // histogram of the slab's seconds
+      const int Q = list(ga, M - ga < kOtMaxTiles ? M - ga : kOtMaxTiles);
       const int32_t n_grp = ps[Q];
-      for (int32_t c0 = 0; c0 < n_grp; c0 += kOtChunk) {
-        const int n_el = n_grp - c0 < kOtChunk ? int(n_grp - c0) : kOtChunk;
-        ot_owners(ps, Q, c0, n_el, own, wsum);
-        ot_gather<false>(tin, rin, t0, ps, psrc, own, c0, n_el, key, rl);
-        const int ebase = (threadIdx.x >> 6) * (64 * kOtItems);
+      for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
+        const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
+        ot_owners<4>(ps, Q, c0, n_el, own, wsum);
+        ot_gather<false>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, t0, ps, psrc, own, c0, n_el, key, rl);
 #pragma unroll
         for (int jj = 0; jj < kOtItems; jj++)
-          if (ebase + jj * 64 + (threadIdx.x & 63) < n_el) atomicAdd(&hist[(key[jj] >> 12) & 63u], 1);
+          if (ebase + jj * 64 + lane < n_el) atomicAdd(&hist[(key[jj] >> kOtIdxBits) & kSec], 1);
         __syncthreads();
       }
     }
@@ -603,27 +674,26 @@ __global__ __launch_bounds__(256, 4) void k_ot_big(const int64_t* __restrict__ t
       gbase[d] = slab_lo + inc - c;
     }
     __syncthreads();
-    for (int64_t ga = 0; ga < M; ga += kOtGroup) {  // chunks in order, each digit at its running base
-      const int Q = list(j, 1, ga, M - ga < kOtGroup ? M - ga : kOtGroup);
+    for (int64_t ga = 0; ga < M; ga += kOtMaxTiles) {  // chunks in order, each second at its running base
+      const int Q = list(ga, M - ga < kOtMaxTiles ? M - ga : kOtMaxTiles);
       const int32_t n_grp = ps[Q];
-      for (int32_t c0 = 0; c0 < n_grp; c0 += kOtChunk) {
-        const int n_el = n_grp - c0 < kOtChunk ? int(n_grp - c0) : kOtChunk;
-        ot_owners(ps, Q, c0, n_el, own, wsum);
-        ot_gather<true>(tin, rin, t0, ps, psrc, own, c0, n_el, key, rl);
-        ot_sort(key, n_el, false, pk, s);
+      for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
+        const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
+        ot_owners<4>(ps, Q, c0, n_el, own, wsum);
+        ot_gather<true>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, t0, ps, psrc, own, c0, n_el, key, rl);
+        ot_sort<4>(key, n_el, false, pk, s);
         for (int p = threadIdx.x; p < n_el; p += 256) {
           const uint32_t v = pk[p];
-          const uint32_t d = (v >> 12) & 63u;
+          const uint32_t d = (v >> kOtIdxBits) & kSec;
           const int64_t dst = gbase[d] + (p - s.dbase[d]);
-          tout[dst] = t0 + 1 + int64_t(v >> 12);
-          rout[dst] = rl[v & 4095u];
+          tout[dst] = t0 + 1 + int64_t(v >> kOtIdxBits);
+          rout[dst] = rl[v & kOtIdxMask];
         }
         __syncthreads();
         if (threadIdx.x < 64) gbase[threadIdx.x] += s.dbase[threadIdx.x + 1] - s.dbase[threadIdx.x];
         __syncthreads();
       }
     }
-    __syncthreads();  // red, gbase and the lists are rewritten by the next task
   }
 }
 
@@ -648,16 +718,19 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   const int passes = std::max(1, (bits + kTsBits - 1) / kTsBits);
   hipStream_t st = c->st;
 
+  // windows <= 4096 s: tile sort + merge (CG_ORDER_LSD=1: the LSD passes)
+  static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;
+  const bool merge = bits <= 12 && !lsd_only;
+  const int tile = merge ? kOtTile : kTsTile;
   if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1))) return rc;
   if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N))))) return rc;
-  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, c->node_off.p, N, c->ts_cnt.p);
+  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, c->node_off.p, N, tile, c->ts_cnt.p);
   launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
   int64_t T = 0;
   if ((rc = cg_hip_check(hipMemcpyAsync(&T, c->ts_base.p + N, 8, hipMemcpyDeviceToHost, st), "tiles")) ||
       (rc = cg_hip_check(hipStreamSynchronize(st), "sync")))
     return rc;
-  const bool merge = bits <= 12 && !getenv("CG_ORDER_LSD");
-  if ((rc = c->ts_tile_node.ensure(T)) || (rc = c->ts_hist.ensure(T * (merge ? 65 : kTsDigits))) ||
+  if ((rc = c->ts_tile_node.ensure(T)) || (rc = c->ts_hist.ensure(T * (merge ? kOtPre : kTsDigits))) ||
       (!merge && (rc = c->ts_off.ensure(T * kTsDigits))) || (rc = c->node_time2.ensure(En)) ||
       (rc = c->node_rule2.ensure(En)))
     return rc;
@@ -666,16 +739,19 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   if (merge) {
     hipLaunchKernelGGL(k_ot_tile, dim3(unsigned(T)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
                        c->ts_tile_node.p, c->ts_base.p, c->node_off.p, c->pn_t0, c->ts_hist.p);
-    // big-slab tasks: at most 64 per node, after one counter word
-    if ((rc = c->ts_off.ensure(int64_t(N) * 64 + 1))) return rc;
-    unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * 64);
+    // big-slab tasks: at most kOtSlabs per node, after one counter word
+    // (then the per-node slab tables, N x kOtPre)
+    if ((rc = c->ts_off.ensure(int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre))) return rc;
+    unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
     if ((rc = cg_hip_check(hipMemsetAsync(big_n, 0, 8, st), "memset"))) return rc;
-    hipLaunchKernelGGL(k_ot_merge, dim3(unsigned(N)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                       c->ts_base.p, c->node_off.p, c->ts_hist.p, N, c->pn_t0, c->node_time2.p, c->node_rule2.p,
-                       c->ts_off.p, big_n);
-    hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, c->node_time.p,
-                       c->node_rule.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, c->pn_t0, c->node_time2.p,
-                       c->node_rule2.p, c->ts_off.p, big_n);
+    int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
+    hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
+    hipLaunchKernelGGL(k_ot_merge<kOtMergeWaves>, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st,
+                       c->node_time.p, c->node_rule.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, N, c->pn_t0,
+                       slab_tab, c->node_time2.p, c->node_rule2.p, c->ts_off.p, big_n);
+    hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st,
+                       c->node_time.p, c->node_rule.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, c->pn_t0,
+                       c->node_time2.p, c->node_rule2.p, c->ts_off.p, big_n);
     (void)hipEventRecord(c->pev[1], st);
     if ((rc = cg_hip_check(hipGetLastError(), "time-order kernels"))) return rc;
     std::swap(c->node_time, c->node_time2);

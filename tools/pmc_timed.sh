@@ -13,8 +13,9 @@ for p in p1 p2; do
 import csv, sys, collections
 agg = collections.defaultdict(float); n = collections.Counter()
 for r in csv.DictReader(open(sys.argv[1])):
-    if 'k_node_timed' not in r['Kernel_Name'] and 'k_node_write' not in r['Kernel_Name']: continue
-    k = ('timed' if 'k_node_timed' in r['Kernel_Name'] else 'write') + ':' + r['Counter_Name']
+    kn = next((x for x in ('k_ot_tile', 'k_ot_merge', 'k_ot_big', 'k_node_write') if x in r['Kernel_Name']), None)
+    if kn is None: continue
+    k = kn + ':' + r['Counter_Name']
     agg[k] += float(r['Counter_Value']); n[k] += 1
 for k in sorted(agg): print(k, '%.4g' % (agg[k] / max(1, n[k]) * 1), 'per-dispatch-avg(sum over rows/dispatch rows)')
 PY
