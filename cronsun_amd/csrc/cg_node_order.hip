@@ -185,7 +185,8 @@ __global__ __launch_bounds__(256) void k_ts_scatter(const int64_t* __restrict__ 
 //   k_ot_big    per queued slab: the histogram of its 16 seconds over all its
 //               portions, then its chunks in order, each sorted in LDS and
 //               stored at its seconds' running bases
-// Each event is read and written twice (24 B + 24 B) and every store is
+// The sorted tiles are kept as 16-bit offsets + rules (6 B per event), so
+// the two passes move 12 + 6 + 6 + 12 = 36 B per event, every store
 // coalesced, where the LSD passes above scatter each event to its own
 // address per pass and read the times again for every histogram.
 constexpr int kOtItems = 16;                  // per thread
@@ -308,10 +309,11 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, bool f
   ot_sync<NW>();
 }
 
-__global__ __launch_bounds__(256) void k_ot_tile(int64_t* __restrict__ time, int32_t* __restrict__ rule,
+__global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ time, const int32_t* __restrict__ rule,
                                                   const int32_t* __restrict__ tile_node,
                                                   const int64_t* __restrict__ tile_base,
                                                   const int64_t* __restrict__ node_off, int64_t t0,
+                                                  uint16_t* __restrict__ toff_out, int32_t* __restrict__ rule_out,
                                                   int32_t* __restrict__ pre) {
   __shared__ OtRank<4> s;
   __shared__ uint32_t pk[kOtTile];
@@ -345,8 +347,8 @@ __global__ __launch_bounds__(256) void k_ot_tile(int64_t* __restrict__ time, int
   }
   for (int p = threadIdx.x; p < n; p += 256) {
     const uint32_t v = pk[p];
-    __builtin_nontemporal_store(t0 + 1 + int64_t(v >> kOtIdxBits), time + r.lo + p);
-    __builtin_nontemporal_store(rl[v & kOtIdxMask], rule + r.lo + p);
+    toff_out[r.lo + p] = uint16_t(v >> kOtIdxBits);
+    __builtin_nontemporal_store(rl[v & kOtIdxMask], rule_out + r.lo + p);
     if constexpr (kOtSlabBits != 6) {  // slab prefix: the slabs that start at p (and past the last event, n)
       const int sp = int(v >> (kOtIdxBits + kOtSlabBits));
       const int sq = p > 0 ? int(pk[p - 1] >> (kOtIdxBits + kOtSlabBits)) : -1;
@@ -457,17 +459,15 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 }
 
 // Items of elements c0 .. c0 + n_el of the portion list (sources relative
-// to tin / rin, < 2^31): key = (offset << 12 | chunk index), rule into
-// rl[chunk index] (RULES).  All loads issued before any is used (clamped
-// indices); the low words of the times suffice.
+// to tin / rin, < 2^31; tin = the tile sort's 16-bit offsets): key =
+// (offset << 12 | chunk index), rule into rl[chunk index] (RULES).  All loads
+// issued before any is used (clamped indices).
 template <bool RULES>
-__device__ __forceinline__ void ot_gather(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
-                                          int64_t t0, const int32_t* ps, const int32_t* psrc, const int32_t* own,
+__device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
+                                          const int32_t* ps, const int32_t* psrc, const int32_t* own,
                                           int32_t c0, int n_el, uint32_t (&key)[kOtItems], int32_t* rl) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * kOtItems);
-  const uint32_t* __restrict__ tlo = reinterpret_cast<const uint32_t*>(tin);
-  const uint32_t b = uint32_t(t0 + 1);
   uint32_t tv[kOtItems];
   int32_t rv[kOtItems];
 #pragma unroll
@@ -476,13 +476,13 @@ __device__ __forceinline__ void ot_gather(const int64_t* __restrict__ tin, const
     const int ec = e < n_el ? e : n_el - 1;
     const int q = own[ot_pad(ec)];
     const uint32_t src = uint32_t(psrc[q] + (c0 + ec - ps[q]));
-    tv[j] = tlo[2u * src];
+    tv[j] = tin[src];
     if (RULES) rv[j] = rin[src];
   }
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
-    key[j] = e < n_el ? ((tv[j] - b) << kOtIdxBits) | uint32_t(e) : 0u;
+    key[j] = e < n_el ? (tv[j] << kOtIdxBits) | uint32_t(e) : 0u;
     if (RULES && e < n_el) rl[e] = rv[j];
   }
 }
@@ -529,7 +529,7 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 }
 
 template <int NW>
-__global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
+__global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
                                                        const int32_t* __restrict__ pre, int32_t N, int64_t t0,
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const int64_t* __restri
   if (M == 1) {  // one tile: already in order
     const int64_t e = node_off[n + 1] - lo_n;
     for (int64_t p = threadIdx.x; p < e; p += kThreads) {
-      __builtin_nontemporal_store(tin[lo_n + p], tout + lo_n + p);
+      __builtin_nontemporal_store(t0 + 1 + int64_t(tin[lo_n + p]), tout + lo_n + p);
       __builtin_nontemporal_store(rin[lo_n + p], rout + lo_n + p);
     }
     return;
@@ -587,7 +587,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const int64_t* __restri
           },
           ps, psrc, wsum);
       ot_owners<NW>(ps, int(M), 0, n_el, own, wsum);
-      ot_gather<true>(tin + lo_n, rin + lo_n, t0, ps, psrc, own, 0, n_el, key, rl);
+      ot_gather<true>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl);
       ot_sort<NW>(key, n_el, jb - ja > 1, pk, s);
       const int64_t o = lo_n + slab_off[ja];
       for (int p = threadIdx.x; p < n_el; p += kThreads) {
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const int64_t* __restri
 // The slabs k_ot_merge queued, one per workgroup turn: the slab's
 // histogram of its 16 seconds over all its portions first, then its chunks
 // in order, each sorted in LDS and stored at its seconds' running bases.
-__global__ __launch_bounds__(256) void k_ot_big(const int64_t* __restrict__ tin, const int32_t* __restrict__ rin,
+__global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                  const int64_t* __restrict__ tile_base,
                                                  const int64_t* __restrict__ node_off,
                                                  const int32_t* __restrict__ pre, int64_t t0,
@@ -655,7 +655,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const int64_t* __restrict__ tin,
       for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
-        ot_gather<false>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, t0, ps, psrc, own, c0, n_el, key, rl);
+        ot_gather<false>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc, own, c0, n_el, key, rl);
 #pragma unroll
         for (int jj = 0; jj < kOtItems; jj++)
           if (ebase + jj * 64 + lane < n_el) atomicAdd(&hist[(key[jj] >> kOtIdxBits) & kSec], 1);
@@ -680,7 +680,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const int64_t* __restrict__ tin,
       for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
-        ot_gather<true>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, t0, ps, psrc, own, c0, n_el, key, rl);
+        ot_gather<true>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc, own, c0, n_el, key, rl);
         ot_sort<4>(key, n_el, false, pk, s);
         for (int p = threadIdx.x; p < n_el; p += 256) {
           const uint32_t v = pk[p];
@@ -737,8 +737,12 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   (void)hipEventRecord(c->pev[0], st);
   hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
   if (merge) {
+    // sorted tiles as 16-bit offsets + rules in the second buffers, merged
+    // back into the result buffers
+    uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
     hipLaunchKernelGGL(k_ot_tile, dim3(unsigned(T)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                       c->ts_tile_node.p, c->ts_base.p, c->node_off.p, c->pn_t0, c->ts_hist.p);
+                       c->ts_tile_node.p, c->ts_base.p, c->node_off.p, c->pn_t0, toff, c->node_rule2.p,
+                       c->ts_hist.p);
     // big-slab tasks: at most kOtSlabs per node, after one counter word
     // (then the per-node slab tables, N x kOtPre)
     if ((rc = c->ts_off.ensure(int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre))) return rc;
@@ -746,16 +750,14 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
     if ((rc = cg_hip_check(hipMemsetAsync(big_n, 0, 8, st), "memset"))) return rc;
     int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
     hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
-    hipLaunchKernelGGL(k_ot_merge<kOtMergeWaves>, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st,
-                       c->node_time.p, c->node_rule.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, N, c->pn_t0,
-                       slab_tab, c->node_time2.p, c->node_rule2.p, c->ts_off.p, big_n);
-    hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st,
-                       c->node_time.p, c->node_rule.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, c->pn_t0,
-                       c->node_time2.p, c->node_rule2.p, c->ts_off.p, big_n);
+    hipLaunchKernelGGL(k_ot_merge<kOtMergeWaves>, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
+                       c->node_rule2.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, N, c->pn_t0, slab_tab,
+                       c->node_time.p, c->node_rule.p, c->ts_off.p, big_n);
+    hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
+                       c->node_rule2.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, c->pn_t0, c->node_time.p,
+                       c->node_rule.p, c->ts_off.p, big_n);
     (void)hipEventRecord(c->pev[1], st);
     if ((rc = cg_hip_check(hipGetLastError(), "time-order kernels"))) return rc;
-    std::swap(c->node_time, c->node_time2);
-    std::swap(c->node_rule, c->node_rule2);
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
     (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);
     return CG_OK;
