@@ -125,8 +125,11 @@ def main():
                     help="config2/config4: advance T0 (and T1) by this many seconds every step, as a "
                          "scheduler's consecutive windows (0 = the same window every step)")
     ap.add_argument("--time-order", action="store_true",
-                    help="pernode/config3: every window's per-node lists are also reordered by (time, "
-                         "rule) on the device (cg_node_result_order_by_time; timed)")
+                    help="pernode/config3: every window's per-node lists in (time, rule) order "
+                         "(cg_set_node_order(TIME): the order pass inside every per-node call, pipelined)")
+    ap.add_argument("--order-pass", action="store_true",
+                    help="with --time-order: rule-major lists reordered afterwards by "
+                         "cg_node_result_order_by_time (the separate pass; synchronous windows)")
     ap.add_argument("--diagnostic", action="store_true",
                     help="allow the diagnostic library / CG_WRITE_* CG_NODE_* switches (the line is "
                          "then marked diagnostic and is not a headline)")
@@ -376,7 +379,9 @@ def main():
     # per-node windows pipelined (cg_expand_per_node_rules_device_async) after
     # a synchronous warmup step sized the outputs; the time-order pass and the
     # gather need every window's result, so they keep synchronous windows
-    pn_pipelined = pn and not args.sync and not args.time_order and not args.gather_node_csr
+    pn_pipelined = pn and not args.sync and not args.order_pass and not args.gather_node_csr
+    if pn and args.time_order and not args.order_pass:
+        eng.set_node_order(_cg.NODE_ORDER_TIME)
     if pn_pipelined and args.warmup < 1:
         args.warmup = 1
     if lean:
@@ -628,9 +633,13 @@ def main():
         # call, plus the transpose on a call that rebuilds the join
         out["kernel_ms"].update({"rule_node_join": nkt[0], "segments_and_offsets": nkt[1],
                                  "node_write": nkt[2]})
-        if args.time_order:  # (time, rule) reorder of every node's list, per step
+        if args.time_order:  # (time, rule) order of every node's list
             out["kernel_ms"]["time_order"] = last["order_ms"] / args.steps
             out["config"]["per_node_order"] = "(time, rule) within every node (cron.go:64-79 byTime)"
+            out["config"]["time_order_by"] = ("cg_node_result_order_by_time after the rule-major writer"
+                                              if args.order_pass else
+                                              "cg_set_node_order(TIME): the pass inside every (pipelined) "
+                                              "per-node call")
         out["config"]["nnz_rule_node_pairs"] = last["nnz"]
         if args.gather_node_csr and world > 1:
             out["config"]["gathered_per_node_csr_on_rank0_events"] = last.get("gathered_events")

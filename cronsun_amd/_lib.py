@@ -31,6 +31,7 @@ PARSE_DEFAULT = 1 | 2 | 4 | 8 | 16 | 64 | 128
 PARSE_STANDARD = 2 | 4 | 8 | 16 | 32 | 128
 
 EXCLUDE_NONE, EXCLUDE_RULE, EXCLUDE_CUMULATIVE = 0, 1, 2
+NODE_ORDER_RULE, NODE_ORDER_TIME = 0, 1  # cg_set_node_order
 INGEST_OK, INGEST_UNMARSHAL, INGEST_INVALID, INGEST_PANIC, INGEST_REPLACED, INGEST_UNSUPPORTED = range(6)
 
 
@@ -142,6 +143,7 @@ def _declare(L):
         "cg_expand_per_node_wait": ([vp, P(i64), P(i64)], C.c_int),
         "cg_node_result_copy_range": ([vp, i64, i64, vp, vp], C.c_int),
         "cg_node_result_order_by_time": ([vp], C.c_int),
+        "cg_set_node_order": ([vp, C.c_int], C.c_int),
         "cg_checksum_device": ([vp, vp, i64, C.c_int, i64, i64, P(u64)], C.c_int),
         "cg_fill_device": ([vp, vp, i64, C.c_int], C.c_int),
         "cg_fill_rate_device": ([vp, vp, i64, C.c_int, P(C.c_float)], C.c_int),

@@ -741,6 +741,14 @@ int cg_set_phase_timing(cg_ctx* c, int level) {
   return CG_OK;
 }
 
+int cg_set_node_order(cg_ctx* c, int order) {
+  if (!c || (order != CG_NODE_ORDER_RULE && order != CG_NODE_ORDER_TIME))
+    return cg_fail(CG_EINVAL, "cg_set_node_order: CG_NODE_ORDER_RULE or CG_NODE_ORDER_TIME");
+  std::lock_guard<std::mutex> g(c->mu);
+  c->node_order = order;
+  return CG_OK;
+}
+
 int cg_last_kernel_times(cg_ctx* c, float* ms, int n) {
   if (!c || !ms) return cg_fail(CG_EINVAL, "cg_last_kernel_times: null");
   int k = std::min(n, int(sizeof(c->kt) / sizeof(c->kt[0])));

@@ -130,6 +130,7 @@ struct PnAsyncSet {
   int64_t* res_dev = nullptr;
   hipEvent_t side_done = nullptr, written = nullptr, nw0 = nullptr, nw1 = nullptr;
   bool pending = false;
+  bool timed = false;  // the window's lists are written in (time, rule) order
   int64_t t0 = 0, t1 = 0, node_cap = 0, rm_cap = 0;
   int32_t N = 0;
   void release() {
@@ -222,7 +223,7 @@ struct cg_ctx {
   // time-order pass (cg_node_order.hip): node-aligned tiles, per-pass
   // histograms/offsets, and the second buffers of the ping-pong
   DBuf<int32_t> ts_cnt, ts_tile_node, ts_hist, node_rule2;
-  DBuf<int64_t> ts_base, ts_off, node_time2;
+  DBuf<int64_t> ts_base, ts_off, node_time2, ts_node_off;
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
@@ -233,6 +234,8 @@ struct cg_ctx {
   // the segment bounds also on the band width
   uint64_t pn_cache_serial = 0;
   int pn_cache_mode = -1;
+  int node_order = CG_NODE_ORDER_RULE;  // cg_set_node_order
+  bool pn_time_ordered = false;         // the last per-node result is in (time, rule) order
   int32_t pn_B = 0, pn_K = 0;  // rules per band, bands of the cached segment bounds (0: none)
 
   void free_all() {
@@ -257,7 +260,7 @@ struct cg_ctx {
     seg_nrec.release(); recs.release();
     rule_info.release();
     ts_cnt.release(); ts_tile_node.release(); ts_hist.release(); node_rule2.release();
-    ts_base.release(); ts_off.release(); node_time2.release();
+    ts_base.release(); ts_off.release(); node_time2.release(); ts_node_off.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);
     pn_res_host = nullptr;
     pn_res_dev = nullptr;
@@ -306,3 +309,8 @@ bool async_pending(const cg_ctx* c);
 // wait) / any pending
 int pn_async_drain(cg_ctx* c);
 bool pn_async_pending(const cg_ctx* c);  // an asynchronous expansion not yet waited for
+// time-order tile sort + merge of c->node_time / c->node_rule (windows <= 4096 s;
+// cg_node_order.hip), enqueued on st without a host sync
+int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st);
+// the time-order pass over the last (rule-major) per-node result; c->mu held
+int order_by_time_locked(cg_ctx* c);

@@ -314,12 +314,13 @@ __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ tim
                                                   const int64_t* __restrict__ tile_base,
                                                   const int64_t* __restrict__ node_off, int64_t t0,
                                                   uint16_t* __restrict__ toff_out, int32_t* __restrict__ rule_out,
-                                                  int32_t* __restrict__ pre) {
+                                                  int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles) {
   __shared__ OtRank<4> s;
   __shared__ uint32_t pk[kOtTile];
   __shared__ int32_t rl[kOtTile];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t t = blockIdx.x;
+  if (t >= *n_tiles) return;  // the grid may be an upper bound (pipelined windows)
   const TileRange r = tile_range(t, tile_node, tile_base, node_off, kOtTile);
   const int n = int(r.hi - r.lo);
   const int ebase = w * (64 * kOtItems);
@@ -701,6 +702,48 @@ int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads
 
 }  // namespace
 
+// Windows <= 4096 s: the tile sort + merge of the per-node lists in c->node_time
+// / c->node_rule (node offsets node_off[N+1] on the device), enqueued on st
+// with no host sync: buffers sized from the output capacity cap, the tile
+// kernel's grid an upper bound it trims on the device.  Used by
+// cg_node_result_order_by_time and by the per-node calls in time order
+// (pipelined windows included).
+int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st) {
+  if (N == 0 || cap == 0) return CG_OK;
+  const int64_t Tmax = cap / kOtTile + N + 1;
+  const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
+  const int64_t tab = int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre;
+  // growing a buffer frees the old one: earlier windows' kernels finish first
+  if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(Tmax) ||
+      c->ts_hist.cap < size_t(Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
+      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->scan_tmp.cap < scan_temp_bytes(N))
+    HIPCHK(hipStreamSynchronize(st));
+  int rc;
+  if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1)) || (rc = c->ts_tile_node.ensure(Tmax)) ||
+      (rc = c->ts_hist.ensure(Tmax * kOtPre)) || (rc = c->node_time2.ensure(toff_words)) ||
+      (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) ||
+      (rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N)))))
+    return rc;
+  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, node_off, N, kOtTile, c->ts_cnt.p);
+  launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
+  hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
+  uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
+  hipLaunchKernelGGL(k_ot_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
+                     c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
+                     c->ts_base.p + N);
+  unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
+  HIPCHK(hipMemsetAsync(big_n, 0, 8, st));
+  int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
+  hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
+  hipLaunchKernelGGL(k_ot_merge<kOtMergeWaves>, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
+                     c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
+                     c->node_rule.p, c->ts_off.p, big_n);
+  hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
+                     c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
+                     c->ts_off.p, big_n);
+  return cg_hip_check(hipGetLastError(), "time-order kernels");
+}
+
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   if (!c) return cg_fail(CG_EINVAL, "cg_node_result_order_by_time: null");
   std::lock_guard<std::mutex> g(c->mu);
@@ -709,9 +752,21 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   if (rc) return rc;
   if (pn_async_pending(c))
     return cg_fail(CG_EINVAL, "pipelined per-node windows pending (call cg_expand_per_node_wait first)");
+  if (c->pn_time_ordered) {  // written in (time, rule) order already
+    c->kt[12] = 0.f;
+    return CG_OK;
+  }
+  return order_by_time_locked(c);
+}
+
+int order_by_time_locked(cg_ctx* c) {
+  int rc = CG_OK;
   const int64_t En = c->pn_E;
   const int32_t N = int32_t(c->pn_N);
-  if (En == 0 || N == 0) return CG_OK;
+  if (En == 0 || N == 0) {
+    c->pn_time_ordered = true;
+    return CG_OK;
+  }
   const int64_t H = c->pn_t1 - c->pn_t0;  // time offsets in [0, H - 1]
   int bits = 0;
   while (bits < 63 && (int64_t(1) << bits) < H) bits++;
@@ -720,48 +775,28 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
 
   // windows <= 4096 s: tile sort + merge (CG_ORDER_LSD=1: the LSD passes)
   static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;
-  const bool merge = bits <= 12 && !lsd_only;
-  const int tile = merge ? kOtTile : kTsTile;
+  if (bits <= 12 && !lsd_only) {
+    (void)hipEventRecord(c->pev[0], st);
+    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, st))) return rc;
+    (void)hipEventRecord(c->pev[1], st);
+    if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+    (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);
+    c->pn_time_ordered = true;
+    return CG_OK;
+  }
   if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1))) return rc;
   if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N))))) return rc;
-  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, c->node_off.p, N, tile, c->ts_cnt.p);
+  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, c->node_off.p, N, kTsTile, c->ts_cnt.p);
   launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
   int64_t T = 0;
   if ((rc = cg_hip_check(hipMemcpyAsync(&T, c->ts_base.p + N, 8, hipMemcpyDeviceToHost, st), "tiles")) ||
       (rc = cg_hip_check(hipStreamSynchronize(st), "sync")))
     return rc;
-  if ((rc = c->ts_tile_node.ensure(T)) || (rc = c->ts_hist.ensure(T * (merge ? kOtPre : kTsDigits))) ||
-      (!merge && (rc = c->ts_off.ensure(T * kTsDigits))) || (rc = c->node_time2.ensure(En)) ||
-      (rc = c->node_rule2.ensure(En)))
+  if ((rc = c->ts_tile_node.ensure(T)) || (rc = c->ts_hist.ensure(T * kTsDigits)) ||
+      (rc = c->ts_off.ensure(T * kTsDigits)) || (rc = c->node_time2.ensure(En)) || (rc = c->node_rule2.ensure(En)))
     return rc;
   (void)hipEventRecord(c->pev[0], st);
   hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
-  if (merge) {
-    // sorted tiles as 16-bit offsets + rules in the second buffers, merged
-    // back into the result buffers
-    uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
-    hipLaunchKernelGGL(k_ot_tile, dim3(unsigned(T)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                       c->ts_tile_node.p, c->ts_base.p, c->node_off.p, c->pn_t0, toff, c->node_rule2.p,
-                       c->ts_hist.p);
-    // big-slab tasks: at most kOtSlabs per node, after one counter word
-    // (then the per-node slab tables, N x kOtPre)
-    if ((rc = c->ts_off.ensure(int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre))) return rc;
-    unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
-    if ((rc = cg_hip_check(hipMemsetAsync(big_n, 0, 8, st), "memset"))) return rc;
-    int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
-    hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
-    hipLaunchKernelGGL(k_ot_merge<kOtMergeWaves>, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
-                       c->node_rule2.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, N, c->pn_t0, slab_tab,
-                       c->node_time.p, c->node_rule.p, c->ts_off.p, big_n);
-    hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
-                       c->node_rule2.p, c->ts_base.p, c->node_off.p, c->ts_hist.p, c->pn_t0, c->node_time.p,
-                       c->node_rule.p, c->ts_off.p, big_n);
-    (void)hipEventRecord(c->pev[1], st);
-    if ((rc = cg_hip_check(hipGetLastError(), "time-order kernels"))) return rc;
-    if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
-    (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);
-    return CG_OK;
-  }
   int64_t* tin = c->node_time.p;
   int32_t* rin = c->node_rule.p;
   int64_t* tout = c->node_time2.p;
@@ -785,5 +820,6 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   }
   if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
   (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);
+  c->pn_time_ordered = true;
   return CG_OK;
 }

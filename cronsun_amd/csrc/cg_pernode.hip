@@ -899,6 +899,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   hipStream_t st = c->st;
   const bool cached = in.serial != 0 && in.serial == c->pn_cache_serial && mode == c->pn_cache_mode;
   c->pn_E = 0;  // no readable result until this call succeeds
+  c->pn_time_ordered = false;
   (void)hipEventRecord(c->pev[0], st);
   if (cached) {
     nnz = c->pn_nnz;
@@ -1025,6 +1026,9 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_cache_mode = mode;
   *n_events = En;
   *nnz_out = nnz;
+  // (time, rule) order asked for: the time-order pass inside the call
+  if (c->node_order == CG_NODE_ORDER_TIME) return order_by_time_locked(c);
+  c->kt[12] = 0.f;
   return CG_OK;
 }
 
@@ -1143,6 +1147,9 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
   const int32_t N = in.n_nodes, K = c->pn_K, B = c->pn_B;
   const int64_t R = in.n_rules, NK = int64_t(N) * K, nnz = c->pn_nnz;
   hipStream_t sc = c->st_cs, st = c->st;
+  const bool timed = c->node_order == CG_NODE_ORDER_TIME;
+  if (timed && t1 - t0 > 4096)
+    return cg_fail(CG_EINVAL, "pipelined per-node windows in time order: windows of at most 4096 s");
   bool empty = false;
   if ((rc = async_count_scan(c, a.rm, s, z, t0, t1, rm_cap, &empty))) return rc;
   if ((rc = a.times.ensure(std::max<int64_t>(rm_cap, 1))) || (rc = a.rule_info.ensure(std::max<int64_t>(R, 1))) ||
@@ -1196,11 +1203,14 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     hipLaunchKernelGGL(k_node_write<0>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), 0, st,
                        c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N, K, B,
                        node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
+    // (time, rule) order: the tile sort + merge after the writer, same stream
+    if (timed && (rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st))) return rc;
   }
   (void)hipEventRecord(a.nw1, st);
   HIPCHK(hipEventRecord(a.written, st));
   HIPCHK(hipGetLastError());
   a.pending = true;
+  a.timed = timed;
   a.t0 = t0;
   a.t1 = t1;
   a.rm_cap = rm_cap;
@@ -1235,6 +1245,7 @@ int cg_expand_per_node_wait(cg_ctx* c, int64_t* n_events, int64_t* n_events_all)
       HIPCHK(hipMemcpyAsync(c->node_off.p, a.node_off.p, (int64_t(a.N) + 1) * 8, hipMemcpyDeviceToDevice, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
       c->pn_E = En;
+      c->pn_time_ordered = a.timed;
       c->pn_N = a.N;
       c->pn_t0 = a.t0;
       c->pn_t1 = a.t1;

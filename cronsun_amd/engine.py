@@ -459,6 +459,14 @@ class Engine:
                                               rule.ctypes.data))
         return time[:count], rule[:count]
 
+    def set_node_order(self, order):
+        """Order of every node's list in later per-node calls
+        (cg_set_node_order): _lib.NODE_ORDER_RULE (rule-major, the default) or
+        _lib.NODE_ORDER_TIME ((time, rule), the byTime order of Cron.run,
+        cron.go:64-79,220: the time-order pass runs inside every per-node call,
+        pipelined windows included)."""
+        check(lib().cg_set_node_order(self._h, int(order)))
+
     def node_order_by_time(self):
         """Reorder every node's list of the last per-node result by (time,
         rule) in device memory (cg_node_result_order_by_time; the byTime order

@@ -392,6 +392,21 @@ int cg_node_result_device(cg_ctx* ctx, const int64_t** d_node_off, const int64_t
  * Later cg_node_result_* calls see the ordered lists; the node offsets are
  * unchanged.  Time of the pass: cg_last_kernel_times [12]. */
 int cg_node_result_order_by_time(cg_ctx* ctx);
+/* Order in which the per-node calls (cg_expand_per_node*, synchronous and
+ * pipelined) write every node's list:
+ *   CG_NODE_ORDER_RULE  rule-major (rules ascending, times ascending within a
+ *                       rule) -- the default, Job.Cmds' evaluation order
+ *   CG_NODE_ORDER_TIME  (time, rule): the byTime order a node's Cron keeps
+ *                       (cron.go:64-79,220): the call runs the time-order
+ *                       pass of cg_node_result_order_by_time itself, after
+ *                       the writer (the pipelined calls enqueue it behind
+ *                       each window's writer, windows of at most 4096 s; a
+ *                       longer pipelined window is refused with CG_EINVAL)
+ * cg_node_result_order_by_time on a result already in time order does
+ * nothing. */
+#define CG_NODE_ORDER_RULE 0
+#define CG_NODE_ORDER_TIME 1
+int cg_set_node_order(cg_ctx* ctx, int order);
 /* copy the last per-node result to host buffers (node_off [N+1]; time/rule
  * [n_events], cap = their capacity); any pointer may be NULL */
 int cg_node_result_copy(cg_ctx* ctx, int64_t* node_off, int64_t* time, int32_t* rule, int64_t cap);

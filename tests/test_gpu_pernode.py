@@ -143,26 +143,47 @@ def test_transpose_cache_keyed_by_rule_set_and_mode(eng):
             eng.expand_per_node(sps[name], None, a, a + 3600, rin, mode)
 
 
+def _ordered_per_node(eng, writer, scheds, zone, t0, t1, rin):
+    """The per-node result in (time, rule) order: "pass" = rule-major lists,
+    then cg_node_result_order_by_time; "direct" = cg_set_node_order(TIME)
+    (the pass inside the per-node call).  Returns the rule-major node offsets
+    and the ordered CSR."""
+    if writer == "direct":
+        eng.set_node_order(_lib.NODE_ORDER_TIME)
+        try:
+            node_off, time, rule = eng.expand_per_node(scheds, zone, t0, t1, rin, _lib.EXCLUDE_NONE)
+        finally:
+            eng.set_node_order(_lib.NODE_ORDER_RULE)
+        assert eng.node_order_by_time() == 0.0  # already ordered: nothing to do
+        return node_off, node_off, time, rule
+    node_off, time, rule = eng.expand_per_node(scheds, zone, t0, t1, rin, _lib.EXCLUDE_NONE)
+    ms = eng.node_order_by_time()
+    assert ms >= 0
+    off2, time2, rule2 = eng.node_result(rin.n_nodes, len(time))
+    return node_off, off2, time2, rule2
+
+
+@pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("zone,t0,secs", [("UTC", synth.T0_2026 + 64 * DAY, 3600), ("UTC", synth.T0_2026, 25 * 3600),
                                           ("America/New_York", 1772953200 - 12 * 3600, 24 * 3600),
                                           ("America/New_York", 1772953200 - 1800, 4096),
-                                          ("UTC", synth.T0_2026 + 7 * 3600 + 13, 61)])
-def test_per_node_time_ordered_vs_oracle(eng, zone, t0, secs):
-    """cg_node_result_order_by_time: every node's list in (time, rule) order
-    -- the byTime order of Cron.run (cron.go:64-79,220) with equal times in
-    rule order -- from the oracle's per-node lists: windows <= 4096 s by the
-    one-pass per-node counting sort (1 h, 4096 s across the NY spring-forward,
-    61 s), longer ones by 3 radix passes (24-25 h: 17-bit time offsets);
-    node offsets unchanged."""
+                                          ("UTC", synth.T0_2026 + 7 * 3600 + 13, 61),
+                                          ("UTC", synth.T0_2026 + 5 * 3600 + 59, 1)])
+def test_per_node_time_ordered_vs_oracle(eng, writer, zone, t0, secs):
+    """Every node's list in (time, rule) order -- the byTime order of Cron.run
+    (cron.go:64-79,220) with equal times in rule order -- against the
+    oracle's per-node lists.  "pass": cg_node_result_order_by_time over the
+    rule-major lists (windows <= 4096 s by the tile sort + merge, longer ones
+    by 3 radix passes); "direct": cg_set_node_order(TIME), the same passes
+    inside the per-node call (1 h, 4096 s across the NY spring-forward, 61 s,
+    1 s, 24-25 h).  Node offsets equal the rule-major ones."""
     hours = secs / 3600
     rin = synth.multi_rule_jobs(300, seed=23)
     specs = synth.spec_mix(rin.n_rules, seed=6, mix=synth.MIX_CONFIG2)
     scheds = [cron.Parse(s) for s in specs]
     t1 = t0 + secs
-    node_off, time, rule = eng.expand_per_node(scheds, product_zone(zone), t0, t1, rin, _lib.EXCLUDE_NONE)
-    ms = eng.node_order_by_time()
-    assert ms >= 0
-    off2, time2, rule2 = eng.node_result(rin.n_nodes, len(time))
+    node_off, off2, time2, rule2 = _ordered_per_node(eng, writer, scheds, product_zone(zone), t0, t1, rin)
+    time = time2
     assert np.array_equal(off2, node_off)
     arr = O.sched_array(oracle_parse_all(specs))
     eo, et = O.expand_batch(arr, t0, t1, oracle_zone(zone))
@@ -180,7 +201,7 @@ def test_per_node_time_ordered_vs_oracle(eng, zone, t0, secs):
         assert np.array_equal(time2[a:b], exp_t[order]), n
         assert np.array_equal(rule2[a:b], exp_r[order]), n
         checked += b - a
-    assert checked == len(time) > (1000 if hours >= 1 else 100)
+    assert checked == len(time) > (1000 if hours >= 1 else (100 if secs > 1 else 10))
 
 
 PROGRESSION_MIX = ["* * * * * *", "*/13 * * * * *", "@every 7s", "@every 1h", "@every 90m", "0 0 * * * *",
@@ -204,13 +225,17 @@ def progression_rules(R, n_nodes):
                    job_pause=np.zeros(R, np.uint8))
 
 
-@pytest.mark.parametrize("R,N,secs,star_every", [(1200, 3, 3600, 13), (2600, 2, 4096, 2), (64, 1, 61, 3)])
-def test_per_node_time_ordered_big_nodes(eng, R, N, secs, star_every):
+@pytest.mark.parametrize("writer", ["pass", "direct"])
+@pytest.mark.parametrize("R,N,secs,star_every", [(1200, 3, 3600, 13), (2600, 2, 4096, 2), (64, 1, 61, 3),
+                                                 (12000, 1, 120, 1)])
+def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
     """The one-pass time order on nodes far larger than one LDS chunk:
     every-second rules put > 4096 events into one 64-s slab (the slab is
     histogrammed, then stored chunk by chunk at its digits' running bases),
     and at 2600 rules on 2 nodes over 4096 s each node holds > 5 M events,
     more than 1024 tiles (portion lists in groups); 61 s: one tile per node.
+    12000 every-second rules on one node: every second holds more events than
+    a merge chunk (k_ot_big sorts the slab chunk by chunk).
     Against the oracle's lists sorted by (time, rule)."""
     specs = [PROGRESSION_MIX[0] if i % star_every == 0 else PROGRESSION_MIX[1 + i % (len(PROGRESSION_MIX) - 1)]
              for i in range(R)]
@@ -218,9 +243,7 @@ def test_per_node_time_ordered_big_nodes(eng, R, N, secs, star_every):
     scheds = [cron.Parse(s) for s in specs]
     t0 = synth.T0_2026 + 9 * DAY + 777
     t1 = t0 + secs
-    node_off, time, rule = eng.expand_per_node(scheds, product_zone("UTC"), t0, t1, rin, _lib.EXCLUDE_NONE)
-    eng.node_order_by_time()
-    off2, time2, rule2 = eng.node_result(rin.n_nodes, len(time))
+    node_off, off2, time2, rule2 = _ordered_per_node(eng, writer, scheds, product_zone("UTC"), t0, t1, rin)
     assert np.array_equal(off2, node_off)
     arr = O.sched_array(oracle_parse_all(specs))
     eo, et = O.expand_batch(arr, t0, t1, oracle_zone("UTC"))
@@ -271,18 +294,25 @@ def test_per_node_progressions_vs_oracle(eng, zone, t0):
         assert np.array_equal(rule[node_off[n]:node_off[n + 1]], exp_r), n
 
 
+@pytest.mark.parametrize("order", ["rule", "time"])
 @pytest.mark.parametrize("zone", ["UTC", "America/New_York"])
-def test_per_node_async_windows(zone):
+def test_per_node_async_windows(zone, order):
     """cg_expand_per_node_rules_device_async / cg_expand_per_node_wait: a node
     scheduler's consecutive windows (node/node.go:121-158 + cron.go:210-275),
     pipelined.  The last window's per-node CSR equals the synchronous result of
     that window and the oracle; the all-window total equals the sum of the
     windows' synchronous totals; accessors refuse while windows are pending; a
     window beyond the capacity reports CG_ECAPACITY at the wait; a synchronous
-    call in between discards pending windows."""
+    call in between discards pending windows.  order "time"
+    (cg_set_node_order): every window's tile sort + merge enqueued behind its
+    writer, the last window against the oracle's lists in (time, rule) order;
+    windows over 4096 s are refused at the call."""
     from cronsun_amd.engine import Engine
     from cronsun_amd._lib import check, lib
     e2 = Engine(0)
+    timed = order == "time"
+    if timed:
+        e2.set_node_order(_lib.NODE_ORDER_TIME)
     rin = synth.multi_rule_jobs(2000, seed=31)
     specs = synth.spec_mix(rin.n_rules, seed=9, mix=synth.MIX_CONFIG2)
     arr, status = cron.parse_batch(specs)
@@ -325,8 +355,19 @@ def test_per_node_async_windows(zone):
             assert off[n + 1] == off[n]
             continue
         exp_t, exp_r = O.node_list(eo, et, per_node[n])
+        if timed:
+            o = np.lexsort((exp_r, exp_t))
+            exp_t, exp_r = exp_t[o], exp_r[o]
         assert np.array_equal(got_t[off[n]:off[n + 1]], exp_t), n
         assert np.array_equal(got_r[off[n]:off[n + 1]], exp_r), n
+    if timed:
+        with pytest.raises(_lib.CgError) as err:
+            e2.expand_per_node_async(sp, z, t0, t0 + 2 * DAY, dr, _lib.EXCLUDE_NONE)
+        assert err.value.code == _lib.CG_EINVAL
+        dr.free()
+        sp.free()
+        e2.close()
+        return
     # a window far beyond the capacity: CG_ECAPACITY at the wait
     e2.expand_per_node_async(sp, z, t0, t0 + 2 * DAY, dr, _lib.EXCLUDE_NONE)
     with pytest.raises(_lib.CgError) as err:
