@@ -300,21 +300,16 @@ def main():
             wake["wakes"] += 1
             return n_due
         if pn and pn_pipelined and last.get("pn_sized"):
-            # pipelined windows: window k+1's expansion and records overlap
-            # window k's per-node writer; one wait per step (the node events
-            # of every window come with it)
+            # pipelined windows, enqueued: window k+1's expansion and records
+            # overlap window k's per-node writer, across steps too (a tick
+            # loop); finish() waits once (the node events of every window come
+            # with it)
             wins = list(range(t0, t1, W))
             for a in wins:
                 eng.expand_per_node_async(sp, utc, a, min(a + W, t1), drules, xmode)
-            En_w, En = eng.expand_per_node_wait(with_total=True)
-            last["En_last"] = En_w
-            nk = eng.node_kernel_times()
-            last.update(kt=np.array(last["kt_sync"]), windows=len(wins),
-                        nkt=np.array([last["nkt_sync"][0], last["nkt_sync"][1], nk[2] * len(wins)]))
-            if world > 1:  # per-node offsets of every rank's slice of the last window
-                eng.node_counts_to_device(node_counts.data_ptr())
-                shard.node_offsets(node_counts.to(cdev), dist)
-            return En
+            last["pending_steps"] = last.get("pending_steps", 0) + 1
+            last["windows"] = len(wins)
+            return None
         if pn:
             En = 0
             kt_sum = np.zeros(6)
@@ -362,7 +357,20 @@ def main():
 
     def finish():
         """End of a run of steps: drain the pipeline (pipelined mode); at N > 1
-        one allgather of the ranks' totals gives the shards' global offsets."""
+        one allgather of the ranks' totals gives the shards' global offsets
+        (per-node: of every rank's per-node counts of the last window).
+        Returns the events of one step."""
+        if pn and pn_pipelined and last.get("pending_steps"):
+            En_w, En = eng.expand_per_node_wait(with_total=True)
+            k = last.pop("pending_steps")
+            last["En_last"] = En_w
+            nk = eng.node_kernel_times()
+            last.update(kt=np.array(last["kt_sync"]),
+                        nkt=np.array([last["nkt_sync"][0], last["nkt_sync"][1], nk[2] * last["windows"]]))
+            if world > 1:
+                eng.node_counts_to_device(node_counts.data_ptr())
+                shard.node_offsets(node_counts.to(cdev), dist)
+            return En // k
         if not pipelined:
             return None
         E = eng.expand_wait()
@@ -390,8 +398,8 @@ def main():
         eng.expand_device(sp, utc, t0, t1 + args.tick * (args.warmup + args.steps + 8))
     for _ in range(args.warmup):
         E = step()
-    if pipelined:
-        E = finish()
+    if pipelined or pn_pipelined:
+        E = finish() or E
     log(f"[rank {rank}] warmup done: {E} events/step ({'pipelined' if pipelined else 'synchronous'} steps)")
     if not pn and wl != "dispatch":
         _, d_times, _ = eng.result_device()
@@ -419,13 +427,17 @@ def main():
         ts = time.perf_counter()
         E = step()
         step_wall.append(time.perf_counter() - ts)
-        if pn:
+        if pn and not pn_pipelined:
             kts.append(last["kt"])
             nkts.append(last["nkt"])
-        elif not pipelined:
+        elif not pipelined and not pn:
             kts.append(eng.kernel_times())
             nkts.append(eng.dispatch_kernel_times() if wl == "dispatch" else eng.node_kernel_times())
-    if pipelined:  # inside the timed region: every step's work is done and checked
+    if pn_pipelined:  # inside the timed region: every window is done and checked
+        E = finish()
+        kts.append(last["kt"])
+        nkts.append(last["nkt"])
+    elif pipelined:  # inside the timed region: every step's work is done and checked
         E = finish()
         kts.append(eng.kernel_times())  # [3] = mean k_write_cf time of the timed steps
         nkts.append(eng.node_kernel_times())
@@ -598,7 +610,8 @@ def main():
                        "step's write; one cg_expand_wait at the end of the timed steps)" if pipelined else
                        "synchronous (one call and stream sync per step)") if lean else
                       ("pipelined per-node windows (cg_expand_per_node_rules_device_async: a window's "
-                       "expansion and records overlap the previous window's writer; one wait per step; "
+                       "expansion and records overlap the previous window's writer, across steps; one "
+                       "cg_expand_per_node_wait at the end of the timed steps; "
                        "per-phase times from the synchronous warmup step, node_write from the timed steps)"
                        if pn_pipelined else "synchronous"),
         "kernel_ms": {"count": kt[0], "scan": kt[1], "block_map": kt[2], "write_cf": kt[3],

@@ -1170,8 +1170,9 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     const int64_t nruns = R * int64_t(pa.G);
     // a quarter of the persistent writer grid: the window's rule-major fires
     // are few, and the previous window's per-node writer keeps the CUs
+    constexpr int side_div = 4;
     launch_write_cf(s->d, pa, a.rm.run_anchor.p, a.rm.run_count.p, a.rm.run_dmask.p, a.rm.run_off.p, nruns,
-                    a.rm.block_run.p, rm_cap, a.times.p, std::max(1, c->write_blocks / 4), sc);
+                    a.rm.block_run.p, rm_cap, a.times.p, std::max(1, c->write_blocks / side_div), sc);
     if ((a.rm.plan.flags & (kPlanT0Walk | kPlanWalkSegs)) != 0)
       launch_write_walk(s->d, R, pa, a.rm.run_anchor.p, a.rm.run_count.p, a.rm.run_dmask.p, a.rm.run_off.p, rm_cap,
                         a.times.p, sc);
