@@ -86,7 +86,7 @@ def store_ceiling(eng, nbytes, dev, achieved_gbps, reps=5):
     torch.cuda.empty_cache()
     rates = {k: nbytes / v / 1e6 for k, v in ms.items() if v > 0}
     best = max(rates, key=rates.get)
-    return {"kind": "fastest of k_fill_stream (16 B/lane nt | plain stores, full occupancy, one launch) and "
+    return {"kind": "fastest of k_fill_stream (16 B/lane nt | plain stores, one 4-wave block per CU, one launch) and "
                     "hipMemsetAsync over the kernel's output bytes", "bytes": nbytes,
             "ms": ms, "GBps": rates, "best": best, "best_GBps": rates[best],
             "frac_of_ceiling": achieved_gbps / rates[best]}

@@ -890,7 +890,10 @@ void launch_fill_stream(void* p, int64_t n16, int nt, hipStream_t st) {
   if (n16 <= 0) return;
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int grid = grid_for((n16 + 3) / 4, 256, cus * 8);  // 8 blocks of 4 waves per CU: full occupancy
+  // one 4-wave block per CU: the fastest plain streaming fill on this part
+  // (profiles/r03_fill_patterns_box*.jsonl: 6.3-6.5 TB/s, the rate of
+  // hipMemsetAsync; 2-8 blocks per CU 5.2-5.7 TB/s)
+  const int grid = grid_for((n16 + 3) / 4, 256, cus);
   if (nt)
     hipLaunchKernelGGL(k_fill_stream<true>, dim3(grid), dim3(256), 0, st, static_cast<v4i32*>(p), n16);
   else
