@@ -357,17 +357,20 @@ func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, 
 	coff := (*C.int64_t)(C.malloc(C.size_t(nn+1) * 8))
 	defer C.free(unsafe.Pointer(coff))
 	out.node_off = coff
+	// byTime: the call itself leaves every node's list in (time, rule) order
+	order := C.int(C.CG_NODE_ORDER_RULE)
+	if byTime {
+		order = C.int(C.CG_NODE_ORDER_TIME)
+	}
+	if rc := C.cg_set_node_order(e.ctx, order); rc != 0 {
+		return nil, lastErr(rc)
+	}
 	if rc := C.cg_expand_per_node(e.ctx, sp.s, z.z, C.int64_t(t0.Unix()), C.int64_t(t1.Unix()), &rin,
 		C.int(mode), out); rc != 0 {
 		return nil, lastErr(rc)
 	}
 	nodeOff := make([]int64, nn+1)
 	copy(nodeOff, unsafe.Slice((*int64)(unsafe.Pointer(coff)), nn+1))
-	if byTime {
-		if rc := C.cg_node_result_order_by_time(e.ctx); rc != 0 {
-			return nil, lastErr(rc)
-		}
-	}
 	tm, rl := make([]int64, int64(out.n_events)), make([]int32, int64(out.n_events))
 	if len(tm) > 0 {
 		if rc := C.cg_node_result_copy(e.ctx, nil, (*C.int64_t)(unsafe.Pointer(&tm[0])),
