@@ -225,30 +225,26 @@ struct OtRank {
 
 // Stable positions of the n valid items (item j of wave w, lane l = element
 // w*64*kOtItems + j*64 + l) by the digit dg[j] < 64: earlier elements with
-// the same digit keep their order.  Ends synchronised.
+// the same digit keep their order.  The rank inside the wave is the value an
+// LDS atomic add on the digit's counter returns: a wave's LDS operations
+// complete in program order, and the lanes of one ds_add_rtn that hit the
+// same address are served in ascending lane order on gfx950
+// (tools/lds_atomic_order.hip: 0 of 6.3 M ranks out of order over random and
+// adversarial digit patterns; the GPU tests check every ordered list against
+// the oracle's).  It replaces a 6-ballot multisplit per element (~40 VALU
+// instructions; the sorts were VALU-bound, profiles/r03_ab_time_order.json).
+// Ends synchronised.
 template <int NW>
 __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, int32_t (&pos)[kOtItems],
                                         OtRank<NW>& s) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  s.run[w][lane] = 0;
+  uint32_t* run = reinterpret_cast<uint32_t*>(s.run[w]);
+  run[lane] = 0;
   const int ebase = w * (64 * kOtItems);
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const bool valid = ebase + j * 64 + lane < n;
-    const uint32_t d = dg[j];
-    uint64_t peers = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 6; b++) {
-      const bool bit = (d >> b) & 1u;
-      const uint64_t m = __ballot(bit);
-      peers &= bit ? m : ~m;
-    }
-    // every lane reads the running count before the group's first lane adds
-    // the group size (a wave's LDS operations complete in program order)
-    const int32_t r0 = s.run[w][d];
-    pos[j] = r0 + __popcll(peers & lt);
-    if (valid && (peers & lt) == 0) s.run[w][d] = r0 + __popcll(peers);
+    pos[j] = valid ? int32_t(atomicAdd(run + dg[j], 1u)) : 0;
   }
   ot_sync<NW>();
   if (threadIdx.x < 64) {
