@@ -390,8 +390,10 @@ def main():
     pn_pipelined = pn and not args.sync and not args.order_pass and not args.gather_node_csr
     if pn and args.time_order and not args.order_pass:
         eng.set_node_order(_cg.NODE_ORDER_TIME)
-    if pn_pipelined and args.warmup < 1:
-        args.warmup = 1
+    if pn_pipelined and args.warmup < 4:
+        # one synchronous step sizes the outputs, then one pipelined step per
+        # window set (3) so no set allocates its buffers inside the timed steps
+        args.warmup = 4
     if lean:
         eng.set_phase_timing(1)
     if pipelined:  # a synchronous call sizes the output for the pipelined ones

@@ -311,6 +311,8 @@ int pn_async_drain(cg_ctx* c);
 bool pn_async_pending(const cg_ctx* c);  // an asynchronous expansion not yet waited for
 // time-order tile sort + merge of c->node_time / c->node_rule (windows <= 4096 s;
 // cg_node_order.hip), enqueued on st without a host sync
-int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st);
+// (in16: the lists' times are 16-bit offsets t - t0 - 1, written by k_node_write<.., true>)
+int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
+                        bool in16);
 // the time-order pass over the last (rule-major) per-node result; c->mu held
-int order_by_time_locked(cg_ctx* c);
+int order_by_time_locked(cg_ctx* c, bool in16 = false);

@@ -305,6 +305,7 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, bool f
   ot_sync<NW>();
 }
 
+template <bool IN16>  // times as 16-bit offsets t - t0 - 1 (else int64 times, their low words read)
 __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ time, const int32_t* __restrict__ rule,
                                                   const int32_t* __restrict__ tile_node,
                                                   const int64_t* __restrict__ tile_base,
@@ -328,7 +329,8 @@ __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ tim
   for (int j = 0; j < kOtItems; j++) {  // every load issued before any is used
     const int e = ebase + j * 64 + lane;
     const int64_t i = r.lo + (e < n ? e : n - 1);
-    tv[j] = tlo[2 * i];
+    if constexpr (IN16) tv[j] = uint32_t(reinterpret_cast<const uint16_t*>(time)[i]) + b;
+    else tv[j] = tlo[2 * i];
     rv[j] = rule[i];
   }
 #pragma unroll
@@ -704,7 +706,8 @@ int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads
 // kernel's grid an upper bound it trims on the device.  Used by
 // cg_node_result_order_by_time and by the per-node calls in time order
 // (pipelined windows included).
-int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st) {
+int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
+                        bool in16) {
   if (N == 0 || cap == 0) return CG_OK;
   const int64_t Tmax = cap / kOtTile + N + 1;
   const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
@@ -724,9 +727,14 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
   hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
   uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
-  hipLaunchKernelGGL(k_ot_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                     c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
-                     c->ts_base.p + N);
+  if (in16)
+    hipLaunchKernelGGL(k_ot_tile<true>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
+                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
+                       c->ts_base.p + N);
+  else
+    hipLaunchKernelGGL(k_ot_tile<false>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
+                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
+                       c->ts_base.p + N);
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
   HIPCHK(hipMemsetAsync(big_n, 0, 8, st));
   int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
@@ -755,7 +763,7 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   return order_by_time_locked(c);
 }
 
-int order_by_time_locked(cg_ctx* c) {
+int order_by_time_locked(cg_ctx* c, bool in16) {
   int rc = CG_OK;
   const int64_t En = c->pn_E;
   const int32_t N = int32_t(c->pn_N);
@@ -773,7 +781,7 @@ int order_by_time_locked(cg_ctx* c) {
   static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;
   if (bits <= 12 && !lsd_only) {
     (void)hipEventRecord(c->pev[0], st);
-    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, st))) return rc;
+    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, st, in16))) return rc;
     (void)hipEventRecord(c->pev[1], st);
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
     (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);

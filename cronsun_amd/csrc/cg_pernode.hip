@@ -521,7 +521,9 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 }
 constexpr int kNodeMajorDefault = 0;  // writer task order: 0 band-major, 1 node-major
 
-template <int V>
+// OFF16: the times go out as 16-bit offsets t - t0 - 1 (windows <= 4096 s
+// whose lists the time-order tile sort reads next: 2 B per event instead of 8)
+template <int V, bool OFF16 = false>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
     const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, int64_t t0,
@@ -575,7 +577,12 @@ __global__ __launch_bounds__(256) void k_node_write(
     const int32_t q_lo = int32_t(o0 - abase), q_hi = q_lo + int32_t(o1 - o0);
     const int64_t* __restrict__ tb = times + band_lo;
     int64_t* __restrict__ ot = out_time + abase;
+    uint16_t* __restrict__ o16 = reinterpret_cast<uint16_t*>(out_time) + abase;
     int32_t* __restrict__ orl = out_rule + abase;
+    auto put_time = [&](int32_t q, int64_t val) {
+      if constexpr (OFF16) out_store<V>(o16 + q, uint16_t(val - t0 - 1));
+      else out_store<V>(ot + q, val);
+    };
     int32_t pq = -1, prule = 0;  // a block carried into the next chunk
     int64_t ptime = 0;
     // records in chunks of 64 (lane i: record i), the next chunk in flight
@@ -624,7 +631,7 @@ __global__ __launch_bounds__(256) void k_node_write(
         }
         if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
           if ((b >= q_lo && b + 64 <= q_hi) || (q >= q_lo && q < q_hi)) {  // whole, or a segment edge
-            out_store<V>(ot + q, val);
+            put_time(q, val);
             if (!(V & 8)) out_store<V>(orl + q, rv);
           }
           pq = -1;
@@ -651,7 +658,7 @@ __global__ __launch_bounds__(256) void k_node_write(
           int64_t val = t0 + int64_t(dl) + int64_t(b + lane - q_lo) * sv;
           const int64_t step = int64_t(64) * sv;
           for (; b < bend; b += 64, val += step) {
-            out_store<V>(ot + b + lane, val);
+            put_time(b + lane, val);
             if (!(V & 8)) out_store<V>(orl + b + lane, rv);
           }
         } else {
@@ -659,7 +666,7 @@ __global__ __launch_bounds__(256) void k_node_write(
             const int32_t gi = b + lane + dl - q_lo;
             int64_t val = (V & 1) ? int64_t(gi) : tb[gi];
             asm volatile("" : "+v"(val));
-            out_store<V>(ot + b + lane, val);
+            put_time(b + lane, val);
             if (!(V & 8)) out_store<V>(orl + b + lane, rv);
           }
         }
@@ -983,16 +990,22 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   static const int per_cu = node_write_blocks_per_cu();
 #endif
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
+  // (time, rule) order of a window <= 4096 s: 16-bit offsets for the tile sort
+  const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0;
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
     if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
-  hipLaunchKernelGGL(k_node_write<V>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
+  hipLaunchKernelGGL((k_node_write<V, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
                      0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,      \
                      c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p,     \
                      c->node_rule.p, node_major)
-      switch (variant) {
+      if (off16) {
+        hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
+                           0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p, c->times.p,
+                           N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
+      } else switch (variant) {
         case 1: CG_NW(1); break;
         case 2: CG_NW(2); break;
         case 3: CG_NW(3); break;
@@ -1027,7 +1040,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   *n_events = En;
   *nnz_out = nnz;
   // (time, rule) order asked for: the time-order pass inside the call
-  if (c->node_order == CG_NODE_ORDER_TIME) return order_by_time_locked(c);
+  if (c->node_order == CG_NODE_ORDER_TIME) return order_by_time_locked(c, off16);
   c->kt[12] = 0.f;
   return CG_OK;
 }
@@ -1201,11 +1214,16 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     // wave slots beside this writer instead of waiting for it to retire
     static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-    hipLaunchKernelGGL(k_node_write<0>, dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), 0, st,
+    if (timed)
+      hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
+                         0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
+                         K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
+    else
+    hipLaunchKernelGGL((k_node_write<0, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), 0, st,
                        c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N, K, B,
                        node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
     // (time, rule) order: the tile sort + merge after the writer, same stream
-    if (timed && (rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st))) return rc;
+    if (timed && (rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st, true))) return rc;
   }
   (void)hipEventRecord(a.nw1, st);
   HIPCHK(hipEventRecord(a.written, st));
