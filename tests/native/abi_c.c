@@ -228,6 +228,17 @@ int main(int argc, char** argv) {
     for (int64_t k = node_off[n]; k < node_off[n + 1]; k++) printf(" %d:%lld", nr[k], (long long)nt[k]);
     printf("\n");
   }
+  /* ... and written in that order by the per-node call itself (the cgo
+     stub's ExpandPerNode with byTime) */
+  CHECK(cg_set_node_order(ctx, CG_NODE_ORDER_TIME));
+  CHECK(cg_expand_per_node(ctx, sp, ny, t0, t1, &rules, CG_EXCLUDE_NONE, &nc));
+  CHECK(cg_node_result_copy(ctx, NULL, nt, nr, nc.n_events));
+  CHECK(cg_set_node_order(ctx, CG_NODE_ORDER_RULE));
+  for (int n = 0; n < rules.n_nodes; n++) {
+    printf("Q %s", cg_jobset_node_id(js, n));
+    for (int64_t k = node_off[n]; k < node_off[n + 1]; k++) printf(" %d:%lld", nr[k], (long long)nt[k]);
+    printf("\n");
+  }
   free(nt);
   free(nr);
 

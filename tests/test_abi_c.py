@@ -93,6 +93,7 @@ def test_call_sequence_matches_oracle(abi_c):
     roff, rules = O.node_rules(rin, 0, np.arange(len(nodes)))
     got = {ln.split(" ", 1)[0]: ln.split(" ")[1:] for ln in lines["L"]}
     got_o = {ln.split(" ", 1)[0]: ln.split(" ")[1:] for ln in lines["O"]}
+    got_q = {ln.split(" ", 1)[0]: ln.split(" ")[1:] for ln in lines["Q"]}  # cg_set_node_order(TIME)
     for k, name in enumerate(nodes):
         exp_t, exp_r = O.node_list(eo, et, rules[roff[k]:roff[k + 1]])
         want = [f"{r}:{t}" for r, t in zip(exp_r.tolist(), exp_t.tolist())]
@@ -100,6 +101,7 @@ def test_call_sequence_matches_oracle(abi_c):
         o = np.lexsort((exp_r, exp_t))  # byTime, equal times in rule order
         want_o = [f"{r}:{t}" for r, t in zip(exp_r[o].tolist(), exp_t[o].tolist())]
         assert [x for x in got_o.get(name, []) if x] == want_o, name
+        assert [x for x in got_q.get(name, []) if x] == want_o, name
     kind = [i % 3 for i in range(R)]
     avg = [1000 * i - 2500 for i in range(R)]
     assert [int(x) for x in lines["K"][0].split()] == [
