@@ -563,26 +563,35 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restr
   for (int j = threadIdx.x; j <= kOtSlabs; j += kThreads) slab_off[j] = slab_tab[int64_t(n) * kOtPre + j];
   ot_sync<NW>();
   uint32_t key[kOtItems];
-  int ja = 0;
+  // the longest run of whole slabs [j0, j1) that fits one chunk (j1 == j0: a
+  // slab of more than a chunk)
+  auto run_end = [&](int j0) {
+    int j1 = j0;
+    while (j1 < kOtSlabs && slab_off[j1 + 1] - slab_off[j0] <= kChunk) j1++;
+    return j1;
+  };
+  // thread q owns tile q (M <= kOtMaxTiles <= threads): its slab prefix at the
+  // run's ends is held in registers, the next run's end loaded one run ahead
+  static_assert(kOtMaxTiles <= kThreads, "one tile per thread");
+  const int q_own = threadIdx.x;
+  const int32_t* __restrict__ pq = pre + (ta + (q_own < M ? q_own : 0)) * kOtPre;
+  int ja = 0, jb = run_end(0);
+  int32_t pa = pq[0], pb = pq[jb];
   while (ja < kOtSlabs) {
-    // the longest run of whole slabs [ja, jb) that fits one chunk
-    int jb = ja;
-    while (jb < kOtSlabs && slab_off[jb + 1] - slab_off[ja] <= kChunk) jb++;
+    const int ja2 = jb == ja ? ja + 1 : jb;
+    const int jb2 = ja2 < kOtSlabs ? run_end(ja2) : ja2;
+    const int32_t pa2 = jb == ja ? pq[ja2 <= kOtSlabs ? ja2 : kOtSlabs] : pb;
+    const int32_t pb2 = pq[jb2 <= kOtSlabs ? jb2 : kOtSlabs];  // in flight while this run is merged
     if (jb == ja) {  // one slab of more than a chunk
       if (threadIdx.x == 0) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | ja;
-      ja++;
-      continue;
-    }
-    const int n_el = int(slab_off[jb] - slab_off[ja]);
-    if (n_el > 0) {
+    } else if (slab_off[jb] > slab_off[ja]) {
+      const int n_el = int(slab_off[jb] - slab_off[ja]);
       // per tile its sorted events of slabs [ja, jb): one contiguous range
       ot_portions<NW>(
           int(M),
           [&](int q, int32_t* src) {
-            const int32_t* pt = pre + (ta + q) * kOtPre;
-            const int32_t a = pt[ja];
-            *src = q * kOtTile + a;
-            return pt[jb] - a;
+            *src = q * kOtTile + pa;  // q == q_own
+            return pb - pa;
           },
           ps, psrc, wsum);
       ot_owners<NW>(ps, int(M), 0, n_el, own, wsum);
@@ -596,7 +605,10 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restr
       }
       ot_sync<NW>();
     }
-    ja = jb;
+    ja = ja2;
+    jb = jb2;
+    pa = pa2;
+    pb = pb2;
   }
 }
 
