@@ -95,7 +95,7 @@ def store_ceiling(eng, nbytes, dev, achieved_gbps, reps=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["config2", "pernode", "config3", "config4", "dispatch", "parse"],
                     default="config2")
