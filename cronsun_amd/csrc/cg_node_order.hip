@@ -171,24 +171,27 @@ __global__ __launch_bounds__(256) void k_ts_scatter(const int64_t* __restrict__ 
 // ---- windows <= 4096 s (12-bit time offsets): tile sort + per-node merge ----
 //
 //   k_ot_tile   per tile (<= kOtTile events of one node, rule-major): a
-//               stable LDS counting sort by the time offset (two 6-bit
-//               passes over packed (offset << 12 | index) words), the tile
-//               written back in (time, rule) order with coalesced stores, and
-//               its slab prefix pre[t][0..256] (slab = offset >> 4: 16 s)
-//   k_ot_merge  one wave per node (many independent nodes in flight): runs
-//               of whole slabs holding <= kOtChunk1 events are gathered from
-//               every tile (one contiguous range per tile: its sorted events
-//               of those slabs; tile order = rule order), sorted by offset in
-//               LDS (one pass over the low 4 bits for a single slab) and
-//               stored contiguously; a larger slab, or every slab of a node
-//               of more than kOtMaxTiles tiles, is queued for k_ot_big
-//   k_ot_big    per queued slab: the histogram of its 16 seconds over all its
+//               stable LDS counting partition of packed (offset << 12 |
+//               index) words by slab (offset >> 6: 64 s; one 6-bit pass), the
+//               tile written back slab by slab with coalesced stores, and its
+//               slab prefix pre[t][0..64].  A node of one tile is sorted by
+//               the whole offset instead (a second pass) and is done.
+//   k_ot_merge  one workgroup per node: runs of whole slabs holding <= a
+//               chunk are gathered from every tile (one contiguous range per
+//               tile: its events of those slabs, in rule order; tile order =
+//               rule order), sorted by offset - the run's first second in LDS
+//               (one 8-bit pass for a run of <= 4 slabs) and stored
+//               contiguously; a larger slab, or every slab of a node of more
+//               than kOtMaxTiles tiles, is queued for k_ot_big
+//   k_ot_big    per queued slab: the histogram of its 64 seconds over all its
 //               portions, then its chunks in order, each sorted in LDS and
 //               stored at its seconds' running bases
-// The sorted tiles are kept as 16-bit offsets + rules (6 B per event), so
-// the two passes move 12 + 6 + 6 + 12 = 36 B per event, every store
-// coalesced, where the LSD passes above scatter each event to its own
-// address per pass and read the times again for every histogram.
+// Every sort is stable and the gathered order is (tile, rule order inside
+// the tile), so equal seconds stay in rule order.  The partitioned tiles are
+// kept as 16-bit offsets + rules (6 B per event), so the two passes move
+// 12 + 6 + 6 + 12 = 36 B per event, every store coalesced, where the LSD
+// passes above scatter each event to its own address per pass and read the
+// times again for every histogram.
 constexpr int kOtItems = 16;                  // per thread
 constexpr int kOtTile = 4 * 64 * kOtItems;    // 4096 events: the tile sort's 4-wave chunk
 #ifndef CG_OT_MERGE_WAVES
@@ -197,10 +200,7 @@ constexpr int kOtTile = 4 * 64 * kOtItems;    // 4096 events: the tile sort's 4-
 constexpr int kOtMergeWaves = CG_OT_MERGE_WAVES;  // k_ot_merge: waves per node
 constexpr int kOtIdxBits = 12;                // chunk index bits of a packed word
 constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
-#ifndef CG_OT_SLAB_BITS
-#define CG_OT_SLAB_BITS 6
-#endif
-constexpr int kOtSlabBits = CG_OT_SLAB_BITS;  // slab = offset >> kOtSlabBits (64 s)
+constexpr int kOtSlabBits = 6;               // slab = offset >> kOtSlabBits (64 s): one 6-bit digit
 constexpr int kOtSlabs = 4096 >> kOtSlabBits;
 constexpr int kOtPre = kOtSlabs + 1;          // pre row per tile
 constexpr int kOtMaxTiles = 256;              // portion list capacity
@@ -216,15 +216,14 @@ __device__ __forceinline__ void ot_sync() {
   }
 }
 
-template <int NW>
+template <int NW, int D>  // D digits: 64 or 256
 struct OtRank {
-  int32_t run[NW][64];   // per wave: events of each digit so far
-  int32_t base[NW][64];  // per wave: first position of its events of each digit
-  int32_t dbase[65];     // exclusive prefix of the digit totals; [64] = events
+  int32_t run[NW][D];  // per wave: its events of each digit, then their first position
+  int32_t dbase[65];   // D == 64: exclusive prefix of the digit totals; [64] = events
 };
 
 // Stable positions of the n valid items (item j of wave w, lane l = element
-// w*64*kOtItems + j*64 + l) by the digit dg[j] < 64: earlier elements with
+// w*64*kOtItems + j*64 + l) by the digit dg[j] < D: earlier elements with
 // the same digit keep their order.  The rank inside the wave is the value an
 // LDS atomic add on the digit's counter returns: a wave's LDS operations
 // complete in program order, and the lanes of one ds_add_rtn that hit the
@@ -233,72 +232,103 @@ struct OtRank {
 // adversarial digit patterns; the GPU tests check every ordered list against
 // the oracle's).  It replaces a 6-ballot multisplit per element (~40 VALU
 // instructions; the sorts were VALU-bound, profiles/r03_ab_time_order.json).
-// Ends synchronised.
-template <int NW>
+// Each wave only touches its own counter row outside the two barriers.
+// RUNS: lanes holding the same digit as their left neighbour join its run and
+// only the run's first lane adds (the run's length): a digit shared by long
+// runs of neighbouring elements (slabs of a rule-major tile: one rule's
+// events sit in neighbouring seconds) would otherwise serialise its lanes on
+// one LDS address.  Ends synchronised.
+template <int NW, int D, bool RUNS = false>
 __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, int32_t (&pos)[kOtItems],
-                                        OtRank<NW>& s) {
+                                        OtRank<NW, D>& s) {
+  static_assert(D == 64 || D == 256, "digits");
+  constexpr int P = D / 64;  // digits per lane in the scan
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint32_t* run = reinterpret_cast<uint32_t*>(s.run[w]);
-  run[lane] = 0;
+#pragma unroll
+  for (int i = 0; i < P; i++) run[lane + 64 * i] = 0;
   const int ebase = w * (64 * kOtItems);
+  const uint64_t upto = ~0ull >> (63 - lane);  // lanes 0 .. lane
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const bool valid = ebase + j * 64 + lane < n;
-    pos[j] = valid ? int32_t(atomicAdd(run + dg[j], 1u)) : 0;
+    if constexpr (RUNS) {
+      const uint32_t d = valid ? dg[j] : uint32_t(D);  // invalid lanes (the tail) add nothing
+      const uint32_t left = __shfl_up(d, 1, 64);
+      const bool head = lane == 0 || left != d;
+      const uint64_t hm = __ballot(head);
+      const int h = 63 - __builtin_clzll(hm & upto);  // this lane's run starts at lane h
+      const uint64_t after = hm & ~upto;
+      const int end = after ? __builtin_ctzll(after) : 64;
+      uint32_t r = 0;
+      if (head && valid) r = atomicAdd(run + d, uint32_t(end - lane));
+      r = __shfl(r, h, 64);
+      pos[j] = valid ? int32_t(r) + (lane - h) : 0;
+    } else {
+      pos[j] = valid ? int32_t(atomicAdd(run + dg[j], 1u)) : 0;
+    }
   }
   ot_sync<NW>();
-  if (threadIdx.x < 64) {
-    const int d = threadIdx.x;
-    int32_t tot = 0;
+  if (threadIdx.x < 64) {  // lane d: digits d*P .. d*P + P - 1
+    const int d0 = threadIdx.x * P;
+    int32_t r[P][NW], sum = 0;
 #pragma unroll
-    for (int ww = 0; ww < NW; ww++) tot += s.run[ww][d];
-    int32_t inc = tot;
+    for (int i = 0; i < P; i++)
+#pragma unroll
+      for (int ww = 0; ww < NW; ww++) {
+        r[i][ww] = s.run[ww][d0 + i];
+        sum += r[i][ww];
+      }
+    int32_t inc = sum;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const int32_t y = __shfl_up(inc, o, 64);
-      if (d >= o) inc += y;
+      if (threadIdx.x >= o) inc += y;
     }
-    int32_t acc = inc - tot;
-    s.dbase[d] = acc;
-    if (d == 63) s.dbase[64] = inc;
+    int32_t acc = inc - sum;
+    if constexpr (D == 64) {
+      s.dbase[d0] = acc;
+      if (d0 == 63) s.dbase[64] = inc;
+    }
 #pragma unroll
-    for (int ww = 0; ww < NW; ww++) {
-      s.base[ww][d] = acc;
-      acc += s.run[ww][d];
-    }
+    for (int i = 0; i < P; i++)
+#pragma unroll
+      for (int ww = 0; ww < NW; ww++) {
+        s.run[ww][d0 + i] = acc;
+        acc += r[i][ww];
+      }
   }
   ot_sync<NW>();
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) pos[j] += s.base[w][dg[j]];
+  for (int j = 0; j < kOtItems; j++) pos[j] += s.run[w][dg[j]];
 }
 
-// Stable sort of n packed words (offset << 12 | index) held as items; the
-// sorted words end in pk[0..n).  full: by the whole offset (low 6 bits, then
-// high 6 bits); else by its low kOtSlabBits bits (the words of one slab).
-// Ends synchronised.
-template <int NW>
-__device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, bool full, uint32_t* pk,
-                                        OtRank<NW>& s) {
+// Stable sort of n packed words (offset << 12 | index) held as items by
+// digits of rel = offset - lo: `passes` (1 or 2) passes of log2(D) bits from
+// bit sh of rel up; the sorted words end in pk[0..n).  Ends synchronised.
+template <int NW, int D, bool RUNS = false>
+__device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, uint32_t lo, int sh, int passes,
+                                        uint32_t* pk, OtRank<NW, D>& s) {
+  constexpr int B = D == 64 ? 6 : 8;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * kOtItems);
-  const uint32_t m0 = full ? 63u : (1u << kOtSlabBits) - 1u;
   uint32_t dg[kOtItems];
   int32_t pos[kOtItems];
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) dg[j] = (key[j] >> kOtIdxBits) & m0;
-  ot_rank<NW>(dg, n, pos, s);
+  for (int j = 0; j < kOtItems; j++) dg[j] = (((key[j] >> kOtIdxBits) - lo) >> sh) & uint32_t(D - 1);
+  ot_rank<NW, D, RUNS>(dg, n, pos, s);
 #pragma unroll
   for (int j = 0; j < kOtItems; j++)
     if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
   ot_sync<NW>();
-  if (!full) return;
+  if (passes == 1) return;
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
     key[j] = e < n ? pk[e] : 0u;
-    dg[j] = (key[j] >> (kOtIdxBits + 6)) & 63u;
+    dg[j] = (((key[j] >> kOtIdxBits) - lo) >> (sh + B)) & uint32_t(D - 1);
   }
-  ot_rank<NW>(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
+  ot_rank<NW, D>(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
 #pragma unroll
   for (int j = 0; j < kOtItems; j++)
     if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
@@ -312,7 +342,7 @@ __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ tim
                                                   const int64_t* __restrict__ node_off, int64_t t0,
                                                   uint16_t* __restrict__ toff_out, int32_t* __restrict__ rule_out,
                                                   int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles) {
-  __shared__ OtRank<4> s;
+  __shared__ OtRank<4, 64> s;
   __shared__ uint32_t pk[kOtTile];
   __shared__ int32_t rl[kOtTile];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -339,22 +369,17 @@ __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ tim
     key[j] = e < n ? ((tv[j] - b) << kOtIdxBits) | uint32_t(e) : 0u;
     if (e < n) rl[e] = rv[j];
   }
-  ot_sort<4>(key, n, true, pk, s);
+  // by slab; a node's only tile by the whole offset (its last pass is the slab)
+  const int32_t nd = tile_node[t];
+  const bool one = tile_base[nd + 1] - tile_base[nd] == 1;
+  if (one) ot_sort<4, 64>(key, n, 0u, 0, 2, pk, s);
+  else ot_sort<4, 64, true>(key, n, 0u, kOtSlabBits, 1, pk, s);
   int32_t* __restrict__ pt = pre + t * kOtPre;
-  if constexpr (kOtSlabBits == 6) {  // slabs = the last pass's digits
-    if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];
-  }
+  if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];  // slabs = the last pass's digits
   for (int p = threadIdx.x; p < n; p += 256) {
     const uint32_t v = pk[p];
     toff_out[r.lo + p] = uint16_t(v >> kOtIdxBits);
     __builtin_nontemporal_store(rl[v & kOtIdxMask], rule_out + r.lo + p);
-    if constexpr (kOtSlabBits != 6) {  // slab prefix: the slabs that start at p (and past the last event, n)
-      const int sp = int(v >> (kOtIdxBits + kOtSlabBits));
-      const int sq = p > 0 ? int(pk[p - 1] >> (kOtIdxBits + kOtSlabBits)) : -1;
-      for (int k = sq + 1; k <= sp; k++) pt[k] = p;
-      if (p == n - 1)
-        for (int k = sp + 1; k <= kOtSlabs; k++) pt[k] = n;
-    }
   }
 }
 
@@ -536,7 +561,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restr
                                                        int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                        int64_t* __restrict__ big, unsigned* __restrict__ big_n) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * kOtItems;
-  __shared__ OtRank<NW> s;
+  __shared__ OtRank<NW, 256> s;
   __shared__ uint32_t pk[kChunk + kChunk / 32];  // the owner list while gathering (padded), then the sorted words
   __shared__ int32_t rl[kChunk];
   __shared__ int32_t ps[kOtMaxTiles + 1];
@@ -596,7 +621,9 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restr
           ps, psrc, wsum);
       ot_owners<NW>(ps, int(M), 0, n_el, own, wsum);
       ot_gather<true>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl);
-      ot_sort<NW>(key, n_el, jb - ja > 1, pk, s);
+      // by rel = offset - the run's first second (< 64 * (jb - ja)): one
+      // 8-bit pass for up to 4 slabs
+      ot_sort<NW, 256>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
       const int64_t o = lo_n + slab_off[ja];
       for (int p = threadIdx.x; p < n_el; p += kThreads) {
         const uint32_t v = pk[p];
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
                                                  const int32_t* __restrict__ pre, int64_t t0,
                                                  int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                  const int64_t* __restrict__ big, const unsigned* __restrict__ big_n) {
-  __shared__ OtRank<4> s;
+  __shared__ OtRank<4, 64> s;
   __shared__ uint32_t pk[kOtTile + kOtTile / 32];
   __shared__ int32_t rl[kOtTile];
   __shared__ int32_t ps[kOtMaxTiles + 1];
@@ -692,7 +719,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
         ot_gather<true>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc, own, c0, n_el, key, rl);
-        ot_sort<4>(key, n_el, false, pk, s);
+        ot_sort<4, 64>(key, n_el, uint32_t(j) << kOtSlabBits, 0, 1, pk, s);
         for (int p = threadIdx.x; p < n_el; p += 256) {
           const uint32_t v = pk[p];
           const uint32_t d = (v >> kOtIdxBits) & kSec;

@@ -227,7 +227,7 @@ def progression_rules(R, n_nodes):
 
 @pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("R,N,secs,star_every", [(1200, 3, 3600, 13), (2600, 2, 4096, 2), (64, 1, 61, 3),
-                                                 (12000, 1, 120, 1)])
+                                                 (12000, 1, 120, 1), (40, 1, 4096, 10**9)])
 def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
     """The one-pass time order on nodes far larger than one LDS chunk:
     every-second rules put > 4096 events into one 64-s slab (the slab is
@@ -235,7 +235,9 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
     and at 2600 rules on 2 nodes over 4096 s each node holds > 5 M events,
     more than 1024 tiles (portion lists in groups); 61 s: one tile per node.
     12000 every-second rules on one node: every second holds more events than
-    a merge chunk (k_ot_big sorts the slab chunk by chunk).
+    a merge chunk (k_ot_big sorts the slab chunk by chunk).  40 sparse rules
+    on one node over 4096 s: ~7 k events in two tiles, merge runs of dozens of
+    slabs (sorted in two 8-bit passes).
     Against the oracle's lists sorted by (time, rule)."""
     specs = [PROGRESSION_MIX[0] if i % star_every == 0 else PROGRESSION_MIX[1 + i % (len(PROGRESSION_MIX) - 1)]
              for i in range(R)]
@@ -259,8 +261,10 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
         assert b - a == len(exp_t), n
         assert np.array_equal(time2[a:b], exp_t[order]), n
         assert np.array_equal(rule2[a:b], exp_r[order]), n
-    if secs == 4096:
+    if R == 2600:
         assert (np.diff(node_off) > 1024 * 4096).all()
+    if R == 40:  # two tiles, runs of more than 4 slabs
+        assert 4096 < node_off[1] < 2 * 4096 and node_off[1] < 64 * 4096 // 8
 
 
 @pytest.mark.parametrize("zone,t0", [("UTC", synth.T0_2026 + 64 * DAY + 1234),
