@@ -1181,11 +1181,13 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
   } else {
     const PlanArgs& pa = a.rm.pa;
     const int64_t nruns = R * int64_t(pa.G);
-    // a quarter of the persistent writer grid: the window's rule-major fires
-    // are few, and the previous window's per-node writer keeps the CUs
-    constexpr int side_div = 4;
+    // the whole persistent grid: beside the previous window's per-node writer
+    // only its free block slots run, and a smaller grid left this
+    // latency-bound writer with fewer waves (same-box A/B,
+    // profiles/r03_ab_pn_side.json: a quarter grid 3.21, a half 3.13, the
+    // whole 3.12 ms per pernode step)
     launch_write_cf(s->d, pa, a.rm.run_anchor.p, a.rm.run_count.p, a.rm.run_dmask.p, a.rm.run_off.p, nruns,
-                    a.rm.block_run.p, rm_cap, a.times.p, std::max(1, c->write_blocks / side_div), sc);
+                    a.rm.block_run.p, rm_cap, a.times.p, c->write_blocks, sc);
     if ((a.rm.plan.flags & (kPlanT0Walk | kPlanWalkSegs)) != 0)
       launch_write_walk(s->d, R, pa, a.rm.run_anchor.p, a.rm.run_count.p, a.rm.run_dmask.p, a.rm.run_off.p, rm_cap,
                         a.times.p, sc);
