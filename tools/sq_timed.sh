@@ -1,5 +1,5 @@
 #!/bin/bash
-# SQ counters of the time-ordered per-node kernels (k_seg_tiles, k_ot_merge), two PMC passes.  tools/sq_timed.sh <tag>
+# SQ counters of the time-ordered per-node kernels (k_ot_tile, k_ot_merge), two PMC passes.  tools/sq_timed.sh <tag>
 set -o pipefail
 OUT=gpurun_out/${1:-sq_tw}
 mkdir -p "$OUT"
@@ -14,7 +14,7 @@ import csv, glob, sys, collections
 tot = collections.defaultdict(float); n = collections.Counter()
 for f in glob.glob(sys.argv[1] + '/sq*/**/*counter_collection.csv', recursive=True):
     for r in csv.DictReader(open(f)):
-        for kn in ('k_seg_tiles', 'k_ot_merge', 'k_seg_records', 'k_node_write'):
+        for kn in ('k_ot_tile', 'k_ot_merge', 'k_seg_records', 'k_node_write'):
             if kn in r['Kernel_Name']:
                 tot[kn, r['Counter_Name']] += float(r['Counter_Value'])
                 n[kn, r['Counter_Name']] += 1
