@@ -59,11 +59,14 @@ class cg_csr(C.Structure):
                 ("times_cap", C.c_int64), ("n_events", C.c_int64)]
 
 
+ABI_VERSION = 2  # CG_ABI_VERSION of include/cronsun_gpu.h
+
+
 class cg_rules_in(C.Structure):
     _fields_ = [("n_nodes", C.c_int32), ("n_groups", C.c_int32), ("n_rules", C.c_int32),
                 ("n_jobs", C.c_int32)] + [(n, C.c_void_p) for n in (
                     "group_off", "group_nodes", "group_exists", "rule_job", "nid_off", "nids",
-                    "gid_off", "gids", "ex_off", "ex", "job_pause")]
+                    "gid_off", "gids", "ex_off", "ex", "job_pause", "rule_key")]
 
 
 class cg_node_csr(C.Structure):
@@ -200,7 +203,7 @@ def lib():
     _preload_torch_hip()
     L = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
     SYMBOLS = _declare(L)
-    if L.cg_abi_version() != 1:
+    if L.cg_abi_version() != ABI_VERSION:
         raise ImportError("libcronsun_gpu ABI mismatch")
     _L = L
     return L

@@ -69,12 +69,18 @@ struct DBuf {
 struct RulesStore {
   DBuf<int64_t> nid_off, gid_off, ex_off, group_off;
   DBuf<int32_t> nids, gids, ex, group_nodes, rule_job;
+  // next_same[r]: the next rule of r's job with r's Cmd key (rule_key), or -1
+  // (Job.Cmds keeps the last included rule per key, job.go:604-609); only
+  // uploaded when some job repeats a key (has_dup)
+  DBuf<int32_t> next_same;
+  bool has_dup = false;
   DBuf<uint8_t> group_exists, job_pause;
   int32_t n_nodes = 0, n_groups = 0, n_rules = 0, n_jobs = 0;
   uint64_t serial = 0;  // unique per upload: keys the per-node transpose cache
   void release() {
     nid_off.release(); gid_off.release(); ex_off.release(); group_off.release();
     nids.release(); gids.release(); ex.release(); group_nodes.release(); rule_job.release();
+    next_same.release();
     group_exists.release(); job_pause.release();
   }
 };
@@ -316,3 +322,6 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
                         bool in16);
 // the time-order pass over the last (rule-major) per-node result; c->mu held
 int order_by_time_locked(cg_ctx* c, bool in16 = false);
+// CG_ORDER_LSD set: order every window by the LSD passes (int64 times; the
+// writer must not emit 16-bit offsets then)
+bool order_lsd_only();

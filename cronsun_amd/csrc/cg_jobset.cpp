@@ -92,6 +92,14 @@ int cg_jobset_rules(cg_jobset* js, cg_rules_in* out) {
   out->ex_off = js->f_ex_off.data();
   out->ex = js->f_ex.data();
   out->job_pause = js->job_pause.data();
+  // Cmd.GetID() = Job.ID + Rule.ID (job.go:130-132): within one job two keys
+  // are equal exactly when the Rule.IDs are, so interning the Rule.IDs is
+  // enough (raw IDs: the node path never trims them, only Job.Check does)
+  std::unordered_map<std::string, int32_t> key_idx;
+  js->f_rule_key.resize(js->rule_ids.size());
+  for (size_t r = 0; r < js->rule_ids.size(); r++)
+    js->f_rule_key[r] = key_idx.emplace(js->rule_ids[r], int32_t(key_idx.size())).first->second;
+  out->rule_key = js->f_rule_key.empty() ? nullptr : js->f_rule_key.data();
   return CG_OK;
 }
 

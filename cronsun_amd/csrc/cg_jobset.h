@@ -30,6 +30,7 @@ struct cg_jobset {
   // frozen arrays
   std::vector<int64_t> f_group_off, f_nid_off, f_gid_off, f_ex_off;
   std::vector<int32_t> f_group_nodes, f_nids, f_gids, f_ex;
+  std::vector<int32_t> f_rule_key;  // interned Rule.ID (Cmd key within a job)
 
   int32_t node(const std::string& id) {
     auto it = node_idx.find(id);

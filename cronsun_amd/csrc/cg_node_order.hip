@@ -37,10 +37,14 @@ constexpr int kTsTile = 256 * kTsItems;  // events per tile (4 waves x 16 items 
 constexpr int kTsBits = 6;
 constexpr int kTsDigits = 1 << kTsBits;
 
-__global__ void k_ts_tile_count(const int64_t* __restrict__ node_off, int32_t N, int tile, int32_t* __restrict__ cnt) {
+// tiles per node; none at all when the lists' total exceeds the buffers' capacity
+// cap (a pipelined window whose writer wrote nothing: CG_ECAPACITY at the wait),
+// so no later kernel of the pass touches an event past cap
+__global__ void k_ts_tile_count(const int64_t* __restrict__ node_off, int32_t N, int tile, int64_t cap,
+                                int32_t* __restrict__ cnt) {
   const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
   if (n >= N) return;
-  cnt[n] = int32_t((node_off[n + 1] - node_off[n] + tile - 1) / tile);
+  cnt[n] = node_off[N] > cap ? 0 : int32_t((node_off[n + 1] - node_off[n] + tile - 1) / tile);
 }
 
 __global__ void k_ts_tiles(const int64_t* __restrict__ tile_base, int32_t N, int32_t* __restrict__ tile_node) {
@@ -762,7 +766,7 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
       (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) ||
       (rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N)))))
     return rc;
-  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, node_off, N, kOtTile, c->ts_cnt.p);
+  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, node_off, N, kOtTile, cap, c->ts_cnt.p);
   launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
   hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
   uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
@@ -802,6 +806,11 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   return order_by_time_locked(c);
 }
 
+bool order_lsd_only() {
+  static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;
+  return lsd_only;
+}
+
 int order_by_time_locked(cg_ctx* c, bool in16) {
   int rc = CG_OK;
   const int64_t En = c->pn_E;
@@ -817,8 +826,7 @@ int order_by_time_locked(cg_ctx* c, bool in16) {
   hipStream_t st = c->st;
 
   // windows <= 4096 s: tile sort + merge (CG_ORDER_LSD=1: the LSD passes)
-  static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;
-  if (bits <= 12 && !lsd_only) {
+  if (bits <= 12 && !order_lsd_only()) {
     (void)hipEventRecord(c->pev[0], st);
     if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, st, in16))) return rc;
     (void)hipEventRecord(c->pev[1], st);
@@ -829,7 +837,8 @@ int order_by_time_locked(cg_ctx* c, bool in16) {
   }
   if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1))) return rc;
   if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N))))) return rc;
-  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, c->node_off.p, N, kTsTile, c->ts_cnt.p);
+  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, c->node_off.p, N, kTsTile, En,
+                     c->ts_cnt.p);
   launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
   int64_t T = 0;
   if ((rc = cg_hip_check(hipMemcpyAsync(&T, c->ts_base.p + N, 8, hipMemcpyDeviceToHost, st), "tiles")) ||

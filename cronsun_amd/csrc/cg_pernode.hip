@@ -27,6 +27,7 @@
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cronsun_gpu.h"
@@ -49,6 +50,7 @@ struct RulesDev {
   const int64_t* group_off;
   const int32_t* group_nodes;
   const uint8_t* group_exists;
+  const int32_t* next_same;  // next rule of the job with the same Cmd key, -1; null: none repeats
   int32_t R, G, N, words;
 };
 
@@ -67,6 +69,40 @@ __device__ __forceinline__ void bm_clear(uint32_t* bm, int32_t n, int32_t N) {
   if (n >= 0 && n < N) atomicAnd(&bm[n >> 5], ~(1u << (n & 31)));
 }
 
+// Rule q's node set under `mode` into the wave's bitmap bm (zeroed here):
+// NodeIDs and existing groups' members (JobRule.included job.go:274-288,
+// Group.Included group.go:111-119), minus the mode's excludes; empty for a
+// paused job (job.go:593).
+__device__ void rule_bitmap(const RulesDev& d, int mode, int64_t q, uint32_t* bm, int lane) {
+  for (int w = lane; w < d.words; w += 64) bm[w] = 0;
+  wave_sync_lds();
+  const int32_t job = d.rule_job[q];
+  if (d.job_pause[job]) return;
+  for (int64_t k = d.nid_off[q] + lane; k < d.nid_off[q + 1]; k += 64) bm_set(bm, d.nids[k], d.N);
+  for (int64_t k = d.gid_off[q]; k < d.gid_off[q + 1]; k++) {
+    int32_t g = d.gids[k];
+    if (g < 0 || g >= d.G || !d.group_exists[g]) continue;  // gs[gid] missing
+    for (int64_t p = d.group_off[g] + lane; p < d.group_off[g + 1]; p += 64)
+      bm_set(bm, d.group_nodes[p], d.N);
+  }
+  wave_sync_lds();
+  if (mode == CG_EXCLUDE_RULE) {
+    for (int64_t k = d.ex_off[q] + lane; k < d.ex_off[q + 1]; k += 64) bm_clear(bm, d.ex[k], d.N);
+  } else if (mode == CG_EXCLUDE_CUMULATIVE) {
+    int64_t r0 = q;
+    while (r0 > 0 && d.rule_job[r0 - 1] == job) r0--;
+    for (int64_t p = r0; p <= q; p++)
+      for (int64_t k = d.ex_off[p] + lane; k < d.ex_off[p + 1]; k += 64) bm_clear(bm, d.ex[k], d.N);
+  }
+  wave_sync_lds();
+}
+
+// One wave per rule r: r's node set (rule_bitmap), minus the node sets of the
+// later rules of r's job with the same Cmd key -- Job.Cmds' map keeps the
+// last included rule per Job.ID+Rule.ID (job.go:604-609) -- then either the
+// count (WRITE false) or the ballot/prefix compaction of the set bits into the
+// rule-major pairs (WRITE true).  With repeated keys each wave has a second
+// bitmap (sh) for the later rules.
 template <bool WRITE>
 __global__ __launch_bounds__(256) void k_rule_nodes(RulesDev d, int mode, int wpb,
                                                      int32_t* __restrict__ rn_cnt,
@@ -76,30 +112,17 @@ __global__ __launch_bounds__(256) void k_rule_nodes(RulesDev d, int mode, int wp
   extern __shared__ uint32_t bm_all[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (wave >= wpb) return;
-  uint32_t* bm = bm_all + size_t(wave) * d.words;
+  const int per = d.next_same ? 2 : 1;
+  uint32_t* bm = bm_all + size_t(wave) * per * d.words;
+  uint32_t* sh = bm + d.words;
   for (int64_t r = int64_t(blockIdx.x) * wpb + wave; r < d.R; r += int64_t(gridDim.x) * wpb) {
-    for (int w = lane; w < d.words; w += 64) bm[w] = 0;
-    wave_sync_lds();
-    const int32_t job = d.rule_job[r];
-    if (!d.job_pause[job]) {  // job.go:593
-      for (int64_t k = d.nid_off[r] + lane; k < d.nid_off[r + 1]; k += 64) bm_set(bm, d.nids[k], d.N);
-      for (int64_t k = d.gid_off[r]; k < d.gid_off[r + 1]; k++) {
-        int32_t g = d.gids[k];
-        if (g < 0 || g >= d.G || !d.group_exists[g]) continue;  // gs[gid] missing
-        for (int64_t q = d.group_off[g] + lane; q < d.group_off[g + 1]; q += 64)
-          bm_set(bm, d.group_nodes[q], d.N);
+    rule_bitmap(d, mode, r, bm, lane);
+    if (d.next_same) {
+      for (int32_t q = d.next_same[r]; q >= 0; q = d.next_same[q]) {
+        rule_bitmap(d, mode, q, sh, lane);
+        for (int w = lane; w < d.words; w += 64) bm[w] &= ~sh[w];
+        wave_sync_lds();
       }
-      wave_sync_lds();
-      if (mode == CG_EXCLUDE_RULE) {
-        for (int64_t k = d.ex_off[r] + lane; k < d.ex_off[r + 1]; k += 64) bm_clear(bm, d.ex[k], d.N);
-      } else if (mode == CG_EXCLUDE_CUMULATIVE) {
-        int64_t r0 = r;
-        while (r0 > 0 && d.rule_job[r0 - 1] == job) r0--;
-        for (int64_t q = r0; q <= r; q++)
-          for (int64_t k = d.ex_off[q] + lane; k < d.ex_off[q + 1]; k += 64)
-            bm_clear(bm, d.ex[k], d.N);
-      }
-      wave_sync_lds();
     }
     if (!WRITE) {
       int32_t c = 0;
@@ -787,6 +810,26 @@ int upload_rules(const cg_rules_in* in, RulesStore* st, hipStream_t s) {
   if ((rc = upload(st->group_off, in->group_off, G ? G + 1 : 0, s))) return rc;
   if ((rc = upload(st->group_nodes, in->group_nodes, n_gn, s))) return rc;
   if ((rc = upload(st->group_exists, in->group_exists, G, s))) return rc;
+  // Cmd keys: next_same[r] = the next rule of r's job with r's key (Job.Cmds'
+  // later-rule-wins map, job.go:604-609), uploaded only when a key repeats
+  std::vector<int32_t> next_same;
+  st->has_dup = false;
+  if (in->rule_key && R) {
+    next_same.assign(size_t(R), -1);
+    std::unordered_map<int32_t, int32_t> last;  // key -> the job's latest rule seen (walking back)
+    for (int32_t r = R - 1; r >= 0; r--) {
+      if (r == R - 1 || in->rule_job[r] != in->rule_job[r + 1]) last.clear();
+      auto it = last.find(in->rule_key[r]);
+      if (it != last.end()) {
+        next_same[size_t(r)] = it->second;
+        it->second = r;
+        st->has_dup = true;
+      } else {
+        last.emplace(in->rule_key[r], r);
+      }
+    }
+  }
+  if (st->has_dup && (rc = upload(st->next_same, next_same.data(), size_t(R), s))) return rc;
   st->n_nodes = in->n_nodes;
   st->n_groups = G;
   st->n_rules = R;
@@ -801,7 +844,9 @@ int rule_nodes_locked(cg_ctx* c, const RulesStore& st, int mode, int64_t* nnz_ou
   if (mode < 0 || mode > 2) return cg_fail(CG_EINVAL, "bad exclude mode");
   const int32_t R = st.n_rules, G = st.n_groups, N = st.n_nodes;
   const int32_t words = (N + 31) / 32;
-  if (size_t(words) * 4 > 64 * 1024) return cg_fail(CG_ERANGE, "more than 524288 nodes");
+  if (size_t(words) * 4 * (st.has_dup ? 2 : 1) > 64 * 1024)
+    return cg_fail(CG_ERANGE, st.has_dup ? "more than 262144 nodes with repeated Cmd keys"
+                                         : "more than 524288 nodes");
   hipStream_t s = c->st;
   int rc;
   if ((rc = c->rn_cnt.ensure(std::max(R, 1)))) return rc;
@@ -809,9 +854,10 @@ int rule_nodes_locked(cg_ctx* c, const RulesStore& st, int mode, int64_t* nnz_ou
   if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(R))))) return rc;
   RulesDev d{st.nid_off.p, st.nids.p, st.gid_off.p, st.gids.p, st.ex_off.p, st.ex.p,
              st.rule_job.p, st.job_pause.p, st.group_off.p, st.group_nodes.p,
-             st.group_exists.p, R, G, N, std::max(words, 1)};
-  int wpb = int(std::min<size_t>(4, std::max<size_t>(1, (64 * 1024) / (size_t(d.words) * 4))));
-  size_t lds = size_t(wpb) * d.words * 4;
+             st.group_exists.p, st.has_dup ? st.next_same.p : nullptr, R, G, N, std::max(words, 1)};
+  const size_t per = st.has_dup ? 2 : 1;  // a second bitmap per wave for repeated Cmd keys
+  int wpb = int(std::min<size_t>(4, std::max<size_t>(1, (64 * 1024) / (per * size_t(d.words) * 4))));
+  size_t lds = size_t(wpb) * per * d.words * 4;
   int grid = gridn(R, wpb, 256 * 16);
   if (R > 0)
     hipLaunchKernelGGL(k_rule_nodes<false>, dim3(grid), dim3(64 * wpb), lds, s, d, mode, wpb,
@@ -991,7 +1037,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
 #endif
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
   // (time, rule) order of a window <= 4096 s: 16-bit offsets for the tile sort
-  const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0;
+  // (the same predicate as order_by_time_locked's tile sort: bits <= 12, not LSD)
+  const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
@@ -1039,8 +1086,15 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_cache_mode = mode;
   *n_events = En;
   *nnz_out = nnz;
-  // (time, rule) order asked for: the time-order pass inside the call
-  if (c->node_order == CG_NODE_ORDER_TIME) return order_by_time_locked(c, off16);
+  // (time, rule) order asked for: the time-order pass inside the call; if it
+  // fails the lists may hold the writer's 16-bit offsets: nothing readable
+  if (c->node_order == CG_NODE_ORDER_TIME) {
+    if ((rc = order_by_time_locked(c, off16))) {
+      c->pn_E = 0;
+      *n_events = 0;
+    }
+    return rc;
+  }
   c->kt[12] = 0.f;
   return CG_OK;
 }
@@ -1143,6 +1197,8 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
                               "on this rule set and exclude mode first (rule->node join, bands, capacity)");
   if (t1 - t0 > CG_MAX_HORIZON || t0 < -(int64_t(1) << 45) || t1 > (int64_t(1) << 45))
     return cg_fail(CG_ERANGE, "horizon must satisfy t1 - t0 <= CG_MAX_HORIZON (40 years)");
+  if (async_pending(c))  // their only readable result would be lost below
+    return cg_fail(CG_EINVAL, "pipelined rule-major calls pending (call cg_expand_wait first)");
   const int64_t rm_cap = int64_t(c->times.cap);
   const int64_t node_cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
   if (rm_cap == 0 || node_cap == 0) return cg_fail(CG_ECAPACITY, "no output capacity yet (run a synchronous call)");

@@ -151,13 +151,22 @@ class RulesIn:
               "rule_job": np.int32, "nid_off": np.int64, "nids": np.int32, "gid_off": np.int64,
               "gids": np.int32, "ex_off": np.int64, "ex": np.int32, "job_pause": np.uint8}
 
-    def __init__(self, n_nodes, n_groups, n_rules, n_jobs, **arrays):
+    def __init__(self, n_nodes, n_groups, n_rules, n_jobs, rule_key=None, **arrays):
+        """rule_key (optional, [R]): the rules' Cmd keys (Job.ID+Rule.ID,
+        job.go:130-132) interned so that two rules of one job compare equal
+        exactly when their Rule.IDs are; None = every rule its own key."""
         self.n_nodes, self.n_groups, self.n_rules, self.n_jobs = n_nodes, n_groups, n_rules, n_jobs
         for f in self.FIELDS:
             a = np.ascontiguousarray(arrays[f], dtype=self.DTYPES[f])
             if a.size == 0:
                 a = np.zeros(1, dtype=self.DTYPES[f])
             setattr(self, f, a)
+        self.rule_key = None
+        if rule_key is not None:
+            k = np.ascontiguousarray(rule_key, dtype=np.int32)
+            if k.shape != (n_rules,):
+                raise ValueError("rule_key must hold one key per rule")
+            self.rule_key = k if k.size else np.zeros(1, dtype=np.int32)
 
     def slice_rules(self, lo, hi):
         """The rules [lo, hi) as their own rule set (job-ID-range shard): the
@@ -183,7 +192,8 @@ class RulesIn:
                        group_off=self.group_off, group_nodes=self.group_nodes,
                        group_exists=self.group_exists, rule_job=rj - j0, nid_off=nid_off, nids=nids,
                        gid_off=gid_off, gids=gids, ex_off=ex_off, ex=ex,
-                       job_pause=self.job_pause[j0:j1])
+                       job_pause=self.job_pause[j0:j1],
+                       rule_key=None if self.rule_key is None else self.rule_key[lo:hi])
 
     def to_c(self):
         s = _lib.cg_rules_in()
@@ -191,6 +201,7 @@ class RulesIn:
             self.n_nodes, self.n_groups, self.n_rules, self.n_jobs)
         for f in self.FIELDS:
             setattr(s, f, getattr(self, f).ctypes.data)
+        s.rule_key = self.rule_key.ctypes.data if self.rule_key is not None else None
         return s
 
 

@@ -207,4 +207,5 @@ def rules_in_of(h) -> RulesIn:
         nid_off=nid_off, nids=arr(c.nids, int(nid_off[-1]), np.int32),
         gid_off=gid_off, gids=arr(c.gids, int(gid_off[-1]), np.int32),
         ex_off=ex_off, ex=arr(c.ex, int(ex_off[-1]), np.int32),
-        job_pause=arr(c.job_pause, J, np.uint8))
+        job_pause=arr(c.job_pause, J, np.uint8),
+        rule_key=arr(c.rule_key, R, np.int32) if c.rule_key else None)

@@ -151,8 +151,10 @@ def rules_for_nodes(n_rules, n_nodes=10000, n_groups=500, seed=0x5EED + 3,
                    job_pause=(rng.random(n_rules) < pause_frac).astype(np.uint8))
 
 
-def multi_rule_jobs(n_jobs, rules_per_job=(1, 4), n_nodes=64, n_groups=12, seed=7):
-    """Small jobsets with several rules per job (exclude-mode semantics tests)."""
+def multi_rule_jobs(n_jobs, rules_per_job=(1, 4), n_nodes=64, n_groups=12, seed=7, key_choices=0):
+    """Small jobsets with several rules per job (exclude-mode semantics tests).
+    key_choices > 0: each rule's Rule.ID is one of that many values (rule_key),
+    so rules of a job repeat Cmd keys (Job.Cmds keeps the last, job.go:604-609)."""
     rng = np.random.default_rng(seed)
     per = rng.integers(rules_per_job[0], rules_per_job[1] + 1, n_jobs)
     rule_job = np.repeat(np.arange(n_jobs, dtype=np.int32), per)
@@ -163,4 +165,6 @@ def multi_rule_jobs(n_jobs, rules_per_job=(1, 4), n_nodes=64, n_groups=12, seed=
     base.rule_job = rule_job
     base.n_jobs = n_jobs
     base.job_pause = (rng.random(n_jobs) < 0.1).astype(np.uint8)
+    if key_choices:
+        base.rule_key = rng.integers(0, key_choices, R).astype(np.int32)
     return base

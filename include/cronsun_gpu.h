@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define CG_ABI_VERSION 1
+/* 2: cg_rules_in.rule_key (Job.Cmds' Job.ID+Rule.ID map key) */
+#define CG_ABI_VERSION 2
 
 #define CG_OK 0
 #define CG_EINVAL (-1)    /* bad argument */
@@ -361,6 +362,21 @@ typedef struct {
   const int64_t* ex_off;        /* [R+1] JobRule.ExcludeNodeIDs */
   const int32_t* ex;
   const uint8_t* job_pause;     /* [J] Job.Pause */
+  /* [R] or NULL: the rule's Cmd key (job.go:130-132 Cmd.GetID() = Job.ID +
+   * Rule.ID), interned to any int32 such that two rules OF THE SAME JOB have
+   * equal values exactly when their Rule.IDs are equal.  Job.Cmds keeps one
+   * Cmd per key -- `cmds[cmd.GetID()] = cmd` (job.go:604-609): the LAST
+   * included rule of the job with that key -- and the node's Cron replaces an
+   * entry by ID (node/node.go:209-211, node/cron/cron.go:131-135).  So in
+   * every mode the pair (r, n) is dropped when a later rule of r's job with
+   * the same key is also scheduled on n (under the same mode: RULE and
+   * CUMULATIVE test the later rule with their own exclusion).  Keys are only
+   * compared within a job: equal Job.ID+Rule.ID strings of DIFFERENT jobs
+   * ("a"+"bc", "ab"+"c") replace each other in the reference in the random
+   * order of GetJobs' map, so both are kept here.  NULL: every rule is its
+   * own key (the caller guarantees distinct Rule.IDs within a job).
+   * cg_jobset_rules fills it from the Rule.IDs. */
+  const int32_t* rule_key;
 } cg_rules_in;
 
 /* Per-node fire lists: for every node n, the (time, rule) events of the rules
@@ -456,7 +472,9 @@ int cg_expand_per_node_rules_device(cg_ctx* ctx, const cg_specs* specs, const cg
  * (cg_node_result_*), and a returned error may belong to any window since the
  * previous wait.  The per-node result accessors refuse (CG_EINVAL) while
  * windows are pending; a synchronous call drains them and discards their
- * results and errors.  cg_last_kernel_times [8] = the mean per-node writer
+ * results and errors.  The call refuses (CG_EINVAL) while pipelined
+ * rule-major calls (cg_expand_device_async) are pending: wait for them first
+ * (a per-node window replaces the readable rule-major result).  cg_last_kernel_times [8] = the mean per-node writer
  * time of the waited windows. */
 int cg_expand_per_node_rules_device_async(cg_ctx* ctx, const cg_specs* specs, const cg_zone* z, int64_t t0,
                                           int64_t t1, const cg_rules* rules, int mode);

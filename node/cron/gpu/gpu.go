@@ -32,6 +32,7 @@ import (
 	"errors"
 	"fmt"
 	"runtime"
+	"sync"
 	"time"
 	"unsafe"
 
@@ -58,14 +59,20 @@ func lastErr(rc C.int) error {
 
 // Engine is one MI355X: a cg_ctx (device, stream, HBM buffers).  Calls on an
 // Engine are serialised by the library and block the calling OS thread.
-type Engine struct{ ctx *C.cg_ctx }
+// Engine owns one device context.  Its methods may be called from several
+// goroutines: calls that set engine state and then use it (ExpandPerNode's
+// node order) hold mu across both steps.
+type Engine struct {
+	ctx *C.cg_ctx
+	mu  sync.Mutex
+}
 
 func NewEngine(device int) (*Engine, error) {
 	var ctx *C.cg_ctx
 	if rc := C.cg_init(C.int(device), &ctx); rc != 0 {
 		return nil, lastErr(rc)
 	}
-	e := &Engine{ctx}
+	e := &Engine{ctx: ctx}
 	runtime.SetFinalizer(e, func(e *Engine) { C.cg_destroy(e.ctx) })
 	return e, nil
 }
@@ -341,6 +348,10 @@ func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, 
 	defer runtime.KeepAlive(sp)
 	defer runtime.KeepAlive(z)
 	defer runtime.KeepAlive(j)
+	// cg_set_node_order is engine state: keep another goroutine's
+	// ExpandPerNode from changing it between the two calls below
+	e.mu.Lock()
+	defer e.mu.Unlock()
 	// cg_rules_in holds C pointers into the jobset (C memory): it may live in Go
 	// memory.  cg_node_csr would hold a pointer to the node offsets, so it and
 	// that buffer live in C memory (cgo's rule on Go pointers to Go pointers).

@@ -1226,7 +1226,9 @@ static int rule_included(const or_jobset *js, int32_t r, int32_t n) {
     return 0;
 }
 
-int or_rule_on_node(const or_jobset *js, int mode, int32_t r, int32_t n) {
+/* the loop body of Job.Cmds (job.go:596-610) for one rule, per mode: would
+ * rule r make a Cmd on node n */
+static int rule_makes_cmd(const or_jobset *js, int mode, int32_t r, int32_t n) {
     int32_t j = js->rule_job[r];
     if (js->job_pause[j]) return 0;          /* job.go:593 */
     if (!rule_included(js, r, n)) return 0;
@@ -1237,6 +1239,16 @@ int or_rule_on_node(const or_jobset *js, int mode, int32_t r, int32_t n) {
     while (r0 > 0 && js->rule_job[r0 - 1] == j) r0--;
     for (int32_t q = r0; q <= r; q++)
         if (in_list(js->ex, js->ex_off[q], js->ex_off[q + 1], n)) return 0;
+    return 1;
+}
+
+int or_rule_on_node(const or_jobset *js, int mode, int32_t r, int32_t n) {
+    if (!rule_makes_cmd(js, mode, r, n)) return 0;
+    if (!js->rule_key) return 1;
+    /* cmds[cmd.GetID()] = cmd (job.go:609): a later rule of the job with the
+     * same Job.ID+Rule.ID that also makes a Cmd on n overwrites r's */
+    for (int32_t q = r + 1; q < js->n_rules && js->rule_job[q] == js->rule_job[r]; q++)
+        if (js->rule_key[q] == js->rule_key[r] && rule_makes_cmd(js, mode, q, n)) return 0;
     return 1;
 }
 

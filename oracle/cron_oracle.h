@@ -144,6 +144,8 @@ typedef struct {
     const int64_t *ex_off;     /* [R+1] */
     const int32_t *ex;
     const uint8_t *job_pause;  /* [J] */
+    const int32_t *rule_key;   /* [R] or NULL: Cmd key (Job.ID+Rule.ID, job.go:130-132),
+                                  equal within a job exactly when the Rule.IDs are */
 } or_jobset;
 
 /* mode 0: reference scheduling path, Job.Cmds (excludes are a no-op,
@@ -151,6 +153,9 @@ typedef struct {
  * mode 1: per-rule exclude (N_r \ E_r), Pause honoured.
  * mode 2: cumulative exclude as web/job.go:222-257 (N_r \ U_{j<=r} E_j within
  *         the job), Pause honoured.
+ * In every mode a rule is dropped on n when a later rule of its job with the
+ * same rule_key is scheduled on n too: Job.Cmds' map keeps the last included
+ * rule per Cmd.GetID() (job.go:604-609).
  * Returns 1 if rule r is scheduled on node n. */
 int or_rule_on_node(const or_jobset *js, int mode, int32_t r, int32_t n);
 /* Job.IsRunOn(nid, groups)  job.go:616-630 (ignores Pause). */

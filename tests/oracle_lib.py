@@ -39,7 +39,7 @@ class OrJobset(C.Structure):
                 ("nid_off", C.c_void_p), ("nids", C.c_void_p),
                 ("gid_off", C.c_void_p), ("gids", C.c_void_p),
                 ("ex_off", C.c_void_p), ("ex", C.c_void_p),
-                ("job_pause", C.c_void_p)]
+                ("job_pause", C.c_void_p), ("rule_key", C.c_void_p)]
 
 
 _lib = None
@@ -245,6 +245,7 @@ def jobset(rin):
     js.n_nodes, js.n_groups, js.n_rules, js.n_jobs = rin.n_nodes, rin.n_groups, rin.n_rules, rin.n_jobs
     for f in rin.FIELDS:
         setattr(js, f, getattr(rin, f).ctypes.data)
+    js.rule_key = rin.rule_key.ctypes.data if rin.rule_key is not None else None
     return js
 
 

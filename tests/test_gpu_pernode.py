@@ -18,11 +18,7 @@ def eng():
 
 
 def oracle_jobset(rin):
-    js = O.OrJobset()
-    js.n_nodes, js.n_groups, js.n_rules, js.n_jobs = rin.n_nodes, rin.n_groups, rin.n_rules, rin.n_jobs
-    for f in rin.FIELDS:
-        setattr(js, f, getattr(rin, f).ctypes.data)
-    return js
+    return O.jobset(rin)
 
 
 def oracle_rule_nodes(rin, mode):
@@ -37,9 +33,13 @@ def oracle_rule_nodes(rin, mode):
     return out
 
 
+@pytest.mark.parametrize("keys", [0, 2])
 @pytest.mark.parametrize("mode", [_lib.EXCLUDE_NONE, _lib.EXCLUDE_RULE, _lib.EXCLUDE_CUMULATIVE])
-def test_rule_nodes_vs_oracle(eng, mode):
-    rin = synth.multi_rule_jobs(400, seed=11 + mode)
+def test_rule_nodes_vs_oracle(eng, mode, keys):
+    """keys 2: Rule.IDs drawn from two values, so a job's rules repeat Cmd keys
+    and the join drops a rule on the nodes a later same-key rule takes
+    (job.go:604-609)."""
+    rin = synth.multi_rule_jobs(400, seed=11 + mode, key_choices=keys)
     off, nodes = eng.rule_nodes(rin, mode)
     exp = oracle_rule_nodes(rin, mode)
     for r in range(rin.n_rules):
@@ -72,6 +72,76 @@ def test_per_node_fire_lists_vs_oracle(eng, mode, zone):
         got_r = rule[node_off[n]:node_off[n + 1]]
         assert np.array_equal(got_t, exp_t), n
         assert np.array_equal(got_r, exp_r), n
+
+
+def _string_world(seed, n_jobs=250, n_nodes=40, n_groups=8):
+    """Jobs with string IDs whose Rule.IDs repeat inside a job (including ""
+    and " "), interned by the C++ host layer (cg_jobset)."""
+    from cronsun_amd.model import Group, Job, JobRule, JobSet
+    rng = np.random.default_rng(seed)
+    nodes = [f"node-{i}" for i in range(n_nodes)]
+    groups = {f"g{g}": Group(f"g{g}", "", list(rng.choice(nodes, int(rng.integers(1, 12)), replace=False)))
+              for g in range(n_groups)}
+    specs = synth.spec_mix(n_jobs * 4, seed=seed, mix=synth.MIX_CONFIG2)
+    jobs, k = [], 0
+    for j in range(n_jobs):
+        rules = []
+        for _ in range(int(rng.integers(1, 5))):
+            rid = ["", " ", "a", "b"][int(rng.integers(0, 4))]
+            gids = [f"g{rng.integers(0, n_groups + 1)}" for _ in range(rng.integers(0, 3))]
+            nids = list(rng.choice(nodes, int(rng.integers(0, 4)), replace=False))
+            ex = list(rng.choice(nodes, int(rng.integers(0, 3)), replace=False))
+            rules.append(JobRule(rid, specs[k], gids, nids, ex))
+            k += 1
+        jobs.append(Job(f"job{j}", Rules=rules, Pause=bool(rng.random() < 0.05)))
+    return JobSet(jobs, groups), nodes
+
+
+@pytest.mark.parametrize("order", ["rule", "time"])
+@pytest.mark.parametrize("mode", [_lib.EXCLUDE_NONE, _lib.EXCLUDE_RULE, _lib.EXCLUDE_CUMULATIVE])
+def test_cmd_keys_per_node_vs_oracle_and_cmds(eng, mode, order):
+    """Job.Cmds keeps one Cmd per Job.ID+Rule.ID, the last included rule
+    (job.go:604-609; the node's Cron replaces entries by that ID,
+    node/node.go:209-211, cron.go:131-135).  Jobs whose rules repeat IDs
+    (empty and blank IDs included): every node's list, rule-ordered and
+    time-ordered, equals the oracle's; in mode NONE each node's rule set is
+    also the union of the host cg_jobset_cmds over the jobs."""
+    js, nodes = _string_world(61 + mode)
+    rin = js.rules_in()
+    assert rin.rule_key is not None
+    scheds = js.schedules()
+    t0, t1 = synth.T0_2026 + 40 * DAY + 600, synth.T0_2026 + 40 * DAY + 600 + 3600
+    if order == "time":
+        eng.set_node_order(_lib.NODE_ORDER_TIME)
+    try:
+        node_off, time, rule = eng.expand_per_node(scheds, None, t0, t1, rin, mode)
+    finally:
+        eng.set_node_order(_lib.NODE_ORDER_RULE)
+    specs = [r.Timer for r in js.rules]
+    eo, et = O.expand_batch(O.sched_array(oracle_parse_all(specs)), t0, t1, oracle_zone("UTC"))
+    rn = oracle_rule_nodes(rin, mode)
+    per_node = [[] for _ in range(rin.n_nodes)]
+    for r in range(rin.n_rules):
+        for n in rn[r]:
+            per_node[n].append(r)
+    raw = O.jobset(rin)
+    raw.rule_key = None
+    L = O.lib()
+    shadowed = sum(L.or_rule_on_node(raw, mode, r, n) for r in range(rin.n_rules) for n in range(rin.n_nodes)) \
+        - sum(len(p) for p in per_node)
+    assert shadowed > 0
+    for n in range(rin.n_nodes):
+        if mode == _lib.EXCLUDE_NONE:
+            nid = js.node_id(n)
+            cmds = sorted(r for j in range(len(js.jobs)) for r in js.cmds(j, nid))
+            assert cmds == per_node[n], n
+        exp_t, exp_r = O.node_list(eo, et, per_node[n]) if per_node[n] else (np.zeros(0, np.int64),
+                                                                            np.zeros(0, np.int32))
+        if order == "time":
+            o = np.lexsort((exp_r, exp_t))
+            exp_t, exp_r = exp_t[o], exp_r[o]
+        assert np.array_equal(time[node_off[n]:node_off[n + 1]], exp_t), n
+        assert np.array_equal(rule[node_off[n]:node_off[n + 1]], exp_r), n
 
 
 def test_per_node_config3_scale_properties(eng):
@@ -371,6 +441,25 @@ def test_per_node_async_windows(zone, order):
         dr.free()
         sp.free()
         e2.close()
+        # a 4096-s window past the output capacity that a 300-s window sized:
+        # the writer and the time-order pass write nothing, CG_ECAPACITY at
+        # the wait, and the engine still gives the right result afterwards
+        e3 = Engine(0)
+        e3.set_node_order(_lib.NODE_ORDER_TIME)
+        sp3, dr3 = e3.upload_c(arr, rin.n_rules), e3.upload_rules(rin)
+        Es, _ = e3.expand_per_node_rules_device(sp3, z, t0, t0 + 300, dr3, _lib.EXCLUDE_NONE)
+        ref = e3.node_copy_range(0, Es)
+        e3.expand_per_node_async(sp3, z, t0, t0 + 4096, dr3, _lib.EXCLUDE_NONE)
+        with pytest.raises(_lib.CgError) as err:
+            e3.expand_per_node_wait()
+        assert err.value.code == _lib.CG_ECAPACITY
+        e3.expand_per_node_async(sp3, z, t0, t0 + 300, dr3, _lib.EXCLUDE_NONE)
+        assert e3.expand_per_node_wait() == Es
+        got = e3.node_copy_range(0, Es)
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+        dr3.free()
+        sp3.free()
+        e3.close()
         return
     # a window far beyond the capacity: CG_ECAPACITY at the wait
     e2.expand_per_node_async(sp, z, t0, t0 + 2 * DAY, dr, _lib.EXCLUDE_NONE)

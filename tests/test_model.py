@@ -10,11 +10,12 @@ from cronsun_amd import _lib
 from cronsun_amd.model import ErrNilRule, Group, Job, JobRule, JobSet
 
 
-def _oracle_js(rin):
-    js = O.OrJobset()
-    js.n_nodes, js.n_groups, js.n_rules, js.n_jobs = rin.n_nodes, rin.n_groups, rin.n_rules, rin.n_jobs
-    for f in rin.FIELDS:
-        setattr(js, f, getattr(rin, f).ctypes.data)
+def _oracle_js(rin, keyed=True):
+    """The oracle's view of rin; keyed=False drops the Cmd keys (every rule its
+    own key), so a test can apply Job.Cmds' map by hand on top."""
+    js = O.jobset(rin)
+    if not keyed:
+        js.rule_key = None
     return js
 
 
@@ -43,7 +44,8 @@ def test_cmds_is_run_on_job_nodes_vs_oracle(seed):
     jobs, groups, nodes = random_world(seed)
     js = JobSet(jobs, groups)
     rin = js.rules_in()
-    ojs = _oracle_js(rin)
+    assert rin.rule_key is not None
+    ojs, ojs_raw = _oracle_js(rin), _oracle_js(rin, keyed=False)
     L = O.lib()
     rule0 = 0
     for j, job in enumerate(jobs):
@@ -54,9 +56,12 @@ def test_cmds_is_run_on_job_nodes_vs_oracle(seed):
             # Job.Cmds: map keyed by Job.ID+Rule.ID, later rules overwrite
             exp = {}
             for r in rules:
-                if n >= 0 and L.or_rule_on_node(ojs, 0, r, n):
+                if n >= 0 and L.or_rule_on_node(ojs_raw, 0, r, n):
                     exp[job.ID + js.rules[r].ID] = r
             assert js.cmds(j, nid) == sorted(exp.values()), (job.ID, nid)
+            # the oracle's per-node filter (what the GPU per-node lists are
+            # checked against) keeps exactly Job.Cmds' rules
+            assert [r for r in rules if n >= 0 and L.or_rule_on_node(ojs, 0, r, n)] == js.cmds(j, nid)
             exp_run = bool(n >= 0 and L.or_job_is_run_on(ojs, j, n))
             assert js.is_run_on(j, nid) == exp_run
         cap = 256
@@ -99,6 +104,61 @@ def test_duplicate_rule_ids_last_included_wins():
                           JobRule("x", "@weekly", NodeIDs=["n2"])])
     cmds = job.Cmds("n1", g)
     assert list(cmds) == ["jx"] and cmds["jx"][1].Timer == "@hourly"
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_keyed_oracle_is_cmds_map_in_every_mode(mode):
+    """or_rule_on_node with keys = the mode's own inclusion + Job.Cmds' map
+    (last scheduled rule per Job.ID+Rule.ID) applied on top."""
+    jobs, groups, nodes = random_world(20 + mode, n_jobs=80)
+    js = JobSet(jobs, groups)
+    rin = js.rules_in()
+    ojs, raw = _oracle_js(rin), _oracle_js(rin, keyed=False)
+    L = O.lib()
+    dropped = 0
+    for n in range(rin.n_nodes):
+        exp = {}
+        for r in range(rin.n_rules):
+            if L.or_rule_on_node(raw, mode, r, n):
+                exp[(int(rin.rule_job[r]), js.rules[r].ID)] = r
+        got = [r for r in range(rin.n_rules) if L.or_rule_on_node(ojs, mode, r, n)]
+        assert got == sorted(exp.values()), (mode, n)
+        dropped += sum(L.or_rule_on_node(raw, mode, r, n) for r in range(rin.n_rules)) - len(got)
+    assert dropped > 0  # the world repeats keys
+
+
+def test_ingested_duplicate_and_blank_rule_ids():
+    """etcd values through the ingest path: Rule.IDs are never trimmed on the
+    node path (only Job.Check does, job.go:524-529), so "" repeats "" but not
+    " "; cross-job GetID collisions ("j"+"1x" vs "j1"+"x") are kept apart."""
+    import json
+    from cronsun_amd.ingest import EtcdJobSet
+    jobs = [
+        {"id": "j", "name": "a", "cmd": "true", "rules": [
+            {"id": "", "timer": "@daily", "nids": ["n1", "n2"]},
+            {"id": " ", "timer": "@hourly", "nids": ["n1"]},
+            {"id": "", "timer": "@weekly", "nids": ["n2", "n3"]},
+            {"id": "1x", "timer": "0 * * * * *", "gids": ["g"]}]},
+        {"id": "j1", "name": "b", "cmd": "true", "rules": [
+            {"id": "x", "timer": "@daily", "nids": ["n1"]},
+            {"id": "x", "timer": "@monthly", "gids": ["g"], "exclude_nids": ["n1"]}]},
+    ]
+    groups = [{"id": "g", "name": "g", "nids": ["n1", "n3"]}]
+    js = EtcdJobSet([json.dumps(j) for j in jobs], [json.dumps(g) for g in groups], threads=2)
+    rin = js.rules_in()
+    assert [js.rule_id(r) for r in range(rin.n_rules)] == [b"", b" ", b"", b"1x", b"x", b"x"]
+    ojs = _oracle_js(rin)
+    L = O.lib()
+    want = {"n1": [[0, 1, 3], [5]], "n2": [[2], []], "n3": [[2, 3], [5]]}
+    for nid, per_job in want.items():
+        n = js.node_index(nid)
+        for j in range(2):
+            assert js.cmds(j, nid) == per_job[j], (nid, j)
+            rules = [r for r in range(rin.n_rules) if rin.rule_job[r] == j]
+            assert [r for r in rules if L.or_rule_on_node(ojs, 0, r, n)] == per_job[j], (nid, j)
+    # RULE mode: rule 5 excludes n1, so rule 4 keeps its Cmd there
+    n1 = js.node_index("n1")
+    assert [r for r in (4, 5) if L.or_rule_on_node(ojs, 1, r, n1)] == [4]
 
 
 def test_rule_valid():
