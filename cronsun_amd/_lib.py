@@ -156,6 +156,12 @@ def _declare(L):
         "cg_expand_per_node_rules_device": ([vp, vp, vp, i64, i64, vp, C.c_int, P(i64), P(i64)],
                                             C.c_int),
         "cg_rule_nodes": ([vp, P(cg_rules_in), C.c_int, vp, vp, i64, P(i64)], C.c_int),
+        "cg_comm_unique_id": ([vp], C.c_int),
+        "cg_comm_init": ([vp, C.c_int, C.c_int, vp, P(vp)], C.c_int),
+        "cg_comm_free": ([vp], None),
+        "cg_comm_allgather_i64": ([vp, vp, sz, vp], C.c_int),
+        "cg_comm_node_offsets": ([vp, vp, vp], C.c_int),
+        "cg_comm_gather_node_csr": ([vp, C.c_int, i64, i64, vp, vp, vp, i64, P(i64)], C.c_int),
         "cg_jobset_new": ([P(vp)], C.c_int),
         "cg_jobset_free": ([vp], None),
         "cg_jobset_add_group": ([vp, C.c_char_p, vp, sz], C.c_int),

@@ -322,6 +322,15 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
                         bool in16);
 // the time-order pass over the last (rule-major) per-node result; c->mu held
 int order_by_time_locked(cg_ctx* c, bool in16 = false);
+// kernels of the per-node CSR gather (cg_pernode.hip), enqueued on st:
+// node n's events [src_off[n], src_off[n+1]) of src to dst_start[n] onwards /
+// n contiguous events / the last per-node result's counts per node
+int launch_node_place(cg_ctx* c, hipStream_t st, int32_t N, const int64_t* src_off, const int64_t* src_time,
+                      const int32_t* src_rule, int32_t rule_add, const int64_t* dst_start, int64_t* dst_time,
+                      int32_t* dst_rule);
+int launch_span_place(cg_ctx* c, hipStream_t st, int64_t n, const int64_t* src_time, const int32_t* src_rule,
+                      int32_t rule_add, int64_t* dst_time, int32_t* dst_rule);
+int launch_node_counts(cg_ctx* c, hipStream_t st, int64_t* d_counts);
 // CG_ORDER_LSD set: order every window by the LSD passes (int64 times; the
 // writer must not emit 16-bit offsets then)
 bool order_lsd_only();

@@ -732,6 +732,17 @@ __global__ __launch_bounds__(256) void k_node_place(const int64_t* __restrict__ 
   }
 }
 
+// n contiguous events copied to dst, rules shifted (a part of one node's slice
+// in the chunked gather, cg_comm.cpp)
+__global__ __launch_bounds__(256) void k_span_place(int64_t n, const int64_t* __restrict__ src_time,
+                                                     const int32_t* __restrict__ src_rule, int32_t rule_add,
+                                                     int64_t* __restrict__ dst_time, int32_t* __restrict__ dst_rule) {
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+    dst_time[i] = src_time[i];
+    dst_rule[i] = src_rule[i] + rule_add;
+  }
+}
+
 // persistent k_node_write grid: as many 4-wave blocks per CU as its register
 // and LDS use let run at once (no block of the grid waits for a slot)
 int node_write_blocks_per_cu() {
@@ -1517,6 +1528,35 @@ int cg_node_csr_place(cg_ctx* c, int32_t n_nodes, const int64_t* d_src_node_off,
   if ((rc = cg_hip_check(hipGetLastError(), "k_node_place"))) return rc;
   return cg_hip_check(hipStreamSynchronize(c->st), "sync");
 }
+
+}  // extern "C"
+
+// placement launchers for the RCCL gather (cg_comm.cpp); enqueued on st
+int launch_node_place(cg_ctx* c, hipStream_t st, int32_t N, const int64_t* src_off, const int64_t* src_time,
+                      const int32_t* src_rule, int32_t rule_add, const int64_t* dst_start, int64_t* dst_time,
+                      int32_t* dst_rule) {
+  if (N > 0)
+    hipLaunchKernelGGL(k_node_place, dim3(unsigned(std::min<int64_t>(N, int64_t(c->write_blocks) * 2))), dim3(256),
+                       0, st, src_off, N, src_time, src_rule, rule_add, dst_start, dst_time, dst_rule);
+  return cg_hip_check(hipGetLastError(), "k_node_place");
+}
+
+int launch_span_place(cg_ctx* c, hipStream_t st, int64_t n, const int64_t* src_time, const int32_t* src_rule,
+                      int32_t rule_add, int64_t* dst_time, int32_t* dst_rule) {
+  if (n > 0)
+    hipLaunchKernelGGL(k_span_place, dim3(unsigned(gridn(n, 256, c->write_blocks * 4))), dim3(256), 0, st, n,
+                       src_time, src_rule, rule_add, dst_time, dst_rule);
+  return cg_hip_check(hipGetLastError(), "k_span_place");
+}
+
+int launch_node_counts(cg_ctx* c, hipStream_t st, int64_t* d_counts) {
+  if (c->pn_N > 0)
+    hipLaunchKernelGGL(k_node_counts, dim3(gridn(c->pn_N, 256, 1 << 30)), dim3(256), 0, st, c->node_off.p,
+                       int32_t(c->pn_N), d_counts);
+  return cg_hip_check(hipGetLastError(), "k_node_counts");
+}
+
+extern "C" {
 
 int cg_node_counts_to_device(cg_ctx* c, int64_t* d_counts) {
   if (!c || !d_counts) return cg_fail(CG_EINVAL, "cg_node_counts_to_device: null");

@@ -69,6 +69,63 @@ class DeviceRules:
             pass
 
 
+class Comm:
+    """The library's RCCL communicator (cg_comm_*): one rank per MI355X, bound
+    to an Engine's device and stream.  unique_id() on rank 0, handed to every
+    rank (e.g. torch.distributed.broadcast_object_list), then Comm(engine,
+    world, rank, id) on every rank."""
+
+    @staticmethod
+    def unique_id():
+        buf = (C.c_uint8 * 128)()
+        check(lib().cg_comm_unique_id(buf))
+        return bytes(buf)
+
+    def __init__(self, engine, world, rank, uid):
+        if len(uid) != 128:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        self.engine, self.world, self.rank = engine, int(world), int(rank)
+        h = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+        check(lib().cg_comm_init(engine._h, self.world, self.rank, buf, C.byref(h)))
+        self._h = h
+
+    def allgather_i64(self, values):
+        """all[g, i] = rank g's values[i] (host int64)."""
+        mine = np.ascontiguousarray(values, dtype=np.int64)
+        out = np.zeros((self.world, mine.size), dtype=np.int64)
+        check(lib().cg_comm_allgather_i64(self._h, mine.ctypes.data, mine.size, out.ctypes.data))
+        return out
+
+    def node_offsets(self, n_nodes):
+        """(node_start [N], node_base [N+1]) of every rank's last per-node result
+        (the all-gather of per-node counts)."""
+        start = np.zeros(max(n_nodes, 1), dtype=np.int64)
+        base = np.zeros(n_nodes + 1, dtype=np.int64)
+        check(lib().cg_comm_node_offsets(self._h, start.ctypes.data, base.ctypes.data))
+        return start[:n_nodes], base
+
+    def gather_node_csr(self, root, rule_base, budget_bytes, d_node_off=0, d_time=0, d_rule=0, cap=0):
+        """cg_comm_gather_node_csr into device pointers (root); returns the
+        global node-event total."""
+        n = C.c_int64()
+        check(lib().cg_comm_gather_node_csr(self._h, int(root), int(rule_base), int(budget_bytes),
+                                            d_node_off or None, d_time or None, d_rule or None, int(cap),
+                                            C.byref(n)))
+        return n.value
+
+    def free(self):
+        if getattr(self, "_h", None):
+            lib().cg_comm_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
 class Dispatcher:
     """Cron.run's entries (node/cron/cron.go:210-275) resident in HBM
     (cg_dispatcher_*): slots with a schedule, Next and Prev."""
@@ -542,4 +599,4 @@ def device_count():
     return lib().cg_device_count()
 
 
-__all__ = ["Engine", "Specs", "Dispatcher", "RulesIn", "default_engine", "device_count", "CgError"]
+__all__ = ["Engine", "Specs", "Dispatcher", "RulesIn", "Comm", "default_engine", "device_count", "CgError"]

@@ -20,7 +20,11 @@ with no data-path collective.  The only exchanges are small:
   gather_node_csr  the same for the per-node CSR (north_star's "gather the
                    final per-node CSR"): every node's global list is the
                    ranks' slices of it in job-ID order, as one process walking
-                   all jobs builds it (node/node.go:121-158 -> Job.Cmds)
+                   all jobs builds it (node/node.go:121-158 -> Job.Cmds); in
+                   chunks of node ranges under a byte budget, so the
+                   destination stages at most the budget beside its output
+                   (the library's cg_comm_gather_node_csr does the same over
+                   RCCL behind the C-ABI)
 
 Works with torch.distributed over RCCL ("nccl", one process per MI355X) and
 over gloo on CPU (tests).
@@ -202,7 +206,52 @@ def place_node_slice(node_off, time, rule, rule_add, starts, out_time, out_rule,
             orl[st[n]:st[n] + b - a] = r[a:b] + rule_add
 
 
-def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst=0, engine=None):
+def node_gather_plan(allc, dst, budget_bytes):
+    """The chunks of the per-node CSR gather, the same on every rank (the
+    library's cg_comm_gather_node_csr plans identically, cg_comm.cpp): whole
+    node ranges [n0, n1) whose peer events (every rank but `dst`, 12 B each)
+    fit the budget, and a node with more peer events than that in k parts
+    (part j of rank g: its events [c*j//k, c*(j+1)//k) of that node).
+    allc: numpy int64 [world, N] per-node counts.  Returns [(n0, n1, j, k)]."""
+    allc = np.asarray(allc, dtype=np.int64)
+    world, N = allc.shape
+    cap_ev = int(budget_bytes) // 12
+    if world > 1 and cap_ev < 2 * world:
+        raise ValueError("gather budget below 24 bytes per rank")
+    P = allc.sum(axis=0) - allc[dst]
+    out = []
+    n = 0
+    while n < N:
+        if P[n] > cap_ev:
+            per = cap_ev - (world - 1)
+            k = (int(P[n]) + per - 1) // per
+            out += [(n, n + 1, j, k) for j in range(k)]
+            n += 1
+            continue
+        n0, acc = n, 0
+        while n < N and P[n] <= cap_ev and acc + P[n] <= cap_ev:
+            acc += int(P[n])
+            n += 1
+        if acc > 0:
+            out.append((n0, n, 0, 1))
+    return out
+
+
+def _piece(off_g, cnt_g, chunk):
+    """Rank g's events [lo, hi) of its own CSR in a chunk."""
+    n0, n1, j, k = chunk
+    a = int(off_g[n0])
+    if k == 1:
+        return a, int(off_g[n1])
+    c = int(cnt_g[n0])
+    return a + c * j // k, a + c * (j + 1) // k
+
+
+DEFAULT_GATHER_BUDGET = 1 << 31  # bytes of peer events staged on dst per chunk
+
+
+def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst=0, engine=None,
+                    budget_bytes=DEFAULT_GATHER_BUDGET):
     """Gather the per-node (time, rule) CSR of job-ID-range shards on rank `dst`.
 
     local_node_off: int64 tensor [N+1] (this rank's node offsets, from 0);
@@ -212,11 +261,14 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
     rule indices) on `dst`, None elsewhere.
 
     Sizes: one all-gather of the per-node counts (N int64 per rank, the
-    collective node_offsets uses).  Payload: one isend of each array per rank
-    into a staging buffer on `dst` (one xGMI link per peer, all in flight
-    together), then each rank's slice of node n is placed at
-    node_base[n] + sum_{g' < g} count[g'][n] by the library's placement
-    kernel (cg_node_csr_place; rule indices made global there)."""
+    collective node_offsets uses).  Payload: in chunks of node ranges
+    (node_gather_plan) whose peer events stay within budget_bytes, so dst
+    stages at most that much beside its output: per chunk every peer's piece
+    (one contiguous range of its CSR) moves with batched isend/irecv into a
+    staging buffer, then each piece is placed at node_base[n] +
+    sum_{g' < g} count[g'][n] by the library's placement kernel
+    (cg_node_csr_place; rule indices made global there).  dst's own slice is
+    placed straight from its buffers."""
     import torch
     world, rank = dist.get_world_size(), dist.get_rank()
     dev = local_time.device
@@ -225,38 +277,60 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
     allc = torch.zeros(world * N, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(allc, counts)
     allc = allc.view(world, N)
-    sizes = allc.sum(dim=1).cpu().numpy()
+    allc_h = allc.cpu().numpy()
     # every rank's range base (the placement makes rule indices global)
     base_t = torch.tensor([int(rule_base)], dtype=torch.int64, device=dev)
     bases = torch.zeros(world, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(bases, base_t)
     bases = bases.cpu().numpy()
+    offs = np.zeros((world, N + 1), dtype=np.int64)
+    offs[:, 1:] = np.cumsum(allc_h, axis=1)
+    plan = node_gather_plan(allc_h, dst, budget_bytes)
+    lt, lr = local_time.contiguous(), local_rule.contiguous()
     if rank != dst:
-        ops = [dist.P2POp(dist.isend, local_time.contiguous(), dst),
-               dist.P2POp(dist.isend, local_rule.contiguous(), dst)]
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
+        for ch in plan:
+            lo, hi = _piece(offs[rank], allc_h[rank], ch)
+            if hi > lo:
+                ops = [dist.P2POp(dist.isend, lt[lo:hi], dst), dist.P2POp(dist.isend, lr[lo:hi], dst)]
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
         return None
-    node_base = None
-    E = int(sizes.sum())
+    E = int(offs[:, -1].sum())
     out_time = torch.empty(E, dtype=torch.int64, device=dev)
     out_rule = torch.empty(E, dtype=torch.int32, device=dev)
-    stage, ops = {}, []
-    for g in range(world):
-        if g == dst:
-            stage[g] = (local_time.contiguous(), local_rule.contiguous())
-            continue
-        stage[g] = (torch.empty(int(sizes[g]), dtype=torch.int64, device=dev),
-                    torch.empty(int(sizes[g]), dtype=torch.int32, device=dev))
-        ops += [dist.P2POp(dist.irecv, stage[g][0], g), dist.P2POp(dist.irecv, stage[g][1], g)]
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-    for g in range(world):
-        starts, node_base = node_slice_starts(allc, g)
-        off = torch.zeros(N + 1, dtype=torch.int64, device=dev)
-        off[1:] = torch.cumsum(allc[g], dim=0)
-        if int(sizes[g]) > 0:
-            place_node_slice(off, stage[g][0], stage[g][1], int(bases[g]), starts, out_time, out_rule, engine)
-        stage[g] = None
+    starts = [node_slice_starts(allc, g)[0] for g in range(world)]
+    node_base = node_slice_starts(allc, dst)[1]
+    starts_h = [x.cpu().numpy() for x in starts]
+    if int(offs[dst, -1]) > 0:  # dst's own slice
+        place_node_slice(local_node_off, lt, lr, int(bases[dst]), starts[dst], out_time, out_rule, engine)
+    pieces = [[_piece(offs[g], allc_h[g], ch) if g != dst else (0, 0) for g in range(world)] for ch in plan]
+    stage_n = max([sum(hi - lo for lo, hi in p) for p in pieces] or [0])
+    stage_t = torch.empty(max(stage_n, 1), dtype=torch.int64, device=dev)
+    stage_r = torch.empty(max(stage_n, 1), dtype=torch.int32, device=dev)
+    for ch, pc in zip(plan, pieces):
+        ops, o = [], 0
+        for g in range(world):
+            lo, hi = pc[g]
+            if g != dst and hi > lo:
+                ops += [dist.P2POp(dist.irecv, stage_t[o:o + hi - lo], g),
+                        dist.P2POp(dist.irecv, stage_r[o:o + hi - lo], g)]
+            o += hi - lo
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        n0, n1, j, k = ch
+        o = 0
+        for g in range(world):
+            lo, hi = pc[g]
+            if g == dst or hi == lo:
+                continue
+            if k == 1:
+                off = torch.from_numpy(offs[g, n0:n1 + 1] - offs[g, n0]).to(dev)
+                place_node_slice(off, stage_t[o:o + hi - lo], stage_r[o:o + hi - lo], int(bases[g]),
+                                 starts[g][n0:n1], out_time, out_rule, engine)
+            else:
+                d = int(starts_h[g][n0]) + (lo - int(offs[g, n0]))
+                out_time[d:d + hi - lo] = stage_t[o:o + hi - lo]
+                out_rule[d:d + hi - lo] = stage_r[o:o + hi - lo] + int(bases[g])
+            o += hi - lo
     return node_base, out_time, out_rule

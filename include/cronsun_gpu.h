@@ -482,6 +482,56 @@ int cg_expand_per_node_rules_device_async(cg_ctx* ctx, const cg_specs* specs, co
  * *n_events_all (may be NULL): the node events of every window waited for. */
 int cg_expand_per_node_wait(cg_ctx* ctx, int64_t* n_events, int64_t* n_events_all);
 
+/* ------------------------------------------- multi-GPU (RCCL over xGMI) --- */
+/* One process (or thread) per MI355X, each with its own cg_ctx; rules shard
+ * by contiguous job-ID ranges with no data-path collective (every cronsun
+ * node filters every job itself, node/node.go:121-141; here a rank evaluates
+ * one range of jobs for every node).  The only exchanges (north_star) are the
+ * all-gather of per-node event counts / offsets and the gather of the final
+ * per-node CSR.  RCCL is loaded at run time (librccl.so.1 beside the HIP
+ * runtime the library links, else /opt/rocm/lib); CG_ENODEV if absent.
+ *
+ *   cg_comm_unique_id   ncclGetUniqueId: rank 0 makes the id, the caller
+ *                       hands it to every rank (any channel)
+ *   cg_comm_init        ncclCommInitRank on the ctx's device (collective)
+ *   cg_comm_allgather_i64  all[g*n + i] = rank g's mine[i] (host buffers;
+ *                       event totals -> global rule-major offsets, per-block
+ *                       weights of the event-balanced cut)
+ *   cg_comm_node_offsets   all-gather of the per-node event counts of every
+ *                       rank's last per-node result (N int64 per rank):
+ *                       node_start[n] = node_base[n] + the counts of the
+ *                       ranks before this one (where this rank's slice of
+ *                       node n lands in the job-ID-ordered global list),
+ *                       node_base[N+1] the global node offsets (host; either
+ *                       may be NULL)
+ *   cg_comm_gather_node_csr  every rank's last per-node result (rule order)
+ *                       gathered on `root` into the caller's DEVICE buffers
+ *                       d_node_off [N+1], d_time / d_rule [cap] (root only;
+ *                       ignored elsewhere): node n's global list is the ranks'
+ *                       slices in rank (= job-ID) order, rule indices made
+ *                       global by each rank's rule_base (its range's first
+ *                       global rule).  The payload moves in chunks of whole
+ *                       node ranges (a node larger than the budget in parts)
+ *                       whose peer bytes (12 B per event) stay within
+ *                       budget_bytes (the smallest any rank passes; at least
+ *                       24 B per rank), so root's staging is bounded by it;
+ *                       grouped ncclSend/ncclRecv per chunk, placed on root by
+ *                       a kernel.  Every rank returns the same status:
+ *                       CG_ECAPACITY when the total exceeds root's cap,
+ *                       CG_EINVAL when a rank's result is time-ordered or the
+ *                       node counts differ.  *n_events = the global total.
+ * Collective calls must be made by every rank of the comm, in the same order. */
+typedef struct cg_comm cg_comm;
+#define CG_COMM_ID_BYTES 128
+int cg_comm_unique_id(uint8_t id[CG_COMM_ID_BYTES]);
+int cg_comm_init(cg_ctx* ctx, int world, int rank, const uint8_t id[CG_COMM_ID_BYTES], cg_comm** out);
+void cg_comm_free(cg_comm* comm);
+int cg_comm_allgather_i64(cg_comm* comm, const int64_t* mine, size_t n, int64_t* all);
+int cg_comm_node_offsets(cg_comm* comm, int64_t* node_start, int64_t* node_base);
+int cg_comm_gather_node_csr(cg_comm* comm, int root, int64_t rule_base, int64_t budget_bytes,
+                            int64_t* d_node_off, int64_t* d_time, int32_t* d_rule, int64_t cap,
+                            int64_t* n_events);
+
 /* rule -> node CSR only (GPU join), host output */
 int cg_rule_nodes(cg_ctx* ctx, const cg_rules_in* rules, int mode, int64_t* rn_off /*[R+1]*/,
                   int32_t* rn_nodes, int64_t cap, int64_t* nnz);

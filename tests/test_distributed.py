@@ -159,14 +159,14 @@ def _node_csr_oracle(rin, mode, specs, t0, t1):
             np.concatenate(rs).astype(np.int32))
 
 
-def _gather_worker(rank, world, port, outdir, mode):
+def _gather_worker(rank, world, port, outdir, mode, budget):
     import torch
     import torch.distributed as dist
     from cronsun_amd import synth
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    rin = synth.multi_rule_jobs(160, seed=5)
+    rin = synth.multi_rule_jobs(160, seed=5, key_choices=2)
     specs = synth.spec_mix(rin.n_rules, seed=6, mix=synth.MIX_LIGHT)
     # job-ID-range shards: cut at the job boundaries nearest to equal rule counts
     starts = np.concatenate([[0], np.nonzero(np.diff(rin.rule_job))[0] + 1, [rin.n_rules]])
@@ -175,28 +175,69 @@ def _gather_worker(rank, world, port, outdir, mode):
     lo, hi = cuts[rank], cuts[rank + 1]
     part = rin.slice_rules(lo, hi)
     off, t, r = _node_csr_oracle(part, mode, specs[lo:hi], T0, T0 + DAY)
-    g = shard.gather_node_csr(torch.from_numpy(off), torch.from_numpy(t), torch.from_numpy(r), lo, dist)
+    g = shard.gather_node_csr(torch.from_numpy(off), torch.from_numpy(t), torch.from_numpy(r), lo, dist,
+                              budget_bytes=budget)
+    cnt = torch.from_numpy(np.diff(off))
+    allc = torch.zeros(world * rin.n_nodes, dtype=torch.int64)
+    dist.all_gather_into_tensor(allc, cnt)
+    plan = shard.node_gather_plan(allc.view(world, -1).numpy(), 0, budget)
     if g is not None:
         np.savez(os.path.join(outdir, f"g{rank}.npz"), node_off=g[0].numpy(), time=g[1].numpy(),
-                 rule=g[2].numpy())
+                 rule=g[2].numpy(), plan=np.array(plan, dtype=np.int64).reshape(-1, 4))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("mode", [0, 2])
-def test_gather_node_csr_gloo(tmp_path, mode):
+@pytest.mark.parametrize("mode,budget", [(0, shard.DEFAULT_GATHER_BUDGET), (2, shard.DEFAULT_GATHER_BUDGET),
+                                         (0, 12 * 700), (1, 12 * 3000)])
+def test_gather_node_csr_gloo(tmp_path, mode, budget):
     """north_star's per-node CSR gather: job-ID-range shards, each with its
     own per-node lists, gathered on rank 0 into exactly the per-node CSR of the
-    unsharded rule set (world_size 3, exclude modes none and cumulative)."""
+    unsharded rule set (world_size 3, three exclude modes; Rule.IDs repeat
+    inside jobs, so Job.Cmds' key drops rules).  Small budgets force the
+    chunked transfer: several node-range chunks and nodes split into parts."""
     import torch.multiprocessing as mp
     from cronsun_amd import synth
     world = 3
-    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
+    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path), mode, budget), nprocs=world, join=True)
     got = np.load(tmp_path / "g0.npz")
     assert not (tmp_path / "g1.npz").exists()
-    rin = synth.multi_rule_jobs(160, seed=5)
+    plan = got["plan"]
+    if budget < shard.DEFAULT_GATHER_BUDGET:
+        assert len(plan) >= 3 and (plan[:, 3] > 1).any() and (plan[:, 3] == 1).any(), plan
+    else:
+        assert len(plan) == 1
+    rin = synth.multi_rule_jobs(160, seed=5, key_choices=2)
     specs = synth.spec_mix(rin.n_rules, seed=6, mix=synth.MIX_LIGHT)
     exp = _node_csr_oracle(rin, mode, specs, T0, T0 + DAY)
     assert np.array_equal(got["node_off"], exp[0])
     assert np.array_equal(got["time"], exp[1])
     assert np.array_equal(got["rule"], exp[2])
+
+
+@pytest.mark.parametrize("world,dst", [(2, 0), (3, 1), (8, 0)])
+def test_node_gather_plan_covers_every_event_within_budget(world, dst):
+    """The chunk plan (shared by shard.gather_node_csr and the library's
+    cg_comm_gather_node_csr): every peer event is in exactly one piece, pieces
+    of a rank are contiguous and in order, and no chunk exceeds the budget."""
+    rng = np.random.default_rng(world)
+    N = 500
+    allc = rng.integers(0, 40, (world, N))
+    allc[:, rng.integers(0, N, 5)] = rng.integers(500, 3000, (world, 5))  # a few big nodes
+    for budget in (12 * 2 * world, 12 * 97, 12 * 1000, 12 * 10**9):
+        plan = shard.node_gather_plan(allc, dst, budget)
+        offs = np.zeros((world, N + 1), dtype=np.int64)
+        offs[:, 1:] = np.cumsum(allc, axis=1)
+        nxt = [0] * world
+        for ch in plan:
+            tot = 0
+            for g in range(world):
+                if g == dst:
+                    continue
+                lo, hi = shard._piece(offs[g], allc[g], ch)
+                if hi > lo:
+                    assert lo == nxt[g], (budget, ch, g)
+                    nxt[g] = hi
+                tot += hi - lo
+            assert 0 < tot * 12 <= budget, (budget, ch)
+        assert all(nxt[g] == offs[g, -1] for g in range(world) if g != dst)

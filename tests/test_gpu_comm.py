@@ -1,0 +1,71 @@
+"""The library's RCCL exchanges behind the C-ABI (cg_comm_*, cg_comm.cpp) on
+one MI355X: a world-1 communicator (one GPU per rank; RCCL refuses two ranks
+on one device, so the N > 1 paths are covered by the same chunk plan in the
+gloo tests, tests/test_distributed.py, and run on the driver's 8-GPU node).
+
+World 1 runs every collective for real: the all-gather of host values, the
+per-node counts all-gather behind cg_comm_node_offsets, and the gather of the
+per-node CSR (root's own slice placed by the kernel into caller buffers),
+plus the status every rank must agree on (capacity, time-ordered input)."""
+import numpy as np
+import pytest
+
+from cronsun_amd import _lib, cron, synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def world1():
+    from cronsun_amd.engine import Comm, Engine
+    eng = Engine(0)
+    comm = Comm(eng, 1, 0, Comm.unique_id())
+    yield eng, comm
+    comm.free()
+    eng.close()
+
+
+def test_allgather_i64_world1(world1):
+    eng, comm = world1
+    v = np.array([5, -7, 1 << 40], dtype=np.int64)
+    assert np.array_equal(comm.allgather_i64(v), v[None, :])
+
+
+def test_node_offsets_and_gather_world1(world1):
+    import torch
+    eng, comm = world1
+    rin = synth.multi_rule_jobs(500, seed=77, key_choices=2)
+    specs = synth.spec_mix(rin.n_rules, seed=78, mix=synth.MIX_CONFIG2)
+    scheds = [cron.Parse(s) for s in specs]
+    t0 = synth.T0_2026 + 5 * 86400
+    node_off, time, rule = eng.expand_per_node(scheds, None, t0, t0 + 3600, rin, _lib.EXCLUDE_NONE)
+    E = int(node_off[-1])
+    assert E > 10000
+    start, base = comm.node_offsets(rin.n_nodes)
+    assert np.array_equal(base, node_off) and np.array_equal(start, node_off[:-1])
+    dev = torch.device("cuda", 0)
+    o = torch.empty(rin.n_nodes + 1, dtype=torch.int64, device=dev)
+    t = torch.full((E,), -1, dtype=torch.int64, device=dev)
+    r = torch.full((E,), -1, dtype=torch.int32, device=dev)
+    for budget in (24, 1 << 30):
+        t.fill_(-1)
+        r.fill_(-1)
+        torch.cuda.synchronize(dev)
+        n = comm.gather_node_csr(0, 1000, budget, o.data_ptr(), t.data_ptr(), r.data_ptr(), E)
+        assert n == E
+        assert np.array_equal(o.cpu().numpy(), node_off)
+        assert np.array_equal(t.cpu().numpy(), time)
+        assert np.array_equal(r.cpu().numpy(), rule + 1000)  # rule_base makes rule indices global
+    # too small a capacity: CG_ECAPACITY, the total still reported
+    with pytest.raises(_lib.CgError) as err:
+        comm.gather_node_csr(0, 0, 1 << 30, o.data_ptr(), t.data_ptr(), r.data_ptr(), E - 1)
+    assert err.value.code == _lib.CG_ECAPACITY
+    # a time-ordered result is refused (its slices would not merge by concatenation)
+    eng.set_node_order(_lib.NODE_ORDER_TIME)
+    try:
+        eng.expand_per_node(scheds, None, t0, t0 + 3600, rin, _lib.EXCLUDE_NONE)
+        with pytest.raises(_lib.CgError) as err:
+            comm.gather_node_csr(0, 0, 1 << 30, o.data_ptr(), t.data_ptr(), r.data_ptr(), E)
+        assert err.value.code == _lib.CG_EINVAL
+    finally:
+        eng.set_node_order(_lib.NODE_ORDER_RULE)
