@@ -318,8 +318,14 @@ bool pn_async_pending(const cg_ctx* c);  // an asynchronous expansion not yet wa
 // time-order tile sort + merge of c->node_time / c->node_rule (windows <= 4096 s;
 // cg_node_order.hip), enqueued on st without a host sync
 // (in16: the lists' times are 16-bit offsets t - t0 - 1, written by k_node_write<.., true>)
+// err: a device word the kernels set when a sorted chunk is out of (time,
+// rule) order (the sorts' ranks rest on lane-ordered LDS atomics; checked)
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
-                        bool in16);
+                        bool in16, int64_t* err);
+constexpr const char* kOrderCheckMsg =
+    "time-order pass: a sorted chunk came out of (time, rule) order (its LDS-atomic ranks were not in lane order)";
+// the mapped pinned per-node result words: [0] node events, [1] size error, [2] order check
+int pn_ensure_res(cg_ctx* c);
 // the time-order pass over the last (rule-major) per-node result; c->mu held
 int order_by_time_locked(cg_ctx* c, bool in16 = false);
 // kernels of the per-node CSR gather (cg_pernode.hip), enqueued on st:

@@ -339,13 +339,22 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, uint32
   ot_sync<NW>();
 }
 
+// two neighbours u, v of a sorted chunk (packed offset << 12 | index, rules in
+// rl by index) out of (time, rule) order: a rule fires once per second, so
+// equal offsets need strictly ascending rules
+__device__ __forceinline__ bool ot_out_of_order(uint32_t u, uint32_t v, const int32_t* rl) {
+  const uint32_t a = u >> kOtIdxBits, b = v >> kOtIdxBits;
+  return a > b || (a == b && rl[u & kOtIdxMask] >= rl[v & kOtIdxMask]);
+}
+
 template <bool IN16>  // times as 16-bit offsets t - t0 - 1 (else int64 times, their low words read)
 __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ time, const int32_t* __restrict__ rule,
                                                   const int32_t* __restrict__ tile_node,
                                                   const int64_t* __restrict__ tile_base,
                                                   const int64_t* __restrict__ node_off, int64_t t0,
                                                   uint16_t* __restrict__ toff_out, int32_t* __restrict__ rule_out,
-                                                  int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles) {
+                                                  int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles,
+                                                  int64_t* __restrict__ err) {
   __shared__ OtRank<4, 64> s;
   __shared__ uint32_t pk[kOtTile];
   __shared__ int32_t rl[kOtTile];
@@ -380,11 +389,24 @@ __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ tim
   else ot_sort<4, 64, true>(key, n, 0u, kOtSlabBits, 1, pk, s);
   int32_t* __restrict__ pt = pre + t * kOtPre;
   if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];  // slabs = the last pass's digits
+  bool bad = false;
   for (int p = threadIdx.x; p < n; p += 256) {
     const uint32_t v = pk[p];
     toff_out[r.lo + p] = uint16_t(v >> kOtIdxBits);
     __builtin_nontemporal_store(rl[v & kOtIdxMask], rule_out + r.lo + p);
+    // the ranks rest on lane-ordered LDS atomics (ot_rank): check the order
+    // they produced -- a node's only tile is final: (offset, rule) ascending;
+    // a partitioned tile keeps rule order inside each slab
+    if (p > 0) {
+      const uint32_t u = pk[p - 1];
+      if (one) bad |= ot_out_of_order(u, v, rl);
+      else if ((u >> (kOtIdxBits + kOtSlabBits)) == (v >> (kOtIdxBits + kOtSlabBits))) {
+        const int32_t ru = rl[u & kOtIdxMask], rv = rl[v & kOtIdxMask];  // rule-major: (rule, offset)
+        bad |= ru > rv || (ru == rv && (u >> kOtIdxBits) >= (v >> kOtIdxBits));
+      }
+    }
   }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
 }
 
 // Exclusive scan of cnt(q) for q in [0, Q) (Q <= kOtMaxTiles) into ps[0..Q]
@@ -563,7 +585,8 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restr
                                                        const int32_t* __restrict__ pre, int32_t N, int64_t t0,
                                                        const int64_t* __restrict__ slab_tab,
                                                        int64_t* __restrict__ tout, int32_t* __restrict__ rout,
-                                                       int64_t* __restrict__ big, unsigned* __restrict__ big_n) {
+                                                       int64_t* __restrict__ big, unsigned* __restrict__ big_n,
+                                                       int64_t* __restrict__ err) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * kOtItems;
   __shared__ OtRank<NW, 256> s;
   __shared__ uint32_t pk[kChunk + kChunk / 32];  // the owner list while gathering (padded), then the sorted words
@@ -629,11 +652,14 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restr
       // 8-bit pass for up to 4 slabs
       ot_sort<NW, 256>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
       const int64_t o = lo_n + slab_off[ja];
+      bool bad = false;
       for (int p = threadIdx.x; p < n_el; p += kThreads) {
         const uint32_t v = pk[p];
         __builtin_nontemporal_store(t0 + 1 + int64_t(v >> kOtIdxBits), tout + o + p);
         __builtin_nontemporal_store(rl[v & kOtIdxMask], rout + o + p);
+        if (p > 0) bad |= ot_out_of_order(pk[p - 1], v, rl);  // (time, rule) order of the chunk
       }
+      if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
       ot_sync<NW>();
     }
     ja = ja2;
@@ -651,7 +677,8 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
                                                  const int64_t* __restrict__ node_off,
                                                  const int32_t* __restrict__ pre, int64_t t0,
                                                  int64_t* __restrict__ tout, int32_t* __restrict__ rout,
-                                                 const int64_t* __restrict__ big, const unsigned* __restrict__ big_n) {
+                                                 const int64_t* __restrict__ big, const unsigned* __restrict__ big_n,
+                                                 int64_t* __restrict__ err) {
   __shared__ OtRank<4, 64> s;
   __shared__ uint32_t pk[kOtTile + kOtTile / 32];
   __shared__ int32_t rl[kOtTile];
@@ -724,13 +751,16 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
         ot_gather<true>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc, own, c0, n_el, key, rl);
         ot_sort<4, 64>(key, n_el, uint32_t(j) << kOtSlabBits, 0, 1, pk, s);
+        bool bad = false;
         for (int p = threadIdx.x; p < n_el; p += 256) {
           const uint32_t v = pk[p];
           const uint32_t d = (v >> kOtIdxBits) & kSec;
           const int64_t dst = gbase[d] + (p - s.dbase[d]);
           tout[dst] = t0 + 1 + int64_t(v >> kOtIdxBits);
           rout[dst] = rl[v & kOtIdxMask];
+          if (p > 0) bad |= ot_out_of_order(pk[p - 1], v, rl);
         }
+        if (__ballot(bad) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
         __syncthreads();
         if (threadIdx.x < 64) gbase[threadIdx.x] += s.dbase[threadIdx.x + 1] - s.dbase[threadIdx.x];
         __syncthreads();
@@ -750,7 +780,7 @@ int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads
 // cg_node_result_order_by_time and by the per-node calls in time order
 // (pipelined windows included).
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
-                        bool in16) {
+                        bool in16, int64_t* err) {
   if (N == 0 || cap == 0) return CG_OK;
   const int64_t Tmax = cap / kOtTile + N + 1;
   const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
@@ -773,21 +803,21 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   if (in16)
     hipLaunchKernelGGL(k_ot_tile<true>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
                        c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
-                       c->ts_base.p + N);
+                       c->ts_base.p + N, err);
   else
     hipLaunchKernelGGL(k_ot_tile<false>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
                        c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
-                       c->ts_base.p + N);
+                       c->ts_base.p + N, err);
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
   HIPCHK(hipMemsetAsync(big_n, 0, 8, st));
   int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
   hipLaunchKernelGGL(k_ot_merge<kOtMergeWaves>, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
                      c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
-                     c->node_rule.p, c->ts_off.p, big_n);
+                     c->node_rule.p, c->ts_off.p, big_n, err);
   hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
                      c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
-                     c->ts_off.p, big_n);
+                     c->ts_off.p, big_n, err);
   return cg_hip_check(hipGetLastError(), "time-order kernels");
 }
 
@@ -827,10 +857,13 @@ int order_by_time_locked(cg_ctx* c, bool in16) {
 
   // windows <= 4096 s: tile sort + merge (CG_ORDER_LSD=1: the LSD passes)
   if (bits <= 12 && !order_lsd_only()) {
+    if ((rc = pn_ensure_res(c))) return rc;
+    c->pn_res_host[2] = 0;
     (void)hipEventRecord(c->pev[0], st);
-    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, st, in16))) return rc;
+    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, st, in16, c->pn_res_dev + 2))) return rc;
     (void)hipEventRecord(c->pev[1], st);
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
+    if (c->pn_res_host[2]) return cg_fail(CG_EHIP, kOrderCheckMsg);
     (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);
     c->pn_time_ordered = true;
     return CG_OK;

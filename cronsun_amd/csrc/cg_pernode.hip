@@ -1005,11 +1005,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     c->pn_B = B;
     c->pn_K = K;
   }
-  if (!c->pn_res_host) {
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pn_res_host), 16,
-                         hipHostMallocMapped | hipHostMallocCoherent));
-    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pn_res_dev), c->pn_res_host, 0));
-  }
+  if ((rc = pn_ensure_res(c))) return rc;
   if ((rc = c->seg_nrec.ensure(std::max<int64_t>(NK, 1))) ||
       (rc = c->recs.ensure(std::max<int64_t>(nnz, 1))) ||
       (rc = c->rule_info.ensure(std::max<int64_t>(R, 1))))
@@ -1146,6 +1142,9 @@ void pn_check_set(cg_ctx* c, PnAsyncSet& a) {
     c->pa_msg = "per-node async window (" + std::to_string(a.t0) + ", " + std::to_string(a.t1) + "]: " +
                 std::to_string(E) + " rule-major events exceed the capacity " + std::to_string(a.rm_cap) +
                 " (run a synchronous per-node call on a window this large first)";
+  } else if (a.res_host[2] != 0) {
+    c->pa_rc = CG_EHIP;
+    c->pa_msg = kOrderCheckMsg;
   } else if (a.res_host[1] != 0) {
     c->pa_rc = CG_ERANGE;
     c->pa_msg = "per-node output: a (node, rule band) segment or a band's fire lists exceed 2^30 events";
@@ -1166,11 +1165,11 @@ int pn_ensure_async(cg_ctx* c) {
     HIPCHK(hipEventCreateWithFlags(&a.written, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&a.nw0, hipEventDisableSystemFence));
     HIPCHK(hipEventCreateWithFlags(&a.nw1, hipEventDisableSystemFence));
-    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&a.res_host), 16, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&a.res_host), 32, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.res_dev), a.res_host, 0));
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&a.rm.res_host), 16, hipHostMallocMapped | hipHostMallocCoherent));
     HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&a.rm.res_dev), a.rm.res_host, 0));
-    a.res_host[0] = a.res_host[1] = 0;
+    a.res_host[0] = a.res_host[1] = a.res_host[2] = 0;
     a.rm.res_host[0] = 0;
     a.rm.res_host[1] = -1;
   }
@@ -1178,6 +1177,14 @@ int pn_ensure_async(cg_ctx* c) {
 }
 
 }  // namespace
+
+int pn_ensure_res(cg_ctx* c) {
+  if (c->pn_res_host) return CG_OK;
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&c->pn_res_host), 32, hipHostMallocMapped | hipHostMallocCoherent));
+  HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&c->pn_res_dev), c->pn_res_host, 0));
+  c->pn_res_host[0] = c->pn_res_host[1] = c->pn_res_host[2] = 0;
+  return CG_OK;
+}
 
 bool pn_async_pending(const cg_ctx* c) {
   for (const PnAsyncSet& a : c->pns)
@@ -1240,6 +1247,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     return rc;
   a.res_host[0] = 0;
   a.res_host[1] = 0;
+  a.res_host[2] = 0;
   if (empty) {  // no rules: every list empty
     a.rm.res_host[0] = 0;
     a.rm.res_host[1] = -1;
@@ -1292,7 +1300,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
                        c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N, K, B,
                        node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
     // (time, rule) order: the tile sort + merge after the writer, same stream
-    if (timed && (rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st, true))) return rc;
+    if (timed && (rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st, true, a.res_dev + 2))) return rc;
   }
   (void)hipEventRecord(a.nw1, st);
   HIPCHK(hipEventRecord(a.written, st));

@@ -506,3 +506,91 @@ func (d *Dispatcher) Remove(idx []int64) error {
 	}
 	return nil
 }
+
+// Comm is the library's RCCL communicator (cg_comm_*): one rank per MI355X of
+// a node, each with its own Engine.  Rules shard by job-ID range (every
+// cronsun node filters every job, node/node.go:121-141; a rank here evaluates
+// one range of jobs for every node), and the only exchanges are the
+// all-gather of per-node counts and the gather of the per-node CSR.
+//
+//	id, _ := gpu.CommUniqueID()            // rank 0; hand it to every rank
+//	c, _ := gpu.NewComm(eng, world, rank, id)
+//	... eng.ExpandPerNode over the rank's jobs ...
+//	start, base, _ := c.NodeOffsets(nNodes) // where this rank's slices land
+//	n, _ := c.GatherNodeCSR(0, ruleBase, 1<<31, dOff, dTime, dRule, cap)
+type Comm struct {
+	c *C.cg_comm
+	e *Engine // cg_comm_free locks the engine's context: keep it reachable
+}
+
+// CommUniqueID is ncclGetUniqueId: made once (rank 0) and passed to every rank.
+func CommUniqueID() ([C.CG_COMM_ID_BYTES]byte, error) {
+	var id [C.CG_COMM_ID_BYTES]byte
+	cid := (*C.uint8_t)(C.malloc(C.CG_COMM_ID_BYTES))
+	defer C.free(unsafe.Pointer(cid))
+	if rc := C.cg_comm_unique_id(cid); rc != 0 {
+		return id, lastErr(rc)
+	}
+	copy(id[:], unsafe.Slice((*byte)(unsafe.Pointer(cid)), C.CG_COMM_ID_BYTES))
+	return id, nil
+}
+
+// NewComm is ncclCommInitRank on the engine's device (collective: every rank
+// calls it with the same id).
+func NewComm(e *Engine, world, rank int, id [C.CG_COMM_ID_BYTES]byte) (*Comm, error) {
+	cid := (*C.uint8_t)(C.malloc(C.CG_COMM_ID_BYTES))
+	defer C.free(unsafe.Pointer(cid))
+	copy(unsafe.Slice((*byte)(unsafe.Pointer(cid)), C.CG_COMM_ID_BYTES), id[:])
+	var c *C.cg_comm
+	if rc := C.cg_comm_init(e.ctx, C.int(world), C.int(rank), cid, &c); rc != 0 {
+		return nil, lastErr(rc)
+	}
+	cm := &Comm{c, e}
+	runtime.SetFinalizer(cm, func(cm *Comm) { C.cg_comm_free(cm.c) })
+	return cm, nil
+}
+
+// AllGather returns every rank's values (rank-major), e.g. the event totals
+// that place each rank's rule-major CSR in the global one.
+func (cm *Comm) AllGather(mine []int64, world int) ([]int64, error) {
+	defer runtime.KeepAlive(cm)
+	all := make([]int64, len(mine)*world)
+	if len(mine) == 0 {
+		return all, nil
+	}
+	rc := C.cg_comm_allgather_i64(cm.c, (*C.int64_t)(unsafe.Pointer(&mine[0])), C.size_t(len(mine)),
+		(*C.int64_t)(unsafe.Pointer(&all[0])))
+	if rc != 0 {
+		return nil, lastErr(rc)
+	}
+	return all, nil
+}
+
+// NodeOffsets all-gathers the per-node counts of every rank's last per-node
+// result: start[n] is where this rank's slice of node n lands in the global
+// list, base[N+1] the global node offsets.
+func (cm *Comm) NodeOffsets(nNodes int) (start, base []int64, err error) {
+	defer runtime.KeepAlive(cm)
+	start, base = make([]int64, nNodes+1), make([]int64, nNodes+1)
+	rc := C.cg_comm_node_offsets(cm.c, (*C.int64_t)(unsafe.Pointer(&start[0])), (*C.int64_t)(unsafe.Pointer(&base[0])))
+	if rc != 0 {
+		return nil, nil, lastErr(rc)
+	}
+	return start[:nNodes], base, nil
+}
+
+// GatherNodeCSR gathers every rank's last per-node result (rule order) on
+// root into device buffers (root only; pass 0 elsewhere), in chunks whose peer
+// bytes stay within budget; ruleBase is this rank's first global rule.
+// Returns the global node-event total.
+func (cm *Comm) GatherNodeCSR(root int, ruleBase, budget int64, dOff, dTime, dRule uintptr, cap int64) (int64, error) {
+	defer runtime.KeepAlive(cm)
+	var n C.int64_t
+	rc := C.cg_comm_gather_node_csr(cm.c, C.int(root), C.int64_t(ruleBase), C.int64_t(budget),
+		(*C.int64_t)(unsafe.Pointer(dOff)), (*C.int64_t)(unsafe.Pointer(dTime)), (*C.int32_t)(unsafe.Pointer(dRule)),
+		C.int64_t(cap), &n)
+	if rc != 0 {
+		return int64(n), lastErr(rc)
+	}
+	return int64(n), nil
+}
