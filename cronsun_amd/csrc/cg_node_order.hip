@@ -769,45 +769,238 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
   }
 }
 
+// ---- the per-node writer fused with the tile sort (time order, windows <= 4096 s) ----
+//
+// k_node_write<.., OFF16> followed by k_ot_tile wrote every event's 16-bit
+// offset and rule rule-major (6 B), then read them back to partition each
+// node-aligned 4096-event tile by slab.  k_node_tile builds a tile's events in
+// LDS straight from the segment records (k_seg_records: {rule, first
+// position, x, stride}; a progression's fire at segment position p is
+// t0 + x + p * stride, another rule's the band's rule-major fire list at
+// x + p) and partitions them there: 12 B per event less, one launch less.
+//
+// k_tile_rec_start: per tile, the segment holding its first position and the
+// record covering it (binary searches, one thread per tile).
+__global__ void k_tile_rec_start(const int64_t* __restrict__ seg_pos, const int64_t* __restrict__ seg_pair,
+                                 const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, int32_t K,
+                                 const int32_t* __restrict__ tile_node, const int64_t* __restrict__ tile_base,
+                                 const int64_t* __restrict__ node_off, const int64_t* __restrict__ n_tiles,
+                                 int64_t* __restrict__ tile_start) {
+  const int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (t >= *n_tiles) return;
+  const int32_t n = tile_node[t];
+  const int64_t X = node_off[n] + (t - tile_base[n]) * kOtTile;  // the tile's first position
+  int64_t lo = int64_t(n) * K, hi = lo + K - 1;  // last segment starting at or before X
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (seg_pos[mid] <= X) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t p0 = seg_pair[lo];
+  const int32_t rel = int32_t(X - seg_pos[lo]);
+  int32_t a = 0, b = seg_nrec[lo] - 1;  // last record whose first position is <= rel
+  while (a < b) {
+    const int32_t mid = (a + b + 1) >> 1;
+    if (recs[p0 + mid].dst <= rel) a = mid;
+    else b = mid - 1;
+  }
+  tile_start[2 * t] = lo;
+  tile_start[2 * t + 1] = a;
+}
+
+constexpr int kNtRecs = 512;  // records staged per pass
+constexpr int kNtSegs = 256;  // segments per window
+
+__global__ __launch_bounds__(256) void k_node_tile(
+    const int64_t* __restrict__ seg_pos, const int64_t* __restrict__ seg_pair, const int32_t* __restrict__ seg_nrec,
+    const PairRec* __restrict__ recs, const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times,
+    int64_t times_cap, int32_t K, int32_t B, int64_t t0, const int32_t* __restrict__ tile_node, const int64_t* __restrict__ tile_base,
+    const int64_t* __restrict__ node_off, const int64_t* __restrict__ tile_start, uint16_t* __restrict__ toff_out,
+    int32_t* __restrict__ rule_out, int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles,
+    int64_t* __restrict__ err) {
+  __shared__ OtRank<4, 64> s;
+  __shared__ uint32_t pk[kOtTile + kOtTile / 32];  // the pass's owner map (padded), then the sorted words
+  __shared__ int32_t rl[kOtTile];
+  __shared__ int4 tab[kNtRecs];            // per staged record {x, stride, window segment, rule}
+  __shared__ int32_t ps[kNtRecs + 1];      // its first position relative to the pass
+  __shared__ int32_t sg_cnt[kNtSegs + 1];  // records of the window's segments before segment j
+  __shared__ int64_t sg_rec[kNtSegs];      // global index of segment j's first record in the window
+  __shared__ int64_t sg_band[kNtSegs];     // band_lo of segment j (fire-list base of its gathers)
+  __shared__ int32_t sg_S[kNtSegs + 1];    // node-relative first position of segment j
+  __shared__ int32_t wsum[4];
+  int32_t* own = reinterpret_cast<int32_t*>(pk);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t t = blockIdx.x;
+  if (t >= *n_tiles) return;  // the grid is an upper bound (pipelined windows)
+  const int32_t n = tile_node[t];
+  const int64_t lo_n = node_off[n], E_n = node_off[n + 1] - lo_n;
+  const int32_t P = int32_t((t - tile_base[n]) * kOtTile);  // node-relative (a node holds < 2^30 events per band)
+  const int n_el = int(E_n - P < kOtTile ? E_n - P : kOtTile);
+  const int32_t hi_t = P + n_el;
+  const int ebase = w * (64 * kOtItems);
+  const int64_t s_end = int64_t(n) * K + K;
+  int64_t s_cur = tile_start[2 * t];
+  int32_t i_cur = int32_t(tile_start[2 * t + 1]);
+  uint32_t key[kOtItems];
+  int32_t done = P;  // positions below are computed
+  bool bad = false;
+  while (done < hi_t && s_cur < s_end) {
+    // a window of up to kNtSegs segments from s_cur (the first from record i_cur)
+    {
+      const int j = threadIdx.x;
+      const int64_t sj = s_cur + j;
+      int32_t cnt = 0;
+      if (sj < s_end) {
+        const int32_t S = int32_t(seg_pos[sj] - lo_n);
+        if (S < hi_t) {
+          const int32_t first = j == 0 ? i_cur : 0;
+          cnt = seg_nrec[sj] - first;
+          sg_rec[j] = seg_pair[sj] + first;
+          sg_band[j] = rule_off[int64_t(sj - int64_t(n) * K) * B];
+        }
+        sg_S[j] = S;
+      }
+      // exclusive block scan of cnt
+      int32_t inc = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) wsum[w] = inc;
+      __syncthreads();
+      int32_t before = 0;
+      for (int ww = 0; ww < w; ww++) before += wsum[ww];
+      sg_cnt[j] = before + inc - cnt;
+      if (j == 255) sg_cnt[kNtSegs] = before + inc;
+      __syncthreads();
+    }
+    const int32_t Wn = sg_cnt[kNtSegs];
+    // segment j's end: the next segment's start, or the node's end
+    auto seg_end = [&](int j) -> int32_t {
+      const int64_t sj = s_cur + j + 1;
+      return sj < s_end ? (j + 1 < kNtSegs ? sg_S[j + 1] : int32_t(seg_pos[sj] - lo_n)) : int32_t(E_n);
+    };
+    for (int32_t fb = 0; fb < Wn && done < hi_t; fb += kNtRecs) {
+      const int nr = Wn - fb < kNtRecs ? int(Wn - fb) : kNtRecs;
+      int32_t pass_end = 0;
+      // stage the pass's records: first positions, and {x, stride, segment, rule}
+      for (int f = threadIdx.x; f < nr; f += 256) {
+        const int32_t fg = fb + f;
+        int a = 0, b = kNtSegs - 1;  // the segment holding flattened record fg
+        while (a < b) {
+          const int mid = (a + b + 1) >> 1;
+          if (sg_cnt[mid] <= fg) a = mid;
+          else b = mid - 1;
+        }
+        const int64_t g = sg_rec[a] + (fg - sg_cnt[a]);
+        const PairRec r = recs[g];
+        ps[f] = sg_S[a] + r.dst;
+        tab[f] = make_int4(r.x, r.st, a, r.rule);
+        if (f == nr - 1) {  // where the pass's last record ends
+          const bool last_of_seg = fg + 1 >= sg_cnt[a + 1];
+          pass_end = last_of_seg ? seg_end(a) : sg_S[a] + recs[g + 1].dst;
+          wsum[0] = pass_end;  // read after the barrier below
+        }
+      }
+      __syncthreads();
+      pass_end = wsum[0];
+      const int32_t plo = done, phi = pass_end < hi_t ? pass_end : hi_t;
+      __syncthreads();  // wsum reused by ot_owners
+      if (phi > plo) {
+        // first positions relative to the pass (the first record may start before it)
+        for (int f = threadIdx.x; f < nr; f += 256) ps[f] = max(ps[f] - plo, 0);
+        if (threadIdx.x == 0) ps[nr] = phi - plo;
+        __syncthreads();
+        ot_owners<4>(ps, nr, 0, phi - plo, own, wsum);
+#pragma unroll
+        for (int j = 0; j < kOtItems; j++) {
+          const int e = ebase + j * 64 + lane;
+          const int32_t q = P + e;
+          if (e < n_el && q >= plo && q < phi) {
+            const int4 r = tab[own[ot_pad(q - plo)]];
+            const int32_t p = q - sg_S[r.z];  // segment-relative position
+            int64_t off;
+            if (r.y != 0) {
+              off = int64_t(r.x) + int64_t(p) * r.y - 1;
+            } else {
+              const int64_t gi = sg_band[r.z] + int64_t(r.x) + p;  // the band's fire list
+              off = gi >= 0 && gi < times_cap ? times[gi] - t0 - 1 : -1;
+            }
+            bad |= off < 0 || off >= 4096;
+            key[j] = (uint32_t(off) << kOtIdxBits) | uint32_t(e);
+            rl[e] = r.w;
+          }
+        }
+        __syncthreads();  // own (pk) is rewritten by the next pass
+        done = phi;
+      }
+    }
+    // the next window: the segment after this one's last
+    s_cur += kNtSegs;
+    i_cur = 0;
+  }
+#pragma unroll
+  for (int j = 0; j < kOtItems; j++)
+    if (ebase + j * 64 + lane >= n_el) key[j] = 0u;
+  // by slab; a node's only tile by the whole offset (its last pass is the slab)
+  const bool one = tile_base[n + 1] - tile_base[n] == 1;
+  if (one) ot_sort<4, 64>(key, n_el, 0u, 0, 2, pk, s);
+  else ot_sort<4, 64, true>(key, n_el, 0u, kOtSlabBits, 1, pk, s);
+  int32_t* __restrict__ pt = pre + t * kOtPre;
+  if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];
+  const int64_t base = lo_n + P;
+  for (int p = threadIdx.x; p < n_el; p += 256) {
+    const uint32_t v = pk[p];
+    toff_out[base + p] = uint16_t(v >> kOtIdxBits);
+    __builtin_nontemporal_store(rl[v & kOtIdxMask], rule_out + base + p);
+    if (p > 0) {
+      const uint32_t u = pk[p - 1];
+      if (one) bad |= ot_out_of_order(u, v, rl);
+      else if ((u >> (kOtIdxBits + kOtSlabBits)) == (v >> (kOtIdxBits + kOtSlabBits))) {
+        const int32_t ru = rl[u & kOtIdxMask], rv = rl[v & kOtIdxMask];
+        bad |= ru > rv || (ru == rv && (u >> kOtIdxBits) >= (v >> kOtIdxBits));
+      }
+    }
+  }
+  if (__ballot(bad) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
+}
+
 int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads - 1) / threads)); }
 
 }  // namespace
 
-// Windows <= 4096 s: the tile sort + merge of the per-node lists in c->node_time
-// / c->node_rule (node offsets node_off[N+1] on the device), enqueued on st
-// with no host sync: buffers sized from the output capacity cap, the tile
-// kernel's grid an upper bound it trims on the device.  Used by
-// cg_node_result_order_by_time and by the per-node calls in time order
-// (pipelined windows included).
-int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
-                        bool in16, int64_t* err) {
-  if (N == 0 || cap == 0) return CG_OK;
-  const int64_t Tmax = cap / kOtTile + N + 1;
+// Windows <= 4096 s, in three steps enqueued on st with no host sync (buffers
+// sized from the output capacity cap, grids upper bounds trimmed on the
+// device): order_setup (node-aligned tiles from the node offsets), the tiles
+// (k_ot_tile over a written rule-major result, or k_node_tile straight from
+// the segment records), order_tail (slab offsets, k_ot_merge, k_ot_big).
+namespace {
+
+int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipStream_t st, int64_t* Tmax) {
+  *Tmax = cap / kOtTile + N + 1;
   const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
   const int64_t tab = int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre;
   // growing a buffer frees the old one: earlier windows' kernels finish first
-  if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(Tmax) ||
-      c->ts_hist.cap < size_t(Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
-      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->scan_tmp.cap < scan_temp_bytes(N))
+  if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(*Tmax) ||
+      c->ts_hist.cap < size_t(*Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
+      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->scan_tmp.cap < scan_temp_bytes(N) ||
+      c->ts_rec.cap < size_t(2 * *Tmax))
     HIPCHK(hipStreamSynchronize(st));
   int rc;
-  if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1)) || (rc = c->ts_tile_node.ensure(Tmax)) ||
-      (rc = c->ts_hist.ensure(Tmax * kOtPre)) || (rc = c->node_time2.ensure(toff_words)) ||
-      (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) ||
+  if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1)) || (rc = c->ts_tile_node.ensure(*Tmax)) ||
+      (rc = c->ts_hist.ensure(*Tmax * kOtPre)) || (rc = c->node_time2.ensure(toff_words)) ||
+      (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) || (rc = c->ts_rec.ensure(2 * *Tmax)) ||
       (rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N)))))
     return rc;
   hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, node_off, N, kOtTile, cap, c->ts_cnt.p);
   launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
   hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
-  uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
-  if (in16)
-    hipLaunchKernelGGL(k_ot_tile<true>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
-                       c->ts_base.p + N, err);
-  else
-    hipLaunchKernelGGL(k_ot_tile<false>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
-                       c->ts_base.p + N, err);
+  return CG_OK;
+}
+
+int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, hipStream_t st, int64_t* err) {
+  const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
   HIPCHK(hipMemsetAsync(big_n, 0, 8, st));
   int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
@@ -819,6 +1012,46 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
                      c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
                      c->ts_off.p, big_n, err);
   return cg_hip_check(hipGetLastError(), "time-order kernels");
+}
+
+}  // namespace
+
+// The tile sort + merge of the per-node lists already in c->node_time /
+// c->node_rule (node offsets node_off[N+1] on the device): used by
+// cg_node_result_order_by_time.
+int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
+                        bool in16, int64_t* err) {
+  if (N == 0 || cap == 0) return CG_OK;
+  int64_t Tmax = 0;
+  int rc = order_setup(c, node_off, N, cap, st, &Tmax);
+  if (rc) return rc;
+  uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
+  if (in16)
+    hipLaunchKernelGGL(k_ot_tile<true>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
+                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
+                       c->ts_base.p + N, err);
+  else
+    hipLaunchKernelGGL(k_ot_tile<false>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
+                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
+                       c->ts_base.p + N, err);
+  return order_tail(c, node_off, N, t0, st, err);
+}
+
+// The per-node writer and tile sort in one (k_node_tile), then the merge: the
+// lists of a window <= 4096 s in (time, rule) order straight from the segment
+// records, into c->node_time / c->node_rule.
+int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int64_t* err) {
+  if (a.N == 0 || a.cap == 0) return CG_OK;
+  int64_t Tmax = 0;
+  int rc = order_setup(c, a.node_off, a.N, a.cap, st, &Tmax);
+  if (rc) return rc;
+  const int64_t* n_tiles = c->ts_base.p + a.N;
+  hipLaunchKernelGGL(k_tile_rec_start, dim3(gridn(Tmax, 256)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec,
+                     a.recs, a.K, c->ts_tile_node.p, c->ts_base.p, a.node_off, n_tiles, c->ts_rec.p);
+  hipLaunchKernelGGL(k_node_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec, a.recs,
+                     a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
+                     reinterpret_cast<uint16_t*>(c->node_time2.p), c->node_rule2.p, c->ts_hist.p, n_tiles, err);
+  return order_tail(c, a.node_off, a.N, a.t0, st, err);
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {

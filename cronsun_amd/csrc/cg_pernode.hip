@@ -1044,22 +1044,25 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
 #endif
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
   // (time, rule) order of a window <= 4096 s: 16-bit offsets for the tile sort
-  // (the same predicate as order_by_time_locked's tile sort: bits <= 12, not LSD)
-  const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
+  // (time, rule) order of a window <= 4096 s (the predicate of
+  // order_by_time_locked's tile sort: bits <= 12, not LSD): the writer fused
+  // with the tile sort, then the merge (order_fused_enqueue)
+  const bool fused = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
+  c->pn_res_host[2] = 0;
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
-    if (NK > 0 && cap > 0) {
+    if (fused) {
+      const FusedOrderArgs fa{c->seg_pos.p, c->seg_pair.p, c->seg_nrec.p, c->recs.p, c->offsets.p, c->times.p,
+                              int64_t(c->times.cap), c->node_off.p, N, K, B, cap, t0};
+      if (NK > 0 && cap > 0 && (rc = order_fused_enqueue(c, fa, st, c->pn_res_dev + 2))) return rc;
+    } else if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL((k_node_write<V, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
                      0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,      \
                      c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p,     \
                      c->node_rule.p, node_major)
-      if (off16) {
-        hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
-                           0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p, c->times.p,
-                           N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
-      } else switch (variant) {
+      switch (variant) {
         case 1: CG_NW(1); break;
         case 2: CG_NW(2); break;
         case 3: CG_NW(3); break;
@@ -1093,10 +1096,20 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_cache_mode = mode;
   *n_events = En;
   *nnz_out = nnz;
-  // (time, rule) order asked for: the time-order pass inside the call; if it
-  // fails the lists may hold the writer's 16-bit offsets: nothing readable
+  if (fused) {  // written in (time, rule) order
+    if (c->pn_res_host[2]) {
+      c->pn_E = 0;
+      *n_events = 0;
+      return cg_fail(CG_EHIP, kOrderCheckMsg);
+    }
+    c->pn_time_ordered = true;
+    c->kt[12] = 0.f;  // inside the writer's time (kt[8])
+    return CG_OK;
+  }
+  // (time, rule) order of a longer window: the LSD passes after the writer; if
+  // they fail nothing is readable
   if (c->node_order == CG_NODE_ORDER_TIME) {
-    if ((rc = order_by_time_locked(c, off16))) {
+    if ((rc = order_by_time_locked(c, false))) {
       c->pn_E = 0;
       *n_events = 0;
     }
@@ -1291,16 +1304,15 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     // wave slots beside this writer instead of waiting for it to retire
     static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-    if (timed)
-      hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
+    if (timed) {  // (time, rule) order: the writer fused with the tile sort, then the merge
+      const FusedOrderArgs fa{a.seg_pos.p, c->seg_pair.p, a.seg_nrec.p, a.recs.p, a.rm.offsets.p, a.times.p,
+                              rm_cap, a.node_off.p, N, K, B, node_cap, t0};
+      if ((rc = order_fused_enqueue(c, fa, st, a.res_dev + 2))) return rc;
+    } else {
+      hipLaunchKernelGGL((k_node_write<0, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
                          0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
                          K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
-    else
-    hipLaunchKernelGGL((k_node_write<0, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), 0, st,
-                       c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N, K, B,
-                       node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
-    // (time, rule) order: the tile sort + merge after the writer, same stream
-    if (timed && (rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st, true, a.res_dev + 2))) return rc;
+    }
   }
   (void)hipEventRecord(a.nw1, st);
   HIPCHK(hipEventRecord(a.written, st));
