@@ -305,8 +305,15 @@ def main():
             # loop); finish() waits once (the node events of every window come
             # with it)
             wins = list(range(t0, t1, W))
-            for a in wins:
+            s_no = last.get("timed_no")
+            for i, a in enumerate(wins):
                 eng.expand_per_node_async(sp, utc, a, min(a + W, t1), drules, xmode)
+                if s_no is not None and i == ck["win"][s_no]:
+                    # the seeded window of this timed step: checksums of the
+                    # sample nodes' lists, enqueued right behind its writer
+                    eng.node_checksum_enqueue(ck["nodes"].data_ptr(), len(ck["nodes"]), ck["out"][s_no].data_ptr())
+            if s_no is not None:
+                last["timed_no"] = s_no + 1
             last["pending_steps"] = last.get("pending_steps", 0) + 1
             last["windows"] = len(wins)
             return None
@@ -417,6 +424,18 @@ def main():
     if wl != "dispatch":
         for ptr, n_ev, w in result_buffers():
             eng.fill(ptr, n_ev * w, 0xFF)
+    # per-node pipelined steps: every timed step checks one seeded window (its
+    # lists are overwritten by later windows) through device checksums of a
+    # node sample, compared with the oracle after the timed region
+    ck = None
+    if pn_pipelined and args.verify_sample > 0:
+        rng_ck = np.random.default_rng(0x5EED + 31 + rank)
+        nw_ck = len(range(t0, t1, W))
+        ck = {"nodes_np": np.sort(rng_ck.choice(n_nodes, 8, replace=False)).astype(np.int32),
+              "win": rng_ck.integers(0, nw_ck, args.steps)}
+        ck["nodes"] = torch.from_numpy(ck["nodes_np"]).to(dev)
+        ck["out"] = torch.zeros((args.steps, 16), dtype=torch.int64, device=dev)
+        last["timed_no"] = 0
     barrier()
     torch.cuda.synchronize()
     start = time.perf_counter()
@@ -466,6 +485,10 @@ def main():
             wa, wb = last.get("window", (t0, t1))  # the last timed step's window
             verify = verify_rule_major(eng, spec_of, R, wa, wb, E, args.verify_sample,
                                        seed=0x5EED + 99 + rank, zone=args.zone)
+        if ck is not None:
+            verify["every_step"] = verify_window_checksums(eng, spec_of, rin, xmode, t0, t1, W, ck,
+                                                           zone=args.zone, time_order=args.time_order)
+            verify["verified"] = verify["verified"] and verify["every_step"]["verified"]
         verify["seconds"] = time.perf_counter() - tv
         verify["unwritten_after_poison"] = unwritten
         verify["verified"] = verify["verified"] and unwritten == 0
@@ -834,6 +857,45 @@ def verify_per_node(eng, spec_of, rin, mode, a, b, En, n_nodes_sample, seed, zon
     return {"verified": bad == 0 and mono, "kind": "per-node lists of the last window vs oracle",
             "nodes_checked": int(len(nodes)), "events_checked": int(ev),
             "mismatched_nodes": int(bad), "offsets_consistent": mono}
+
+
+def verify_window_checksums(eng, spec_of, rin, mode, t0, t1, W, ck, zone="UTC", time_order=False):
+    """Every timed step's seeded window: the device checksums of the sample
+    nodes' lists (cg_node_checksum_enqueue, taken in the timed region right
+    behind that window's writer) against the same checksums of the oracle's
+    lists (the nodes' own filter over every rule composed with the Next loop,
+    expanded once over the whole horizon and sliced per window)."""
+    import numpy as np
+    O = _oracle()
+    threads = host_cpus()[0]
+    nodes = ck["nodes_np"]
+    roff, rules = O.node_rules(rin, mode, nodes, threads=threads)
+    union = np.unique(rules)
+    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(r)) for r in union]), t0, t1, O.Loc(zone),
+                            threads=threads)
+    slot = np.repeat(np.arange(len(union), dtype=np.int64), np.diff(eo))
+    key = slot * (1 << 32) + (et - t0)
+    got = ck["out"].cpu().numpy().view(np.uint64)
+    wins = list(range(t0, t1, W))
+    bad = 0
+    for s, wi in enumerate(ck["win"]):
+        a, b = wins[int(wi)], min(wins[int(wi)] + W, t1)
+        for k, n in enumerate(nodes):
+            pos = np.searchsorted(union, rules[roff[k]:roff[k + 1]])
+            lo = np.searchsorted(key, pos * (1 << 32) + (a - t0), side="right")
+            hi = np.searchsorted(key, pos * (1 << 32) + (b - t0), side="right")
+            lens = hi - lo
+            idx = np.repeat(lo - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
+            exp_t, exp_r = et[idx], union[np.repeat(pos, lens)]
+            if time_order:
+                o = np.argsort(exp_t, kind="stable")  # rule-major input: stable by time = (time, rule)
+                exp_t, exp_r = exp_t[o], exp_r[o]
+            ct, cr = eng.node_list_checksum(exp_t, exp_r)
+            bad += not (int(got[s, 2 * k]) == ct and int(got[s, 2 * k + 1]) == cr)
+    return {"verified": bad == 0, "kind": "every timed step: a seeded window's lists of 8 sample nodes, "
+            "device checksums taken behind its writer vs the oracle's", "steps": int(len(ck["win"])),
+            "windows": [int(x) for x in ck["win"]], "nodes": [int(x) for x in nodes],
+            "mismatches": int(bad)}
 
 
 def cpu_dispatch(specs, t0, threads=0):

@@ -141,6 +141,7 @@ def _declare(L):
         "cg_node_result_device": ([vp, P(vp), P(vp), P(vp), P(i64)], C.c_int),
         "cg_node_result_copy": ([vp, vp, vp, vp, i64], C.c_int),
         "cg_node_counts_to_device": ([vp, vp], C.c_int),
+        "cg_node_checksum_enqueue": ([vp, vp, C.c_int32, vp], C.c_int),
         "cg_node_csr_place": ([vp, C.c_int32, vp, vp, vp, C.c_int32, vp, vp, vp], C.c_int),
         "cg_expand_per_node_rules_device_async": ([vp, vp, vp, i64, i64, vp, C.c_int], C.c_int),
         "cg_expand_per_node_wait": ([vp, P(i64), P(i64)], C.c_int),

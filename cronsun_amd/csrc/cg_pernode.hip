@@ -748,6 +748,49 @@ __global__ __launch_bounds__(256) void k_span_place(int64_t n, const int64_t* __
   }
 }
 
+// Order-sensitive checksums of k nodes' lists (cg_node_checksum_enqueue): for
+// node nodes[i], out[2i] = sum_j mix(j, time[j]) and out[2i+1] = sum_j
+// mix(j, rule[j]) over its list (j node-relative), the cg_checksum_device mix.
+// One block per node; nothing is read when the lists' total exceeds cap.
+__device__ __forceinline__ uint64_t ck_mix(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+__global__ __launch_bounds__(256) void k_node_checksums(const int64_t* __restrict__ node_off, int32_t N, int64_t cap,
+                                                         const int64_t* __restrict__ time,
+                                                         const int32_t* __restrict__ rule,
+                                                         const int32_t* __restrict__ nodes,
+                                                         unsigned long long* __restrict__ out) {
+  __shared__ uint64_t s[2][4];
+  const int32_t n = nodes[blockIdx.x];
+  uint64_t at = 0, ar = 0;
+  if (n >= 0 && n < N && node_off[N] <= cap) {
+    const int64_t a = node_off[n], b = node_off[n + 1];
+    for (int64_t i = a + threadIdx.x; i < b; i += blockDim.x) {
+      const uint64_t h = ck_mix(uint64_t(i - a) * 0x9E3779B97F4A7C15ull);
+      at += ck_mix(uint64_t(time[i]) ^ h);
+      ar += ck_mix(uint64_t(int64_t(rule[i])) ^ h);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    at += __shfl_xor(at, o, 64);
+    ar += __shfl_xor(ar, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s[0][threadIdx.x >> 6] = at;
+    s[1][threadIdx.x >> 6] = ar;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    out[2 * blockIdx.x] = s[0][0] + s[0][1] + s[0][2] + s[0][3];
+    out[2 * blockIdx.x + 1] = s[1][0] + s[1][1] + s[1][2] + s[1][3];
+  }
+}
+
 // persistent k_node_write grid: as many 4-wave blocks per CU as its register
 // and LDS use let run at once (no block of the grid waits for a slot)
 int node_write_blocks_per_cu() {
@@ -1582,6 +1625,29 @@ int launch_node_counts(cg_ctx* c, hipStream_t st, int64_t* d_counts) {
 }
 
 extern "C" {
+
+int cg_node_checksum_enqueue(cg_ctx* c, const int32_t* d_nodes, int32_t k, uint64_t* d_out) {
+  if (!c || k < 0 || (k > 0 && (!d_nodes || !d_out))) return cg_fail(CG_EINVAL, "cg_node_checksum_enqueue: bad argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  // the lists of the last enqueued window (pipelined) or of the last result
+  const int64_t* off = nullptr;
+  int32_t N = 0;
+  if (pn_async_pending(c) && c->pa_last >= 0) {
+    off = c->pns[c->pa_last].node_off.p;
+    N = c->pns[c->pa_last].N;
+  } else {
+    if (c->pn_E == 0 && c->pn_N == 0) return cg_fail(CG_EINVAL, "cg_node_checksum_enqueue: no per-node result");
+    off = c->node_off.p;
+    N = int32_t(c->pn_N);
+  }
+  const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
+  if (k > 0)
+    hipLaunchKernelGGL(k_node_checksums, dim3(unsigned(k)), dim3(256), 0, c->st, off, N, cap, c->node_time.p,
+                       c->node_rule.p, d_nodes, reinterpret_cast<unsigned long long*>(d_out));
+  return cg_hip_check(hipGetLastError(), "k_node_checksums");
+}
 
 int cg_node_counts_to_device(cg_ctx* c, int64_t* d_counts) {
   if (!c || !d_counts) return cg_fail(CG_EINVAL, "cg_node_counts_to_device: null");

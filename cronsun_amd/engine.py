@@ -519,6 +519,26 @@ class Engine:
                                         rule.ctypes.data, n_events))
         return node_off, time[:n_events], rule[:n_events]
 
+    def node_checksum_enqueue(self, d_nodes, k, d_out):
+        """cg_node_checksum_enqueue: checksums of k nodes' lists of the last
+        enqueued window (device pointers: int32 nodes [k], uint64 out [2k])."""
+        check(lib().cg_node_checksum_enqueue(self._h, d_nodes, int(k), d_out))
+
+    @staticmethod
+    def node_list_checksum(time, rule):
+        """The host form of cg_node_checksum_enqueue's checksums of one list."""
+        def mix(x):
+            x = x ^ (x >> np.uint64(30))
+            x = x * np.uint64(0xBF58476D1CE4E5B9)
+            x = x ^ (x >> np.uint64(27))
+            x = x * np.uint64(0x94D049BB133111EB)
+            return x ^ (x >> np.uint64(31))
+        with np.errstate(over="ignore"):
+            h = mix(np.arange(len(time), dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+            ct = mix(np.asarray(time, dtype=np.int64).view(np.uint64) ^ h).sum(dtype=np.uint64)
+            cr = mix(np.asarray(rule, dtype=np.int64).view(np.uint64) ^ h).sum(dtype=np.uint64)
+        return int(ct), int(cr)
+
     def node_copy_range(self, first, count):
         """Events [first, first+count) of the last per-node result (time, rule)."""
         time = np.empty(max(count, 1), dtype=np.int64)

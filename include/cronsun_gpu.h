@@ -431,6 +431,15 @@ int cg_node_result_copy(cg_ctx* ctx, int64_t* node_off, int64_t* time, int32_t* 
  * fetches; either pointer may be NULL */
 int cg_node_result_copy_range(cg_ctx* ctx, int64_t first, int64_t count, int64_t* time,
                               int32_t* rule);
+/* Integrity check for pipelined windows (instrumentation; no reference
+ * counterpart): enqueues on the ctx's stream, right behind the last enqueued
+ * per-node window (or the last synchronous result), order-sensitive checksums
+ * of the lists of the k nodes d_nodes[] (device int32): d_out[2i] = sum_j
+ * mix(j, time[j]), d_out[2i+1] = sum_j mix(j, rule[j]) over node d_nodes[i]'s
+ * list, j node-relative, mix as cg_checksum_device (device uint64 [2k]).  A
+ * window past the output capacity gives zeros.  Lets a caller check windows
+ * whose result a later window overwrites. */
+int cg_node_checksum_enqueue(cg_ctx* ctx, const int32_t* d_nodes, int32_t k, uint64_t* d_out);
 /* per-node event counts of the last per-node result, copied to a DEVICE
  * buffer of N int64 (e.g. a torch tensor for an RCCL allgather) */
 int cg_node_counts_to_device(cg_ctx* ctx, int64_t* d_counts);
