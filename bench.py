@@ -118,6 +118,12 @@ def main():
     ap.add_argument("--gather-node-csr", action="store_true",
                     help="pernode/config3 at N > 1: every step also gathers the whole per-node CSR on "
                          "rank 0 (shard.gather_node_csr; timed)")
+    ap.add_argument("--lib-comm", action="store_true",
+                    help="N > 1: the exchanges through the library's RCCL communicator behind the C-ABI "
+                         "(cg_comm_*: totals all-gather, per-node offsets, chunked per-node CSR gather) "
+                         "instead of torch.distributed")
+    ap.add_argument("--gather-budget", type=int, default=1 << 31,
+                    help="bytes of peer events rank 0 stages per chunk of the per-node CSR gather")
     ap.add_argument("--sync", action="store_true",
                     help="config2/config4: synchronous steps (cg_expand_device: every step ends with a "
                          "stream sync) instead of the pipelined cg_expand_device_async")
@@ -284,6 +290,15 @@ def main():
 
     dev = torch.device("cuda", local)
     cdev = dev if backend == "nccl" else torch.device("cpu")  # collective tensors
+    lcomm = None
+    if args.lib_comm and world > 1:
+        # the library's own RCCL communicator (cg_comm_init): rank 0's unique id
+        # handed to every rank over torch.distributed
+        from cronsun_amd.engine import Comm
+        uid = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        lcomm = Comm(eng, world, rank, uid[0])
+    gath = {}
     tot = torch.zeros(world, dtype=torch.int64, device=cdev)
     node_counts = torch.zeros(n_nodes, dtype=torch.int64, device=dev) if pn else None
     last = {}
@@ -331,16 +346,30 @@ def main():
                 if args.time_order:
                     last["order_ms"] = last.get("order_ms", 0.0) + eng.node_order_by_time()
                 last.setdefault("first_nkt", eng.node_kernel_times())  # the uncached join
-                if world > 1 and args.gather_node_csr:
+                if world > 1 and args.gather_node_csr and lcomm is not None:
+                    # the gather behind the C-ABI (cg_comm_gather_node_csr):
+                    # node-range chunks under the byte budget, RCCL send/recv
+                    if rank == 0 and not gath:
+                        cap = 2 * En_w * world + (1 << 20)  # every window about the same size
+                        gath.update(off=torch.empty(rin.n_nodes + 1, dtype=torch.int64, device=dev),
+                                    t=torch.empty(cap, dtype=torch.int64, device=dev),
+                                    r=torch.empty(cap, dtype=torch.int32, device=dev), cap=cap)
+                    ptrs = (gath["off"].data_ptr(), gath["t"].data_ptr(), gath["r"].data_ptr(), gath["cap"]) \
+                        if rank == 0 else (0, 0, 0, 0)
+                    last["gathered_events"] = lcomm.gather_node_csr(0, shard_info["lo"], args.gather_budget,
+                                                                    *ptrs)
+                elif world > 1 and args.gather_node_csr:
                     # north_star's second collective: the whole per-node CSR on
                     # rank 0 (per-node counts all-gathered, then each rank's
-                    # slice to rank 0 over its own link)
+                    # slice to rank 0 over its own link, in chunks under the budget)
                     n_off, n_time, n_rule = eng.node_result_tensors(rin.n_nodes)
                     g = shard.gather_node_csr(n_off.to(cdev), n_time.to(cdev), n_rule.to(cdev),
-                                              shard_info["lo"], dist, engine=eng)
+                                              shard_info["lo"], dist, engine=eng, budget_bytes=args.gather_budget)
                     if g is not None:
                         last["gathered_events"] = int(g[1].numel())
                     del g
+                elif lcomm is not None:
+                    lcomm.node_offsets(rin.n_nodes)  # per-node offsets over the library's RCCL comm
                 elif world > 1:
                     # per-node offsets of every rank's slice (RCCL allgather of N int64)
                     eng.node_counts_to_device(node_counts.data_ptr())
@@ -356,7 +385,9 @@ def main():
             eng.expand_async(sp, utc, t0 + off_t, t1 + off_t)
             return None
         E = eng.expand_device(sp, utc, t0 + off_t, t1 + off_t)
-        if world > 1:
+        if lcomm is not None:
+            lcomm.allgather_i64([E])  # global CSR offsets over the library's RCCL comm
+        elif world > 1:
             # global CSR offsets of the job-ID-range shards (RCCL allgather)
             mine = torch.tensor([E], dtype=torch.int64, device=cdev)
             dist.all_gather_into_tensor(tot, mine)
@@ -374,14 +405,18 @@ def main():
             nk = eng.node_kernel_times()
             last.update(kt=np.array(last["kt_sync"]),
                         nkt=np.array([last["nkt_sync"][0], last["nkt_sync"][1], nk[2] * last["windows"]]))
-            if world > 1:
+            if lcomm is not None:
+                lcomm.node_offsets(rin.n_nodes)
+            elif world > 1:
                 eng.node_counts_to_device(node_counts.data_ptr())
                 shard.node_offsets(node_counts.to(cdev), dist)
             return En // k
         if not pipelined:
             return None
         E = eng.expand_wait()
-        if world > 1:
+        if lcomm is not None:
+            lcomm.allgather_i64([E])
+        elif world > 1:
             mine = torch.tensor([E], dtype=torch.int64, device=cdev)
             dist.all_gather_into_tensor(tot, mine)
         return E
@@ -628,7 +663,8 @@ def main():
             "zone": args.zone,
             "events_per_gpu_step": E,
             "shard": shard_info or {"lo": 0, "hi": R},
-            "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard totals / per-node counts)",
+            "parallelism": f"dp{world} (job-ID range shards; RCCL allgather of shard totals / per-node counts"
+                           + (", through the library's cg_comm)" if lcomm is not None else ")"),
         },
         "hbm_gbps_step": algo_bytes * world / (elapsed / args.steps) / 1e9,
         "steps_mode": ("pipelined (cg_expand_device_async: count/scan of a step overlap the previous "
