@@ -899,34 +899,36 @@ def verify_window_checksums(eng, spec_of, rin, mode, t0, t1, W, ck, zone="UTC", 
     """Every timed step's seeded window: the device checksums of the sample
     nodes' lists (cg_node_checksum_enqueue, taken in the timed region right
     behind that window's writer) against the same checksums of the oracle's
-    lists (the nodes' own filter over every rule composed with the Next loop,
-    expanded once over the whole horizon and sliced per window)."""
+    lists (the nodes' own filter over every rule composed with the Next loop
+    started at the window's start)."""
     import numpy as np
     O = _oracle()
     threads = host_cpus()[0]
     nodes = ck["nodes_np"]
     roff, rules = O.node_rules(rin, mode, nodes, threads=threads)
     union = np.unique(rules)
-    eo, et = O.expand_batch(_oracle_scheds(O, [spec_of(int(r)) for r in union]), t0, t1, O.Loc(zone),
-                            threads=threads)
-    slot = np.repeat(np.arange(len(union), dtype=np.int64), np.diff(eo))
-    key = slot * (1 << 32) + (et - t0)
+    osch = _oracle_scheds(O, [spec_of(int(r)) for r in union])
+    loc = O.Loc(zone)
     got = ck["out"].cpu().numpy().view(np.uint64)
     wins = list(range(t0, t1, W))
+    exp = {}  # window -> per node (times, rules)
     bad = 0
     for s, wi in enumerate(ck["win"]):
-        a, b = wins[int(wi)], min(wins[int(wi)] + W, t1)
-        for k, n in enumerate(nodes):
-            pos = np.searchsorted(union, rules[roff[k]:roff[k + 1]])
-            lo = np.searchsorted(key, pos * (1 << 32) + (a - t0), side="right")
-            hi = np.searchsorted(key, pos * (1 << 32) + (b - t0), side="right")
-            lens = hi - lo
-            idx = np.repeat(lo - np.concatenate([[0], np.cumsum(lens)[:-1]]), lens) + np.arange(int(lens.sum()))
-            exp_t, exp_r = et[idx], union[np.repeat(pos, lens)]
-            if time_order:
-                o = np.argsort(exp_t, kind="stable")  # rule-major input: stable by time = (time, rule)
-                exp_t, exp_r = exp_t[o], exp_r[o]
-            ct, cr = eng.node_list_checksum(exp_t, exp_r)
+        wi = int(wi)
+        if wi not in exp:
+            a, b = wins[wi], min(wins[wi] + W, t1)
+            eo, et = O.expand_batch(osch, a, b, loc, threads=threads)
+            exp[wi] = []
+            for k in range(len(nodes)):
+                pos = np.searchsorted(union, rules[roff[k]:roff[k + 1]])
+                exp_t, exp_p = O.node_list(eo, et, pos)
+                exp_r = union[exp_p]
+                if time_order:
+                    o = np.argsort(exp_t, kind="stable")  # rule-major input: stable by time = (time, rule)
+                    exp_t, exp_r = exp_t[o], exp_r[o]
+                exp[wi].append(eng.node_list_checksum(exp_t, exp_r))
+        for k in range(len(nodes)):
+            ct, cr = exp[wi][k]
             bad += not (int(got[s, 2 * k]) == ct and int(got[s, 2 * k + 1]) == cr)
     return {"verified": bad == 0, "kind": "every timed step: a seeded window's lists of 8 sample nodes, "
             "device checksums taken behind its writer vs the oracle's", "steps": int(len(ck["win"])),

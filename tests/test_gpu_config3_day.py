@@ -8,10 +8,10 @@ sample of 48 nodes are compared bit-exact with the oracle, in rule order
 (Job.Cmds' evaluation order, job.go:591-614) and in (time, rule) order
 (cg_set_node_order(TIME): Cron.run's sort.Sort(byTime), cron.go:64-79,220).
 
-The oracle expands the sampled nodes' rules over the whole day once
-(spec.go:55-145 restated) and each window is sliced from that: a rule's fires
-in (a, b] are exactly the fires of the Next loop started at a, because Next
-depends only on its input time."""
+The oracle expands the sampled nodes' rules window by window (spec.go:55-145,
+constantdelay.go:25-27 restated): each window is the Next loop started at the
+window's own start, which for @every rules (Next(t) = t + D) differs from a
+slice of one day-long loop."""
 import numpy as np
 import pytest
 
@@ -35,38 +35,24 @@ def day():
     t0 = synth.T0_2026
     nodes = np.sort(np.random.default_rng(2404).choice(rin.n_nodes, 48, replace=False))
     roff, nrules = O.node_rules(rin, _lib.EXCLUDE_NONE, nodes, threads=host_threads())
-    # the sampled nodes' rules over the whole day, once
     uniq = np.unique(nrules)
-    eo, et = O.expand_batch(oracle_scheds([specs[r] for r in uniq]), t0, t0 + 24 * HOUR, oracle_zone_utc(),
-                            threads=host_threads())
-    # a sortable key per fire: (rule slot, second of the day)
-    slot = np.repeat(np.arange(len(uniq), dtype=np.int64), np.diff(eo))
-    key = slot * (1 << 17) + (et - t0)
+    osch = oracle_scheds([specs[r] for r in uniq])
     sp = eng.upload_c(arr, R)
     dr = eng.upload_rules(rin)
-    yield eng, sp, dr, rin, t0, nodes, roff, nrules, uniq, eo, et, key
+    yield eng, sp, dr, rin, t0, nodes, roff, nrules, uniq, osch
     dr.free()
     sp.free()
     eng.close()
 
 
-def expected_window(uniq, eo, et, key, rules, a, b, t0):
-    """One node's rule-major list over (a, b] from the day's oracle fires."""
-    k = np.searchsorted(uniq, rules)
-    lo = np.searchsorted(key, k * (1 << 17) + (a - t0), side="right")
-    hi = np.searchsorted(key, k * (1 << 17) + (b - t0), side="right")
-    lens = hi - lo
-    total = int(lens.sum())
-    if total == 0:
-        return np.zeros(0, np.int64), np.zeros(0, np.int32)
-    excl = np.concatenate([[0], np.cumsum(lens)[:-1]])
-    idx = np.repeat(lo - excl, lens) + np.arange(total)
-    return et[idx], np.repeat(rules, lens).astype(np.int32)
+def expected_window(eo, et, uniq, rules):
+    """One node's rule-major list from the oracle's window expansion of uniq."""
+    return O.node_list(eo, et, np.searchsorted(uniq, rules))
 
 
 @pytest.mark.parametrize("order", ["rule", "time"])
 def test_config3_every_window_of_the_day(day, order):
-    eng, sp, dr, rin, t0, nodes, roff, nrules, uniq, eo, et, key = day
+    eng, sp, dr, rin, t0, nodes, roff, nrules, uniq, osch = day
     from cronsun_amd._lib import check, lib
     utc = cron.UTC()
     try:
@@ -84,9 +70,11 @@ def test_config3_every_window_of_the_day(day, order):
             total += En
             check(lib().cg_node_result_copy(eng._h, off.ctypes.data, None, None, 0))
             assert off[-1] == En
+            eo, et = O.expand_batch(osch, a, b, oracle_zone_utc(), threads=host_threads())
             for k, n in enumerate(nodes):
                 rules = nrules[roff[k]:roff[k + 1]]
-                exp_t, exp_r = expected_window(uniq, eo, et, key, rules, a, b, t0)
+                exp_t, exp_p = expected_window(eo, et, uniq, rules)
+                exp_r = uniq[exp_p].astype(np.int32)
                 if order == "time":  # rule-major input: a stable sort by time gives (time, rule)
                     o = np.argsort((exp_t - a).astype(np.uint16), kind="stable")
                     exp_t, exp_r = exp_t[o], exp_r[o]
