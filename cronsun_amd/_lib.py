@@ -85,6 +85,17 @@ def _preload_torch_hip():
         C.CDLL(p, mode=C.RTLD_GLOBAL)
 
 
+def preload_torch_rccl():
+    """Import torch (when installed) before the library first loads RCCL
+    (cg_comm_*): torch links the same librccl.so, and a process that loads it
+    through the library first and imports torch afterwards aborts at exit
+    (glibc heap check in the shared libraries' teardown; tools/probe_comm_exit.py:
+    torch first, or no torch at all, exit cleanly).  A C or Go host without
+    torch is unaffected."""
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
 def _declare(L):
     vp, i32, i64, u64, sz = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_size_t
     P = C.POINTER

@@ -77,6 +77,7 @@ class Comm:
 
     @staticmethod
     def unique_id():
+        _lib.preload_torch_rccl()
         buf = (C.c_uint8 * 128)()
         check(lib().cg_comm_unique_id(buf))
         return bytes(buf)
@@ -85,6 +86,7 @@ class Comm:
         if len(uid) != 128:
             raise ValueError("RCCL unique id must be 128 bytes")
         self.engine, self.world, self.rank = engine, int(world), int(rank)
+        _lib.preload_torch_rccl()
         h = C.c_void_p()
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().cg_comm_init(engine._h, self.world, self.rank, buf, C.byref(h)))
