@@ -21,11 +21,9 @@ int cg_hip_check(hipError_t e, const char* what);
 
 // Grow-only device buffer (grows by 1.25x so repeated calls settle).
 // per-node writer record of one non-empty (node, rule) pair of a segment
-// (cg_pernode.hip, k_seg_records): the rule and its first position d in the
-// segment (8 B).  The writers take the rest from the rule's RuleInfo (a
-// band's infos stay in L2): a progression's fire at segment position p is
-// t0 + first + (p - d) * st, another rule's the band's fire list at
-// off + (p - d).
+// (cg_pernode.hip, k_seg_records): rule, first position in the segment, and
+// x, st -- fire at position p = t0 + x + p * st (a progression rule), or
+// band-relative fire-list index = x + p when st == 0
 // per rule of a per-node window (k_rule_info): fire count, band-relative
 // index of the first fire, and {first - t0, stride} of a progression (st 0:
 // not one)
@@ -33,21 +31,9 @@ struct alignas(16) RuleInfo {
   int32_t cnt, off, first, st;
 };
 
-struct alignas(8) PairRec {
-  int32_t rule, dst;
+struct alignas(16) PairRec {
+  int32_t rule, dst, x, st;
 };
-
-// a record's x, stride as the writers use them: fire at segment position p =
-// t0 + x + p * st (a progression whose x fits 32 bits), else st = 0 and the
-// band-relative fire-list index is x + p
-struct RecXS {
-  int32_t x, st;
-};
-__host__ __device__ __forceinline__ RecXS rec_xs(const PairRec& r, const RuleInfo& g) {
-  const int64_t x = int64_t(g.first) - int64_t(r.dst) * g.st;
-  if (g.st != 0 && x >= INT32_MIN && x <= INT32_MAX) return RecXS{int32_t(x), g.st};
-  return RecXS{g.off - r.dst, 0};
-}
 
 template <class T>
 struct DBuf {
@@ -341,7 +327,6 @@ struct FusedOrderArgs {
   const int64_t* seg_pair;  // [N*K+1] first record (pair index) of each segment
   const int32_t* seg_nrec;  // [N*K] records of each segment
   const PairRec* recs;
-  const RuleInfo* info;     // the window's rule infos (x, stride of the records)
   const int64_t* rule_off;  // the window's rule-major offsets and fire times (gathers)
   const int64_t* times;
   int64_t times_cap;

@@ -813,8 +813,8 @@ constexpr int kNtSegs = 256;  // segments per window
 
 __global__ __launch_bounds__(256) void k_node_tile(
     const int64_t* __restrict__ seg_pos, const int64_t* __restrict__ seg_pair, const int32_t* __restrict__ seg_nrec,
-    const PairRec* __restrict__ recs, const RuleInfo* __restrict__ info, const int64_t* __restrict__ rule_off,
-    const int64_t* __restrict__ times, int64_t times_cap, int32_t K, int32_t B, int64_t t0, const int32_t* __restrict__ tile_node, const int64_t* __restrict__ tile_base,
+    const PairRec* __restrict__ recs, const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times,
+    int64_t times_cap, int32_t K, int32_t B, int64_t t0, const int32_t* __restrict__ tile_node, const int64_t* __restrict__ tile_base,
     const int64_t* __restrict__ node_off, const int64_t* __restrict__ tile_start, uint16_t* __restrict__ toff_out,
     int32_t* __restrict__ rule_out, int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles,
     int64_t* __restrict__ err) {
@@ -895,9 +895,8 @@ __global__ __launch_bounds__(256) void k_node_tile(
         }
         const int64_t g = sg_rec[a] + (fg - sg_cnt[a]);
         const PairRec r = recs[g];
-        const RecXS xs = rec_xs(r, info[r.rule]);
         ps[f] = sg_S[a] + r.dst;
-        tab[f] = make_int4(xs.x, xs.st, a, r.rule);
+        tab[f] = make_int4(r.x, r.st, a, r.rule);
         if (f == nr - 1) {  // where the pass's last record ends
           const bool last_of_seg = fg + 1 >= sg_cnt[a + 1];
           pass_end = last_of_seg ? seg_end(a) : sg_S[a] + recs[g + 1].dst;
@@ -1050,7 +1049,7 @@ int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int6
   hipLaunchKernelGGL(k_tile_rec_start, dim3(gridn(Tmax, 256)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec,
                      a.recs, a.K, c->ts_tile_node.p, c->ts_base.p, a.node_off, n_tiles, c->ts_rec.p);
   hipLaunchKernelGGL(k_node_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec, a.recs,
-                     a.info, a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
+                     a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
                      reinterpret_cast<uint16_t*>(c->node_time2.p), c->node_rule2.p, c->ts_hist.p, n_tiles, err);
   return order_tail(c, a.node_off, a.N, a.t0, st, err);
 }

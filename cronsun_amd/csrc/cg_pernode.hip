@@ -451,7 +451,12 @@ __global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__
         const int64_t d = run + (incl - g[u].cnt);
         const uint64_t ball = __ballot(g[u].cnt > 0);
         const uint32_t ne = uint32_t(lane < 32 ? ball : ball >> 32);  // this half's non-empty pairs
-        if (g[u].cnt > 0) recs[cur.p0 + nrec + __popc(ne & below)] = PairRec{r[u], int32_t(d)};
+        if (g[u].cnt > 0) {
+          const int64_t at = cur.p0 + nrec + __popc(ne & below);
+          const int64_t x = int64_t(g[u].first) - d * g[u].st;
+          const bool prog = g[u].st != 0 && x >= INT32_MIN && x <= INT32_MAX;
+          recs[at] = PairRec{r[u], int32_t(d), int32_t(prog ? x : int64_t(g[u].off) - d), prog ? g[u].st : 0};
+        }
         run += half_total(incl);
         nrec += __popc(ne);
       }
@@ -544,8 +549,7 @@ constexpr int kNodeMajorDefault = 0;  // writer task order: 0 band-major, 1 node
 template <int V, bool OFF16 = false>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
-    const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, const RuleInfo* __restrict__ info,
-    int64_t t0,
+    const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, int64_t t0,
     const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times, int32_t N, int32_t K,
     int32_t B, int64_t cap, uint32_t* __restrict__ tickets, int64_t* __restrict__ out_time,
     int32_t* __restrict__ out_rule, int node_major) {
@@ -604,32 +608,23 @@ __global__ __launch_bounds__(256) void k_node_write(
     };
     int32_t pq = -1, prule = 0;  // a block carried into the next chunk
     int64_t ptime = 0;
-    // records in chunks of 64 (lane i: record i), the next two chunks in
-    // flight and the next chunk's rule infos (unconditional loads at clamped
-    // indices: a load under a branch is waited for at the branch's end, so
-    // the prefetch would not stay in flight)
-    auto fetch = [&](int32_t w, PairRec& r, int32_t& e) {
-      r = recs[p0 + (w + lane < nrec ? w + lane : nrec - 1)];
+    // records in chunks of 64 (lane i: record i), the next chunk in flight
+    // (an unconditional load at a clamped index: a load under a branch is
+    // waited for at the branch's end, so the prefetch would not stay in flight)
+    PairRec nx;
+    int32_t nx_end = q_hi;
+    auto fetch = [&](int32_t w) {
+      nx = recs[p0 + (w + lane < nrec ? w + lane : nrec - 1)];
       // the chunk ends where the next one's first record starts
-      e = w + 64 < nrec ? recs[p0 + w + 64].dst + q_lo : q_hi;
+      nx_end = w + 64 < nrec ? recs[p0 + w + 64].dst + q_lo : q_hi;
     };
-    PairRec ra, rb;  // records of chunks w and w + 64
-    int32_t ea = q_hi, eb = q_hi;
-    fetch(0, ra, ea);
-    RuleInfo ia = info[ra.rule];  // infos of chunk w
-    if (64 < nrec) fetch(64, rb, eb);
+    fetch(0);
     for (int32_t w = 0; w < nrec; w += 64) {
-      // q of first event; x and stride of the record (its rule's info)
-      const RecXS xs = rec_xs(ra, ia);
-      const int32_t rr = ra.rule, dst = ra.dst + q_lo, dlt = xs.x, sst = xs.st, we = ea;
+      // q of first event; x and stride of the record (k_seg_records)
+      const int32_t rr = nx.rule, dst = nx.dst + q_lo, dlt = nx.x, sst = nx.st, we = nx_end;
       const int nc = nrec - w < 64 ? nrec - w : 64;
       const int32_t qw = __builtin_amdgcn_readlane(dst, 0);
-      if (w + 64 < nrec) {  // chunk w + 64 arrived an iteration ago: its infos now, chunk w + 128 next
-        ia = info[rb.rule];
-        ra = rb;
-        ea = eb;
-        if (w + 128 < nrec) fetch(w + 128, rb, eb);
-      }
+      if (w + 64 < nrec) fetch(w + 64);
       const bool live = lane < nc;
       auto one = [&](int32_t b) {
         tag++;
@@ -1101,13 +1096,13 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
     if (fused) {
-      const FusedOrderArgs fa{c->seg_pos.p, c->seg_pair.p, c->seg_nrec.p, c->recs.p, c->rule_info.p, c->offsets.p, c->times.p,
+      const FusedOrderArgs fa{c->seg_pos.p, c->seg_pair.p, c->seg_nrec.p, c->recs.p, c->offsets.p, c->times.p,
                               int64_t(c->times.cap), c->node_off.p, N, K, B, cap, t0};
       if (NK > 0 && cap > 0 && (rc = order_fused_enqueue(c, fa, st, c->pn_res_dev + 2))) return rc;
     } else if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL((k_node_write<V, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
-                     0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, c->rule_info.p, t0, c->offsets.p, \
+                     0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,      \
                      c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p,     \
                      c->node_rule.p, node_major)
       switch (variant) {
@@ -1353,12 +1348,12 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
     if (timed) {  // (time, rule) order: the writer fused with the tile sort, then the merge
-      const FusedOrderArgs fa{a.seg_pos.p, c->seg_pair.p, a.seg_nrec.p, a.recs.p, a.rule_info.p, a.rm.offsets.p, a.times.p,
+      const FusedOrderArgs fa{a.seg_pos.p, c->seg_pair.p, a.seg_nrec.p, a.recs.p, a.rm.offsets.p, a.times.p,
                               rm_cap, a.node_off.p, N, K, B, node_cap, t0};
       if ((rc = order_fused_enqueue(c, fa, st, a.res_dev + 2))) return rc;
     } else {
       hipLaunchKernelGGL((k_node_write<0, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
-                         0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, a.rule_info.p, t0, a.rm.offsets.p, a.times.p, N,
+                         0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
                          K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
     }
   }
