@@ -27,8 +27,13 @@ constexpr size_t kPlanLdsBytes = 60 * 1024;
 
 // closed-form writer: 4 waves per block; waves take output slices by ticket
 constexpr int kWriteWaves = 4;
+// 3 blocks per CU (12 waves): fewer concurrent write streams store faster
+// (same-box A/B on config 2, profiles/r04_ab_writer_bpc.txt: k_write_cf
+// 1.005-1.008 ms at 3 vs 1.041-1.042 at 4 and 1.081-1.088 at 2; a window
+// prefetched one slice ahead was slower at 4 (spills) and at 3 -- the wait at
+// its commit drains the previous slice's stores anyway)
 #ifndef CG_WRITE_BPC
-#define CG_WRITE_BPC 4
+#define CG_WRITE_BPC 3
 #endif
 constexpr int kWriteBlocksPerCU = CG_WRITE_BPC;  // persistent grid: blocks of 4 waves per CU
 // writer slice tickets: one u32 counter per group of blocks, 128 B apart

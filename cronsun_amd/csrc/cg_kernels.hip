@@ -565,9 +565,6 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 }
 
 
-#ifndef CG_WRITE_PREFETCH
-#define CG_WRITE_PREFETCH 0
-#endif
 // Persistent closed-form writer.  Waves work independently on 2^super_shift(cap)-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
 // consecutive runs (one coalesced round of loads, staged in its LDS slice;
@@ -657,71 +654,6 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
       cur = cur + 1 == ng ? 0 : cur + 1;
     }
   };
-#if CG_WRITE_PREFETCH
-  // The first window of a slice is loaded one slice ahead (its run data in
-  // registers, committed to LDS when the slice starts), and the slice bounds
-  // two slices ahead: a slice then starts without waiting for loads issued at
-  // its start (the wait at the commit only drains the previous slice's stores).
-  struct Head {
-    int64_t pos, S1, jw, jend;
-  };
-  auto head = [&](int64_t c) -> Head {
-    Head h{0, 0, 0, 0};
-    if (c >= nsup) return h;
-    h.pos = um ? umap[2 * c] : c << sh;
-    h.S1 = um ? umap[2 * c + 2] : (E - h.pos < sup ? E : h.pos + sup);
-    h.jw = um ? umap[2 * c + 1] : chunk_run[c];
-    h.jend = (um ? umap[2 * c + 3] : chunk_run[c + 1]) + 1;
-    return h;
-  };
-  struct Pre {
-    WinRun w;
-    int64_t off;
-  };
-  auto issue = [&](const Head& h) -> Pre {
-    Pre q;
-    const int64_t jl = h.jw + lane;
-    if (h.pos < h.S1 && jl < h.jend) {
-      const int64_t r = G == 1 ? jl : jl / G;
-      q.off = run_off[jl];
-      q.w.anchor = run_anchor[jl];
-      q.w.count = run_count[jl];
-      q.w.dmask = run_dmask[jl];
-      q.w.sp = load_spec(specs + r);
-      q.w.sp.kind |= uint32_t(jl - r * G) << 8;
-    } else {
-      q.off = INT64_MAX;
-      q.w.anchor = 0;
-      q.w.count = 0;
-      q.w.dmask = 0;
-      q.w.sp = DSpec{};
-    }
-    return q;
-  };
-  int64_t c = take();
-  int64_t c_next = take();
-  Head hc = head(c), hn = head(c_next);
-  Pre pf = issue(hc);
-  while (c < nsup) {
-    const int64_t c_after = take();
-    const Head ha = head(c_after);  // in flight while this slice is written
-    int64_t pos = hc.pos;
-    const int64_t S1 = hc.S1;
-    int64_t jw = hc.jw;
-    jend = hc.jend;
-    // commit the prefetched first window
-    __syncwarp();
-    win[lane] = pf.w;
-    woff = pf.off;
-    wcnt = pf.w.count;
-    __syncwarp();
-    pf = issue(hn);  // the next slice's first window, in flight while this one is written
-    c = c_next;
-    c_next = c_after;
-    hc = hn;
-    hn = ha;
-    if (pos >= S1) continue;  // a cost-space slice of empty runs only
-#else
   for (int64_t c = take(); c < nsup;) {
     const int64_t c_next = take();
     // slice start: a multiple of 64, so every store below is a whole 512 B block
@@ -734,7 +666,6 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
     int64_t jw = um ? umap[2 * c + 1] : chunk_run[c];  // run_off[jw] <= pos
     jend = (um ? umap[2 * c + 3] : chunk_run[c + 1]) + 1;  // the run holding S1 (or the last run)
     load_window(jw);
-#endif
     Pending pd;
     pd.blk = -1;
     pd.val = 0;
@@ -805,9 +736,7 @@ __global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_c
     }
     // the last slice ends inside a block
     if (pd.blk >= 0 && pd.blk + lane < S1) put(times + pd.blk + lane, pd.val);
-#if !CG_WRITE_PREFETCH
     c = c_next;
-#endif
   }
 }
 

@@ -786,6 +786,17 @@ __global__ __launch_bounds__(256) void k_node_checksums(const int64_t* __restric
   }
 }
 
+// Time order of windows <= 4096 s: 1 = k_node_tile builds the tiles straight
+// from the segment records (no 16-bit list written and read back); 0 = the
+// writer's 16-bit lists, then k_ot_tile.  Same-box A/B
+// (profiles/r04_ab_pernode_builds.txt): pernode --time-order 10.9 ms per step
+// fused vs 9.4 separate -- k_node_tile (5.9 ms) waits on its dependent loads
+// per tile (segment window, records, gathers) where the writer (1.5 ms) and
+// k_ot_tile (2.65 ms) stream.
+#ifndef CG_NODE_TILE_FUSED
+#define CG_NODE_TILE_FUSED 0
+#endif
+
 // persistent k_node_write grid: as many 4-wave blocks per CU as its register
 // and LDS use let run at once (no block of the grid waits for a slot)
 int node_write_blocks_per_cu() {
@@ -1086,11 +1097,12 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   static const int per_cu = node_write_blocks_per_cu();
 #endif
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-  // (time, rule) order of a window <= 4096 s: 16-bit offsets for the tile sort
   // (time, rule) order of a window <= 4096 s (the predicate of
-  // order_by_time_locked's tile sort: bits <= 12, not LSD): the writer fused
-  // with the tile sort, then the merge (order_fused_enqueue)
-  const bool fused = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
+  // order_by_time_locked's tile sort: bits <= 12, not LSD): the writer emits
+  // 16-bit offsets t - t0 - 1 for the tile sort; or (CG_NODE_TILE_FUSED) the
+  // writer fused with the tile sort, k_node_tile, then the merge
+  const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
+  const bool fused = off16 && CG_NODE_TILE_FUSED;
   c->pn_res_host[2] = 0;
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
@@ -1099,6 +1111,10 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
       const FusedOrderArgs fa{c->seg_pos.p, c->seg_pair.p, c->seg_nrec.p, c->recs.p, c->offsets.p, c->times.p,
                               int64_t(c->times.cap), c->node_off.p, N, K, B, cap, t0};
       if (NK > 0 && cap > 0 && (rc = order_fused_enqueue(c, fa, st, c->pn_res_dev + 2))) return rc;
+    } else if (NK > 0 && cap > 0 && off16) {
+      hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
+                         0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p, c->times.p,
+                         N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
     } else if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL((k_node_write<V, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
@@ -1149,10 +1165,11 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     c->kt[12] = 0.f;  // inside the writer's time (kt[8])
     return CG_OK;
   }
-  // (time, rule) order of a longer window: the LSD passes after the writer; if
-  // they fail nothing is readable
+  // (time, rule) order: the tile sort + merge (or, past 4096 s, the LSD
+  // passes) after the writer; if it fails nothing is readable (the lists may
+  // hold the writer's 16-bit offsets)
   if (c->node_order == CG_NODE_ORDER_TIME) {
-    if ((rc = order_by_time_locked(c, false))) {
+    if ((rc = order_by_time_locked(c, off16))) {
       c->pn_E = 0;
       *n_events = 0;
     }
@@ -1347,10 +1364,15 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     // wave slots beside this writer instead of waiting for it to retire
     static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-    if (timed) {  // (time, rule) order: the writer fused with the tile sort, then the merge
+    if (timed && CG_NODE_TILE_FUSED) {  // the writer fused with the tile sort, then the merge
       const FusedOrderArgs fa{a.seg_pos.p, c->seg_pair.p, a.seg_nrec.p, a.recs.p, a.rm.offsets.p, a.times.p,
                               rm_cap, a.node_off.p, N, K, B, node_cap, t0};
       if ((rc = order_fused_enqueue(c, fa, st, a.res_dev + 2))) return rc;
+    } else if (timed) {  // 16-bit offsets, then the tile sort + merge on the same stream
+      hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
+                         0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
+                         K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
+      if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st, true, a.res_dev + 2))) return rc;
     } else {
       hipLaunchKernelGGL((k_node_write<0, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
                          0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
