@@ -799,7 +799,11 @@ __global__ __launch_bounds__(256) void k_node_checksums(const int64_t* __restric
 
 // persistent k_node_write grid: as many 4-wave blocks per CU as its register
 // and LDS use let run at once (no block of the grid waits for a slot)
+#ifndef CG_NODE_BPC
+#define CG_NODE_BPC 0  // 0: as many as the occupancy allows (up to 8)
+#endif
 int node_write_blocks_per_cu() {
+  if (CG_NODE_BPC > 0) return CG_NODE_BPC + 2;  // the pipelined windows leave two slots free
   int n = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_node_write<0>, 256, 0) != hipSuccess || n < 1) n = 4;
   return std::min(n, 8);
