@@ -26,7 +26,10 @@ constexpr int kMaxSegments = 1024;
 constexpr size_t kPlanLdsBytes = 60 * 1024;
 
 // closed-form writer: 4 waves per block; waves take output slices by ticket
-constexpr int kWriteWaves = 4;
+#ifndef CG_WRITE_WAVES
+#define CG_WRITE_WAVES 4
+#endif
+constexpr int kWriteWaves = CG_WRITE_WAVES;
 // 3 blocks per CU (12 waves): fewer concurrent write streams store faster
 // (same-box A/B on config 2, profiles/r04_ab_writer_bpc.txt: k_write_cf
 // 1.005-1.008 ms at 3 vs 1.041-1.042 at 4 and 1.081-1.088 at 2; a window

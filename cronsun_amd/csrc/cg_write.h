@@ -67,7 +67,13 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t x, uint32_t n, float inv) {
 // one whole 512-B block); nontemporal: the fires are not read back by this
 // kernel (same-box A/B, profiles/r03_ab_writer_nt.json: equal or ~1 % faster
 // than plain stores on configs 2 and 4).
-__device__ __forceinline__ void put(int64_t* p, int64_t v) { __builtin_nontemporal_store(v, p); }
+#ifndef CG_WRITE_NT
+#define CG_WRITE_NT 1
+#endif
+__device__ __forceinline__ void put(int64_t* p, int64_t v) {
+  if (CG_WRITE_NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 
 // cf_seek (cg_expand.h) with the three variable divisions done by fdiv
 // (quotients < 2^24); same result, fewer instructions.
