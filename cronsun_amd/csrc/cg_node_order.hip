@@ -202,7 +202,10 @@ constexpr int kOtTile = 4 * 64 * kOtItems;    // 4096 events: the tile sort's 4-
 #define CG_OT_MERGE_WAVES 4
 #endif
 constexpr int kOtMergeWaves = CG_OT_MERGE_WAVES;  // k_ot_merge: waves per node
-constexpr int kOtIdxBits = 12;                // chunk index bits of a packed word
+// chunk index bits of a packed word (offset << kOtIdxBits | index): the merge's
+// chunk is 64 * 16 * kOtMergeWaves events
+constexpr int kOtIdxBits = kOtMergeWaves > 4 ? 13 : 12;
+static_assert(kOtMergeWaves <= 8 && 12 + kOtIdxBits <= 32, "packed words");
 constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
 constexpr int kOtSlabBits = 6;               // slab = offset >> kOtSlabBits (64 s): one 6-bit digit
 constexpr int kOtSlabs = 4096 >> kOtSlabBits;
@@ -512,10 +515,12 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 // to tin / rin, < 2^31; tin = the tile sort's 16-bit offsets): key =
 // (offset << 12 | chunk index), rule into rl[chunk index] (RULES).  All loads
 // issued before any is used (clamped indices).
-template <bool RULES>
+// SEARCH: each element finds its portion by a binary search of ps (Q
+// portions) instead of reading the owner map (no ot_owners pass)
+template <bool RULES, bool SEARCH = false>
 __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                           const int32_t* ps, const int32_t* psrc, const int32_t* own,
-                                          int32_t c0, int n_el, uint32_t (&key)[kOtItems], int32_t* rl) {
+                                          int32_t c0, int n_el, uint32_t (&key)[kOtItems], int32_t* rl, int Q = 0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * kOtItems);
   uint32_t tv[kOtItems];
@@ -524,7 +529,7 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
     const int ec = e < n_el ? e : n_el - 1;
-    const int q = own[ot_pad(ec)];
+    const int q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
     const uint32_t src = uint32_t(psrc[q] + (c0 + ec - ps[q]));
     tv[j] = tin[src];
     if (RULES) rv[j] = rin[src];
@@ -578,8 +583,11 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
   if (lane == 63) so[kOtSlabs] = run;
 }
 
+#ifndef CG_OT_OWN_SEARCH
+#define CG_OT_OWN_SEARCH 0
+#endif
 template <int NW>
-__global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
+__global__ __launch_bounds__(64 * NW, 16 / NW) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
                                                        const int32_t* __restrict__ pre, int32_t N, int64_t t0,
@@ -646,8 +654,12 @@ __global__ __launch_bounds__(64 * NW, 4) void k_ot_merge(const uint16_t* __restr
             return pb - pa;
           },
           ps, psrc, wsum);
+#if CG_OT_OWN_SEARCH
+      ot_gather<true, true>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl, int(M));
+#else
       ot_owners<NW>(ps, int(M), 0, n_el, own, wsum);
       ot_gather<true>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl);
+#endif
       // by rel = offset - the run's first second (< 64 * (jb - ja)): one
       // 8-bit pass for up to 4 slabs
       ot_sort<NW, 256>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
