@@ -134,7 +134,10 @@ __device__ __forceinline__ uint32_t lane_offset(int64_t p0) {
   return uint32_t(x < 0 ? x + 64 : x);
 }
 
-constexpr int kBatch = 8;  // blocks computed before their stores are issued
+#ifndef CG_WRITE_BATCH
+#define CG_WRITE_BATCH 8
+#endif
+constexpr int kBatch = CG_WRITE_BATCH;  // blocks computed before their stores are issued
 // 64-bit ds_bpermute (lane src's value; src taken mod 64)
 __device__ __forceinline__ int64_t bperm64_w(int64_t v, int src) {
   const int lo = __builtin_amdgcn_ds_bpermute(src << 2, int(uint32_t(v)));
