@@ -26,8 +26,12 @@ constexpr int kMaxSegments = 1024;
 constexpr size_t kPlanLdsBytes = 60 * 1024;
 
 // closed-form writer: 4 waves per block; waves take output slices by ticket
+// 2-wave blocks, 6 per CU (12 waves per CU, as 3 blocks of 4): 1-2 % faster
+// than 4-wave blocks on two boxes (profiles/r04_ab_writer_layout.txt; 8-wave
+// blocks, 1-wave blocks, 1024-event slices, plain stores, 4/16-block store
+// batches and 16/64 ticket groups were slower or equal)
 #ifndef CG_WRITE_WAVES
-#define CG_WRITE_WAVES 4
+#define CG_WRITE_WAVES 2
 #endif
 constexpr int kWriteWaves = CG_WRITE_WAVES;
 // 3 blocks per CU (12 waves): fewer concurrent write streams store faster
@@ -36,7 +40,7 @@ constexpr int kWriteWaves = CG_WRITE_WAVES;
 // prefetched one slice ahead was slower at 4 (spills) and at 3 -- the wait at
 // its commit drains the previous slice's stores anyway)
 #ifndef CG_WRITE_BPC
-#define CG_WRITE_BPC 3
+#define CG_WRITE_BPC (12 / CG_WRITE_WAVES)
 #endif
 constexpr int kWriteBlocksPerCU = CG_WRITE_BPC;  // persistent grid: blocks of 4 waves per CU
 // writer slice tickets: one u32 counter per group of blocks, 128 B apart
