@@ -565,6 +565,11 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 }
 
 
+// the second launch bound is the minimum waves per SIMD (HIP/AMDGPU: it caps
+// the VGPRs): the grid's own occupancy, so the writer never spills
+#ifndef CG_WRITE_WPE
+#define CG_WRITE_WPE (kWriteWaves * kWriteBlocksPerCU / 4)
+#endif
 // Persistent closed-form writer.  Waves work independently on 2^super_shift(cap)-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
 // consecutive runs (one coalesced round of loads, staged in its LDS slice;
@@ -576,7 +581,7 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 // @every progression (coop_every); short runs by per-lane seeks (tiny_cf).
 // Walked runs' own blocks are left to k_write_walk, which runs after this
 // kernel.
-__global__ __launch_bounds__(kWriteWaves * 64, kWriteBlocksPerCU) void k_write_cf(
+__global__ __launch_bounds__(kWriteWaves * 64, CG_WRITE_WPE) void k_write_cf(
     const DSpec* __restrict__ specs, PlanArgs p, const int64_t* __restrict__ run_anchor,
     const int32_t* __restrict__ run_count, const uint32_t* __restrict__ run_dmask,
     const int64_t* __restrict__ run_off, int64_t nruns, int64_t* __restrict__ chunk_run,
