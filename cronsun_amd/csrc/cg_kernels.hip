@@ -565,10 +565,16 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 }
 
 
-// the second launch bound is the minimum waves per SIMD (HIP/AMDGPU: it caps
-// the VGPRs): the grid's own occupancy, so the writer never spills
+// The second launch bound is the minimum waves per SIMD (HIP/AMDGPU: it caps
+// the VGPRs).  The grid runs 3 waves per SIMD; a bound of 6 caps the writer at
+// 80 VGPRs (148 B/lane of spills) and is the fastest measured: k_write_cf
+// 0.978-0.985 ms vs 1.004-1.019 at the grid's own 3 (122 VGPRs, no spills),
+// 0.985-0.991 at 5 (96 VGPRs), 1.027-1.029 at 8 (64 VGPRs), two boxes
+// (profiles/r04_ab_writer_regcap.txt).  The spills hold per-slice state that
+// the inner block loops do not touch; the tighter allocation changes where
+// the compiler puts the waits of the window and spec loads.
 #ifndef CG_WRITE_WPE
-#define CG_WRITE_WPE (kWriteWaves * kWriteBlocksPerCU / 4)
+#define CG_WRITE_WPE 6
 #endif
 // Persistent closed-form writer.  Waves work independently on 2^super_shift(cap)-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
