@@ -234,6 +234,7 @@ struct cg_ctx {
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
+  int64_t pn_R = INT64_MAX;  // rule count of the per-node lists being ordered (the merge packs rules below 2^20)
   int64_t* pn_res_host = nullptr;  // mapped pinned: per-node event total of the last call
   int64_t* pn_res_dev = nullptr;
   // the rule->node join + transpose depend only on (rule set, exclude mode):

@@ -202,6 +202,9 @@ constexpr int kOtTile = 4 * 64 * kOtItems;    // 4096 events: the tile sort's 4-
 #define CG_OT_MERGE_WAVES 4
 #endif
 constexpr int kOtMergeWaves = CG_OT_MERGE_WAVES;  // k_ot_merge: waves per node
+// the merge's packed words when every rule index is below 2^20: offset << 20 |
+// rule (the word order is the (time, rule) order; no rule array in LDS)
+constexpr int kOtRuleBits = 20;
 // chunk index bits of a packed word (offset << kOtIdxBits | index): the merge's
 // chunk is 64 * 16 * kOtMergeWaves events
 constexpr int kOtIdxBits = kOtMergeWaves > 4 ? 13 : 12;
@@ -313,7 +316,7 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, i
 // Stable sort of n packed words (offset << 12 | index) held as items by
 // digits of rel = offset - lo: `passes` (1 or 2) passes of log2(D) bits from
 // bit sh of rel up; the sorted words end in pk[0..n).  Ends synchronised.
-template <int NW, int D, bool RUNS = false>
+template <int NW, int D, bool RUNS = false, int IB = kOtIdxBits>  // IB: bits below the offset
 __device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, uint32_t lo, int sh, int passes,
                                         uint32_t* pk, OtRank<NW, D>& s) {
   constexpr int B = D == 64 ? 6 : 8;
@@ -322,7 +325,7 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, uint32
   uint32_t dg[kOtItems];
   int32_t pos[kOtItems];
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) dg[j] = (((key[j] >> kOtIdxBits) - lo) >> sh) & uint32_t(D - 1);
+  for (int j = 0; j < kOtItems; j++) dg[j] = (((key[j] >> IB) - lo) >> sh) & uint32_t(D - 1);
   ot_rank<NW, D, RUNS>(dg, n, pos, s);
 #pragma unroll
   for (int j = 0; j < kOtItems; j++)
@@ -333,7 +336,7 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, uint32
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
     key[j] = e < n ? pk[e] : 0u;
-    dg[j] = (((key[j] >> kOtIdxBits) - lo) >> (sh + B)) & uint32_t(D - 1);
+    dg[j] = (((key[j] >> IB) - lo) >> (sh + B)) & uint32_t(D - 1);
   }
   ot_rank<NW, D>(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
 #pragma unroll
@@ -517,7 +520,8 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 // issued before any is used (clamped indices).
 // SEARCH: each element finds its portion by a binary search of ps (Q
 // portions) instead of reading the owner map (no ot_owners pass)
-template <bool RULES, bool SEARCH = false>
+// PACK: key = offset << kOtRuleBits | rule (rules < 2^kOtRuleBits), no rl
+template <bool RULES, bool SEARCH = false, bool PACK = false>
 __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                           const int32_t* ps, const int32_t* psrc, const int32_t* own,
                                           int32_t c0, int n_el, uint32_t (&key)[kOtItems], int32_t* rl, int Q = 0) {
@@ -537,8 +541,12 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
-    key[j] = e < n_el ? (tv[j] << kOtIdxBits) | uint32_t(e) : 0u;
-    if (RULES && e < n_el) rl[e] = rv[j];
+    if (PACK) {
+      key[j] = e < n_el ? (tv[j] << kOtRuleBits) | uint32_t(rv[j]) : 0u;
+    } else {
+      key[j] = e < n_el ? (tv[j] << kOtIdxBits) | uint32_t(e) : 0u;
+      if (RULES && e < n_el) rl[e] = rv[j];
+    }
   }
 }
 
@@ -586,8 +594,11 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 #ifndef CG_OT_OWN_SEARCH
 #define CG_OT_OWN_SEARCH 0
 #endif
-template <int NW>
-__global__ __launch_bounds__(64 * NW, 16 / NW) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
+#ifndef CG_OT_MERGE_WPE
+#define CG_OT_MERGE_WPE 4  // min waves per SIMD of the packed merge (its LDS allows 6 blocks per CU)
+#endif
+template <int NW, bool PACK>
+__global__ __launch_bounds__(64 * NW, (PACK ? CG_OT_MERGE_WPE : 4) * 4 / NW) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
                                                        const int32_t* __restrict__ pre, int32_t N, int64_t t0,
@@ -598,7 +609,7 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void k_ot_merge(const uint16_t* _
   constexpr int kThreads = 64 * NW, kChunk = kThreads * kOtItems;
   __shared__ OtRank<NW, 256> s;
   __shared__ uint32_t pk[kChunk + kChunk / 32];  // the owner list while gathering (padded), then the sorted words
-  __shared__ int32_t rl[kChunk];
+  __shared__ int32_t rl[PACK ? 1 : kChunk];
   __shared__ int32_t ps[kOtMaxTiles + 1];
   __shared__ int32_t psrc[kOtMaxTiles];       // node-relative (M <= kOtMaxTiles: < 2^20)
   __shared__ int64_t slab_off[kOtSlabs + 1];  // node-relative first position of each slab
@@ -655,21 +666,27 @@ __global__ __launch_bounds__(64 * NW, 16 / NW) void k_ot_merge(const uint16_t* _
           },
           ps, psrc, wsum);
 #if CG_OT_OWN_SEARCH
-      ot_gather<true, true>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl, int(M));
+      ot_gather<true, true, PACK>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl, int(M));
 #else
       ot_owners<NW>(ps, int(M), 0, n_el, own, wsum);
-      ot_gather<true>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl);
+      ot_gather<true, false, PACK>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl);
 #endif
       // by rel = offset - the run's first second (< 64 * (jb - ja)): one
       // 8-bit pass for up to 4 slabs
-      ot_sort<NW, 256>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
+      constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
+      ot_sort<NW, 256, false, IB>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
       const int64_t o = lo_n + slab_off[ja];
       bool bad = false;
       for (int p = threadIdx.x; p < n_el; p += kThreads) {
         const uint32_t v = pk[p];
-        __builtin_nontemporal_store(t0 + 1 + int64_t(v >> kOtIdxBits), tout + o + p);
-        __builtin_nontemporal_store(rl[v & kOtIdxMask], rout + o + p);
-        if (p > 0) bad |= ot_out_of_order(pk[p - 1], v, rl);  // (time, rule) order of the chunk
+        __builtin_nontemporal_store(t0 + 1 + int64_t(v >> IB), tout + o + p);
+        if (PACK) {
+          __builtin_nontemporal_store(int32_t(v & ((1u << kOtRuleBits) - 1u)), rout + o + p);
+          if (p > 0) bad |= pk[p - 1] >= v;  // (time, rule) order of the chunk: the words ascend
+        } else {
+          __builtin_nontemporal_store(rl[v & kOtIdxMask], rout + o + p);
+          if (p > 0) bad |= ot_out_of_order(pk[p - 1], v, rl);  // (time, rule) order of the chunk
+        }
       }
       if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
       ot_sync<NW>();
@@ -980,6 +997,10 @@ __global__ __launch_bounds__(256) void k_node_tile(
 
 int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads - 1) / threads)); }
 
+#ifndef CG_OT_PACK
+#define CG_OT_PACK 1
+#endif
+
 }  // namespace
 
 // Windows <= 4096 s, in three steps enqueued on st with no host sync (buffers
@@ -1011,15 +1032,21 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
   return CG_OK;
 }
 
-int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, hipStream_t st, int64_t* err) {
+int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, hipStream_t st, int64_t* err, int64_t R) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
   HIPCHK(hipMemsetAsync(big_n, 0, 8, st));
   int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
-  hipLaunchKernelGGL(k_ot_merge<kOtMergeWaves>, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
-                     c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
-                     c->node_rule.p, c->ts_off.p, big_n, err);
+  // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
+  if (CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits))
+    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, true>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
+                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
+                       c->node_rule.p, c->ts_off.p, big_n, err);
+  else
+    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, false>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
+                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
+                       c->node_rule.p, c->ts_off.p, big_n, err);
   hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
                      c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
                      c->ts_off.p, big_n, err);
@@ -1046,7 +1073,7 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
     hipLaunchKernelGGL(k_ot_tile<false>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
                        c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
                        c->ts_base.p + N, err);
-  return order_tail(c, node_off, N, t0, st, err);
+  return order_tail(c, node_off, N, t0, st, err, c->pn_R);
 }
 
 // The per-node writer and tile sort in one (k_node_tile), then the merge: the
@@ -1063,7 +1090,7 @@ int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int6
   hipLaunchKernelGGL(k_node_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec, a.recs,
                      a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
                      reinterpret_cast<uint16_t*>(c->node_time2.p), c->node_rule2.p, c->ts_hist.p, n_tiles, err);
-  return order_tail(c, a.node_off, a.N, a.t0, st, err);
+  return order_tail(c, a.node_off, a.N, a.t0, st, err, c->pn_R);
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {

@@ -1022,6 +1022,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   const bool cached = in.serial != 0 && in.serial == c->pn_cache_serial && mode == c->pn_cache_mode;
   c->pn_E = 0;  // no readable result until this call succeeds
   c->pn_time_ordered = false;
+  c->pn_R = R;
   (void)hipEventRecord(c->pev[0], st);
   if (cached) {
     nnz = c->pn_nnz;
@@ -1312,6 +1313,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
   const int64_t R = in.n_rules, NK = int64_t(N) * K, nnz = c->pn_nnz;
   hipStream_t sc = c->st_cs, st = c->st;
   const bool timed = c->node_order == CG_NODE_ORDER_TIME;
+  c->pn_R = R;
   if (timed && t1 - t0 > 4096)
     return cg_fail(CG_EINVAL, "pipelined per-node windows in time order: windows of at most 4096 s");
   bool empty = false;
