@@ -202,12 +202,17 @@ constexpr int kOtTile = 4 * 64 * kOtItems;    // 4096 events: the tile sort's 4-
 #define CG_OT_MERGE_WAVES 4
 #endif
 constexpr int kOtMergeWaves = CG_OT_MERGE_WAVES;  // k_ot_merge: waves per node
+#ifndef CG_OT_MERGE_ITEMS
+#define CG_OT_MERGE_ITEMS 16
+#endif
+constexpr int kOtMergeItems = CG_OT_MERGE_ITEMS;  // k_ot_merge: events per thread of a chunk
 // the merge's packed words when every rule index is below 2^20: offset << 20 |
 // rule (the word order is the (time, rule) order; no rule array in LDS)
 constexpr int kOtRuleBits = 20;
-// chunk index bits of a packed word (offset << kOtIdxBits | index): the merge's
-// chunk is 64 * 16 * kOtMergeWaves events
-constexpr int kOtIdxBits = kOtMergeWaves > 4 ? 13 : 12;
+// chunk index bits of a packed word (offset << kOtIdxBits | index): up to
+// 8192 events (k_ot_mid's chunk: 8 waves x 64 x 16)
+constexpr int kOtIdxBits = 13;
+constexpr int kOtMidWaves = 8;  // k_ot_mid: waves per slab
 static_assert(kOtMergeWaves <= 8 && 12 + kOtIdxBits <= 32, "packed words");
 constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
 constexpr int kOtSlabBits = 6;               // slab = offset >> kOtSlabBits (64 s): one 6-bit digit
@@ -248,8 +253,8 @@ struct OtRank {
 // runs of neighbouring elements (slabs of a rule-major tile: one rule's
 // events sit in neighbouring seconds) would otherwise serialise its lanes on
 // one LDS address.  Ends synchronised.
-template <int NW, int D, bool RUNS = false>
-__device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, int32_t (&pos)[kOtItems],
+template <int NW, int D, bool RUNS = false, int IT = kOtItems>
+__device__ __forceinline__ void ot_rank(const uint32_t (&dg)[IT], int n, int32_t (&pos)[IT],
                                         OtRank<NW, D>& s) {
   static_assert(D == 64 || D == 256, "digits");
   constexpr int P = D / 64;  // digits per lane in the scan
@@ -257,10 +262,10 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, i
   uint32_t* run = reinterpret_cast<uint32_t*>(s.run[w]);
 #pragma unroll
   for (int i = 0; i < P; i++) run[lane + 64 * i] = 0;
-  const int ebase = w * (64 * kOtItems);
+  const int ebase = w * (64 * IT);
   const uint64_t upto = ~0ull >> (63 - lane);  // lanes 0 .. lane
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) {
+  for (int j = 0; j < IT; j++) {
     const bool valid = ebase + j * 64 + lane < n;
     if constexpr (RUNS) {
       const uint32_t d = valid ? dg[j] : uint32_t(D);  // invalid lanes (the tail) add nothing
@@ -310,37 +315,37 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[kOtItems], int n, i
   }
   ot_sync<NW>();
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) pos[j] += s.run[w][dg[j]];
+  for (int j = 0; j < IT; j++) pos[j] += s.run[w][dg[j]];
 }
 
 // Stable sort of n packed words (offset << 12 | index) held as items by
 // digits of rel = offset - lo: `passes` (1 or 2) passes of log2(D) bits from
 // bit sh of rel up; the sorted words end in pk[0..n).  Ends synchronised.
-template <int NW, int D, bool RUNS = false, int IB = kOtIdxBits>  // IB: bits below the offset
-__device__ __forceinline__ void ot_sort(uint32_t (&key)[kOtItems], int n, uint32_t lo, int sh, int passes,
+template <int NW, int D, bool RUNS = false, int IB = kOtIdxBits, int IT = kOtItems>  // IB: bits below the offset; IT: items per thread
+__device__ __forceinline__ void ot_sort(uint32_t (&key)[IT], int n, uint32_t lo, int sh, int passes,
                                         uint32_t* pk, OtRank<NW, D>& s) {
   constexpr int B = D == 64 ? 6 : 8;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ebase = w * (64 * kOtItems);
-  uint32_t dg[kOtItems];
-  int32_t pos[kOtItems];
+  const int ebase = w * (64 * IT);
+  uint32_t dg[IT];
+  int32_t pos[IT];
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) dg[j] = (((key[j] >> IB) - lo) >> sh) & uint32_t(D - 1);
-  ot_rank<NW, D, RUNS>(dg, n, pos, s);
+  for (int j = 0; j < IT; j++) dg[j] = (((key[j] >> IB) - lo) >> sh) & uint32_t(D - 1);
+  ot_rank<NW, D, RUNS, IT>(dg, n, pos, s);
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++)
+  for (int j = 0; j < IT; j++)
     if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
   ot_sync<NW>();
   if (passes == 1) return;
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) {
+  for (int j = 0; j < IT; j++) {
     const int e = ebase + j * 64 + lane;
     key[j] = e < n ? pk[e] : 0u;
     dg[j] = (((key[j] >> IB) - lo) >> (sh + B)) & uint32_t(D - 1);
   }
-  ot_rank<NW, D>(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
+  ot_rank<NW, D, false, IT>(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++)
+  for (int j = 0; j < IT; j++)
     if (ebase + j * 64 + lane < n) pk[pos[j]] = key[j];
   ot_sync<NW>();
 }
@@ -473,7 +478,7 @@ __device__ __forceinline__ int ot_find(const int32_t* ps, int Q, int32_t e) {
 // per-thread runs of kOtItems do not collide in the LDS banks.  Ends
 // synchronised.
 __device__ __forceinline__ int ot_pad(int i) { return i + (i >> 5); }
-template <int NW>
+template <int NW, int IT = kOtItems>
 __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, int n_el, int32_t* own,
                                           int32_t* wsum) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -485,10 +490,10 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
   }
   if (threadIdx.x == 0) own[0] = ot_find(ps, Q, c0);  // the portion the chunk starts in (the same q if it starts at c0)
   ot_sync<NW>();
-  int32_t v[kOtItems], m = -1;
+  int32_t v[IT], m = -1;
 #pragma unroll
-  for (int i = 0; i < kOtItems; i++) {
-    const int idx = threadIdx.x * kOtItems + i;
+  for (int i = 0; i < IT; i++) {
+    const int idx = threadIdx.x * IT + i;
     v[i] = idx < n_el ? own[ot_pad(idx)] : -1;
     m = v[i] > m ? v[i] : m;
     v[i] = m;
@@ -507,8 +512,8 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
     for (int ww = 0; ww < w; ww++) prev = wsum[ww] > prev ? wsum[ww] : prev;
   }
 #pragma unroll
-  for (int i = 0; i < kOtItems; i++) {
-    const int idx = threadIdx.x * kOtItems + i;
+  for (int i = 0; i < IT; i++) {
+    const int idx = threadIdx.x * IT + i;
     if (idx < n_el) own[ot_pad(idx)] = v[i] > prev ? v[i] : prev;
   }
   ot_sync<NW>();
@@ -521,16 +526,16 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 // SEARCH: each element finds its portion by a binary search of ps (Q
 // portions) instead of reading the owner map (no ot_owners pass)
 // PACK: key = offset << kOtRuleBits | rule (rules < 2^kOtRuleBits), no rl
-template <bool RULES, bool SEARCH = false, bool PACK = false>
+template <bool RULES, bool SEARCH = false, bool PACK = false, int IT = kOtItems>
 __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                           const int32_t* ps, const int32_t* psrc, const int32_t* own,
-                                          int32_t c0, int n_el, uint32_t (&key)[kOtItems], int32_t* rl, int Q = 0) {
+                                          int32_t c0, int n_el, uint32_t (&key)[IT], int32_t* rl, int Q = 0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ebase = w * (64 * kOtItems);
-  uint32_t tv[kOtItems];
-  int32_t rv[kOtItems];
+  const int ebase = w * (64 * IT);
+  uint32_t tv[IT];
+  int32_t rv[IT];
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) {
+  for (int j = 0; j < IT; j++) {
     const int e = ebase + j * 64 + lane;
     const int ec = e < n_el ? e : n_el - 1;
     const int q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
@@ -539,7 +544,7 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
     if (RULES) rv[j] = rin[src];
   }
 #pragma unroll
-  for (int j = 0; j < kOtItems; j++) {
+  for (int j = 0; j < IT; j++) {
     const int e = ebase + j * 64 + lane;
     if (PACK) {
       key[j] = e < n_el ? (tv[j] << kOtRuleBits) | uint32_t(rv[j]) : 0u;
@@ -594,19 +599,71 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 #ifndef CG_OT_OWN_SEARCH
 #define CG_OT_OWN_SEARCH 0
 #endif
+#ifndef CG_OT_MID_WPE
+#define CG_OT_MID_WPE 4  // min waves per SIMD of k_ot_mid (8-wave blocks: 2 per SIMD each)
+#endif
+#ifndef CG_OT_MID
+#define CG_OT_MID 1  // 0: every slab of more than a merge chunk to k_ot_big (A/B)
+#endif
 #ifndef CG_OT_MERGE_WPE
 #define CG_OT_MERGE_WPE 4  // min waves per SIMD of the packed merge (its LDS allows 6 blocks per CU)
 #endif
-template <int NW, bool PACK>
-__global__ __launch_bounds__(64 * NW, (PACK ? CG_OT_MERGE_WPE : 4) * 4 / NW) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
+
+// One chunk of n_el <= 64 * NW * kOtItems events of a node (tin_n / rin_n:
+// the node's tile-sorted offsets and rules): the M tiles' portions
+// (portion(q, &src) -> count, thread q's tile; src node-relative), gathered,
+// sorted in LDS by rel = offset - lo (`passes` 8-bit passes) and stored at
+// tout_o / rout_o in (time, rule) order.  Ends synchronised.
+template <int NW, bool PACK, int IT, class Portion>
+__device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_n, const int32_t* __restrict__ rin_n,
+                                               int M, int n_el, uint32_t lo, int passes, Portion&& portion,
+                                               int64_t t0, int64_t* __restrict__ tout_o,
+                                               int32_t* __restrict__ rout_o, OtRank<NW, 256>& s, uint32_t* pk,
+                                               int32_t* rl, int32_t* ps, int32_t* psrc, int32_t* wsum,
+                                               int64_t* __restrict__ err) {
+  int32_t* own = reinterpret_cast<int32_t*>(pk);
+  uint32_t key[IT];
+  ot_portions<NW>(M, portion, ps, psrc, wsum);
+#if CG_OT_OWN_SEARCH
+  ot_gather<true, true, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M);
+#else
+  ot_owners<NW, IT>(ps, M, 0, n_el, own, wsum);
+  ot_gather<true, false, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl);
+#endif
+  constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
+  ot_sort<NW, 256, false, IB, IT>(key, n_el, lo, 0, passes, pk, s);
+  bool bad = false;
+  for (int p = threadIdx.x; p < n_el; p += 64 * NW) {
+    const uint32_t v = pk[p];
+    __builtin_nontemporal_store(t0 + 1 + int64_t(v >> IB), tout_o + p);
+    if (PACK) {
+      __builtin_nontemporal_store(int32_t(v & ((1u << kOtRuleBits) - 1u)), rout_o + p);
+      if (p > 0) bad |= pk[p - 1] >= v;  // (time, rule) order of the chunk: the words ascend
+    } else {
+      __builtin_nontemporal_store(rl[v & kOtIdxMask], rout_o + p);
+      if (p > 0) bad |= ot_out_of_order(pk[p - 1], v, rl);  // (time, rule) order of the chunk
+    }
+  }
+  if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
+  ot_sync<NW>();
+}
+
+// Per node: its slabs in runs that fit one chunk, each merged by
+// ot_merge_chunk.  A slab of more than a chunk is queued: to k_ot_mid when it
+// fits k_ot_mid's chunk (mid / mid_n), else to k_ot_big (big / big_n);
+// entries (node << 8 | slab).
+template <int NW, bool PACK, int IT = kOtItems>
+__global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
                                                        const int32_t* __restrict__ pre, int32_t N, int64_t t0,
                                                        const int64_t* __restrict__ slab_tab,
                                                        int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                        int64_t* __restrict__ big, unsigned* __restrict__ big_n,
+                                                       int64_t* __restrict__ mid, unsigned* __restrict__ mid_n,
                                                        int64_t* __restrict__ err) {
-  constexpr int kThreads = 64 * NW, kChunk = kThreads * kOtItems;
+  constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
+  constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems;
   __shared__ OtRank<NW, 256> s;
   __shared__ uint32_t pk[kChunk + kChunk / 32];  // the owner list while gathering (padded), then the sorted words
   __shared__ int32_t rl[PACK ? 1 : kChunk];
@@ -614,7 +671,6 @@ __global__ __launch_bounds__(64 * NW, (PACK ? CG_OT_MERGE_WPE : 4) * 4 / NW) voi
   __shared__ int32_t psrc[kOtMaxTiles];       // node-relative (M <= kOtMaxTiles: < 2^20)
   __shared__ int64_t slab_off[kOtSlabs + 1];  // node-relative first position of each slab
   __shared__ int32_t wsum[NW];
-  int32_t* own = reinterpret_cast<int32_t*>(pk);
   const int32_t n = blockIdx.x;
   if (n >= N) return;
   const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta, lo_n = node_off[n];
@@ -633,7 +689,6 @@ __global__ __launch_bounds__(64 * NW, (PACK ? CG_OT_MERGE_WPE : 4) * 4 / NW) voi
   }
   for (int j = threadIdx.x; j <= kOtSlabs; j += kThreads) slab_off[j] = slab_tab[int64_t(n) * kOtPre + j];
   ot_sync<NW>();
-  uint32_t key[kOtItems];
   // the longest run of whole slabs [j0, j1) that fits one chunk (j1 == j0: a
   // slab of more than a chunk)
   auto run_end = [&](int j0) {
@@ -654,47 +709,71 @@ __global__ __launch_bounds__(64 * NW, (PACK ? CG_OT_MERGE_WPE : 4) * 4 / NW) voi
     const int32_t pa2 = jb == ja ? pq[ja2 <= kOtSlabs ? ja2 : kOtSlabs] : pb;
     const int32_t pb2 = pq[jb2 <= kOtSlabs ? jb2 : kOtSlabs];  // in flight while this run is merged
     if (jb == ja) {  // one slab of more than a chunk
-      if (threadIdx.x == 0) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | ja;
+      if (threadIdx.x == 0) {
+        if (CG_OT_MID && slab_off[ja + 1] - slab_off[ja] <= kMidChunk) mid[atomicAdd(mid_n, 1u)] = (int64_t(n) << 8) | ja;
+        else big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | ja;
+      }
     } else if (slab_off[jb] > slab_off[ja]) {
-      const int n_el = int(slab_off[jb] - slab_off[ja]);
-      // per tile its sorted events of slabs [ja, jb): one contiguous range
-      ot_portions<NW>(
-          int(M),
+      // per tile its sorted events of slabs [ja, jb): one contiguous range; by
+      // rel = offset - the run's first second (< 64 * (jb - ja)): one 8-bit
+      // pass for up to 4 slabs
+      const int64_t o = lo_n + slab_off[ja];
+      ot_merge_chunk<NW, PACK, IT>(
+          tin + lo_n, rin + lo_n, int(M), int(slab_off[jb] - slab_off[ja]), uint32_t(ja) << kOtSlabBits,
+          jb - ja > 4 ? 2 : 1,
           [&](int q, int32_t* src) {
             *src = q * kOtTile + pa;  // q == q_own
             return pb - pa;
           },
-          ps, psrc, wsum);
-#if CG_OT_OWN_SEARCH
-      ot_gather<true, true, PACK>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl, int(M));
-#else
-      ot_owners<NW>(ps, int(M), 0, n_el, own, wsum);
-      ot_gather<true, false, PACK>(tin + lo_n, rin + lo_n, ps, psrc, own, 0, n_el, key, rl);
-#endif
-      // by rel = offset - the run's first second (< 64 * (jb - ja)): one
-      // 8-bit pass for up to 4 slabs
-      constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
-      ot_sort<NW, 256, false, IB>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
-      const int64_t o = lo_n + slab_off[ja];
-      bool bad = false;
-      for (int p = threadIdx.x; p < n_el; p += kThreads) {
-        const uint32_t v = pk[p];
-        __builtin_nontemporal_store(t0 + 1 + int64_t(v >> IB), tout + o + p);
-        if (PACK) {
-          __builtin_nontemporal_store(int32_t(v & ((1u << kOtRuleBits) - 1u)), rout + o + p);
-          if (p > 0) bad |= pk[p - 1] >= v;  // (time, rule) order of the chunk: the words ascend
-        } else {
-          __builtin_nontemporal_store(rl[v & kOtIdxMask], rout + o + p);
-          if (p > 0) bad |= ot_out_of_order(pk[p - 1], v, rl);  // (time, rule) order of the chunk
-        }
-      }
-      if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
-      ot_sync<NW>();
+          t0, tout + o, rout + o, s, pk, rl, ps, psrc, wsum, err);
     }
     ja = ja2;
     jb = jb2;
     pa = pa2;
     pb = pb2;
+  }
+}
+
+// The slabs k_ot_merge queued for a bigger chunk (more than its own, at most
+// 64 * kOtMidWaves * kOtItems events), one per workgroup turn: the same
+// gather + one-pass LDS sort with NW waves (a slab of 64 s: one 8-bit pass).
+template <int NW, bool PACK, int IT = kOtItems>
+__global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
+                                                    const int64_t* __restrict__ tile_base,
+                                                    const int64_t* __restrict__ node_off,
+                                                    const int32_t* __restrict__ pre, int64_t t0,
+                                                    const int64_t* __restrict__ slab_tab,
+                                                    int64_t* __restrict__ tout, int32_t* __restrict__ rout,
+                                                    const int64_t* __restrict__ mid,
+                                                    const unsigned* __restrict__ mid_n, int64_t* __restrict__ err) {
+  constexpr int kChunk = 64 * NW * IT;
+  __shared__ OtRank<NW, 256> s;
+  __shared__ uint32_t pk[kChunk + kChunk / 32];
+  __shared__ int32_t rl[PACK ? 1 : kChunk];
+  __shared__ int32_t ps[kOtMaxTiles + 1];
+  __shared__ int32_t psrc[kOtMaxTiles];
+  __shared__ int32_t wsum[NW];
+  static_assert(kOtMaxTiles <= 64 * NW, "one tile per thread");
+  const unsigned nm = *mid_n;
+  for (unsigned task = blockIdx.x; task < nm; task += gridDim.x) {
+    const int64_t e = mid[task];
+    const int32_t n = int32_t(e >> 8);
+    const int j = int(e & 255);
+    const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta, lo_n = node_off[n];
+    const int64_t* so = slab_tab + int64_t(n) * kOtPre;
+    const int64_t a = so[j], n_el = so[j + 1] - a;
+    if (n_el <= 0 || n_el > kChunk || M > kOtMaxTiles) {  // never queued so
+      if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
+      continue;
+    }
+    ot_merge_chunk<NW, PACK, IT>(
+        tin + lo_n, rin + lo_n, int(M), int(n_el), uint32_t(j) << kOtSlabBits, 1,
+        [&](int q, int32_t* src) {
+          const int32_t* pt = pre + (ta + q) * kOtPre;
+          *src = q * kOtTile + pt[j];
+          return pt[j + 1] - pt[j];
+        },
+        t0, tout + lo_n + a, rout + lo_n + a, s, pk, rl, ps, psrc, wsum, err);
   }
 }
 
@@ -1013,7 +1092,8 @@ namespace {
 int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipStream_t st, int64_t* Tmax) {
   *Tmax = cap / kOtTile + N + 1;
   const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
-  const int64_t tab = int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre;
+  // ts_off: [k_ot_big queue N*kOtSlabs][big, mid counters][slab_tab N*kOtPre][k_ot_mid queue N*kOtSlabs]
+  const int64_t tab = 2 * int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre;
   // growing a buffer frees the old one: earlier windows' kernels finish first
   if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(*Tmax) ||
       c->ts_hist.cap < size_t(*Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
@@ -1034,19 +1114,28 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
 
 int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, hipStream_t st, int64_t* err, int64_t R) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
-  unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
+  unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);  // [0] big, [1] mid
   HIPCHK(hipMemsetAsync(big_n, 0, 8, st));
   int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
+  int64_t* mid = slab_tab + int64_t(N) * kOtPre;
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
+  const int cus = std::max(1, c->write_blocks / kWriteBlocksPerCU);
   // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
-  if (CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits))
-    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, true>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
+  if (CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits)) {
+    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, true, kOtMergeItems>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
                        c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
-                       c->node_rule.p, c->ts_off.p, big_n, err);
-  else
-    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, false>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
+                       c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, err);
+    hipLaunchKernelGGL((k_ot_mid<kOtMidWaves, true>), dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, st, toff,
+                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p,
+                       c->node_rule.p, mid, big_n + 1, err);
+  } else {
+    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, false, kOtMergeItems>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
                        c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
-                       c->node_rule.p, c->ts_off.p, big_n, err);
+                       c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, err);
+    hipLaunchKernelGGL((k_ot_mid<kOtMidWaves, false>), dim3(unsigned(cus * 2)), dim3(64 * kOtMidWaves), 0, st, toff,
+                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p,
+                       c->node_rule.p, mid, big_n + 1, err);
+  }
   hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
                      c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
                      c->ts_off.p, big_n, err);

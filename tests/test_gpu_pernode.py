@@ -297,7 +297,7 @@ def progression_rules(R, n_nodes):
 
 @pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("R,N,secs,star_every", [(1200, 3, 3600, 13), (2600, 2, 4096, 2), (64, 1, 61, 3),
-                                                 (12000, 1, 120, 1), (40, 1, 4096, 10**9)])
+                                                 (12000, 1, 120, 1), (40, 1, 4096, 10**9), (200, 1, 3600, 2)])
 def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
     """The one-pass time order on nodes far larger than one LDS chunk:
     every-second rules put > 4096 events into one 64-s slab (the slab is
@@ -307,7 +307,9 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
     12000 every-second rules on one node: every second holds more events than
     a merge chunk (k_ot_big sorts the slab chunk by chunk).  40 sparse rules
     on one node over 4096 s: ~7 k events in two tiles, merge runs of dozens of
-    slabs (sorted in two 8-bit passes).
+    slabs (sorted in two 8-bit passes).  200 rules on one node, every other one
+    every second, over 1 h: ~6.5 k events per slab, each merged by k_ot_mid's
+    8192-event chunk.
     Against the oracle's lists sorted by (time, rule)."""
     specs = [PROGRESSION_MIX[0] if i % star_every == 0 else PROGRESSION_MIX[1 + i % (len(PROGRESSION_MIX) - 1)]
              for i in range(R)]
@@ -333,6 +335,9 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
         assert np.array_equal(rule2[a:b], exp_r[order]), n
     if R == 2600:
         assert (np.diff(node_off) > 1024 * 4096).all()
+    if R == 200:  # every slab between a merge chunk and a k_ot_mid chunk
+        per_slab = node_off[1] / (secs / 64)
+        assert 4096 < per_slab < 8192 and node_off[1] < 256 * 4096
     if R == 40:  # two tiles, runs of more than 4 slabs
         assert 4096 < node_off[1] < 2 * 4096 and node_off[1] < 64 * 4096 // 8
 
