@@ -358,17 +358,29 @@ __device__ __forceinline__ bool ot_out_of_order(uint32_t u, uint32_t v, const in
   return a > b || (a == b && rl[u & kOtIdxMask] >= rl[v & kOtIdxMask]);
 }
 
-template <bool IN16>  // times as 16-bit offsets t - t0 - 1 (else int64 times, their low words read)
-__global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ time, const int32_t* __restrict__ rule,
+#ifndef CG_OT_TILE_PACK
+#define CG_OT_TILE_PACK 1  // 0: the tile sort keeps an LDS rule array (A/B)
+#endif
+#ifndef CG_OT_TILE_WPE
+#define CG_OT_TILE_WPE 6  // min waves per SIMD of the packed tile sort (its LDS allows 9 blocks per CU)
+#endif
+// PACK (rule indices < 2^kOtRuleBits): the sorted words are offset << 20 |
+// rule, so no rule array in LDS (17 KB per block instead of 34: more blocks
+// per CU); the sorts are stable, so the rule-major order inside a slab (and
+// the rule order of equal offsets) carries through without the index.
+template <bool IN16, bool PACK>  // IN16: times as 16-bit offsets t - t0 - 1 (else int64 times, their low words read)
+__global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(const int64_t* __restrict__ time, const int32_t* __restrict__ rule,
                                                   const int32_t* __restrict__ tile_node,
                                                   const int64_t* __restrict__ tile_base,
                                                   const int64_t* __restrict__ node_off, int64_t t0,
                                                   uint16_t* __restrict__ toff_out, int32_t* __restrict__ rule_out,
                                                   int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles,
                                                   int64_t* __restrict__ err) {
+  constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
+  constexpr uint32_t kLow = (1u << IB) - 1u;
   __shared__ OtRank<4, 64> s;
   __shared__ uint32_t pk[kOtTile];
-  __shared__ int32_t rl[kOtTile];
+  __shared__ int32_t rl[PACK ? 1 : kOtTile];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t t = blockIdx.x;
   if (t >= *n_tiles) return;  // the grid may be an upper bound (pipelined windows)
@@ -390,31 +402,35 @@ __global__ __launch_bounds__(256) void k_ot_tile(const int64_t* __restrict__ tim
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
     const int e = ebase + j * 64 + lane;
-    key[j] = e < n ? ((tv[j] - b) << kOtIdxBits) | uint32_t(e) : 0u;
-    if (e < n) rl[e] = rv[j];
+    if constexpr (PACK) {
+      key[j] = e < n ? ((tv[j] - b) << IB) | uint32_t(rv[j]) : 0u;
+    } else {
+      key[j] = e < n ? ((tv[j] - b) << IB) | uint32_t(e) : 0u;
+      if (e < n) rl[e] = rv[j];
+    }
   }
   // by slab; a node's only tile by the whole offset (its last pass is the slab)
   const int32_t nd = tile_node[t];
   const bool one = tile_base[nd + 1] - tile_base[nd] == 1;
-  if (one) ot_sort<4, 64>(key, n, 0u, 0, 2, pk, s);
-  else ot_sort<4, 64, true>(key, n, 0u, kOtSlabBits, 1, pk, s);
+  if (one) ot_sort<4, 64, false, IB>(key, n, 0u, 0, 2, pk, s);
+  else ot_sort<4, 64, true, IB>(key, n, 0u, kOtSlabBits, 1, pk, s);
   int32_t* __restrict__ pt = pre + t * kOtPre;
   if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];  // slabs = the last pass's digits
+  auto rule_of = [&](uint32_t v) { return PACK ? int32_t(v & kLow) : rl[v & kLow]; };
   bool bad = false;
   for (int p = threadIdx.x; p < n; p += 256) {
     const uint32_t v = pk[p];
-    toff_out[r.lo + p] = uint16_t(v >> kOtIdxBits);
-    __builtin_nontemporal_store(rl[v & kOtIdxMask], rule_out + r.lo + p);
+    toff_out[r.lo + p] = uint16_t(v >> IB);
+    __builtin_nontemporal_store(rule_of(v), rule_out + r.lo + p);
     // the ranks rest on lane-ordered LDS atomics (ot_rank): check the order
     // they produced -- a node's only tile is final: (offset, rule) ascending;
     // a partitioned tile keeps rule order inside each slab
     if (p > 0) {
       const uint32_t u = pk[p - 1];
-      if (one) bad |= ot_out_of_order(u, v, rl);
-      else if ((u >> (kOtIdxBits + kOtSlabBits)) == (v >> (kOtIdxBits + kOtSlabBits))) {
-        const int32_t ru = rl[u & kOtIdxMask], rv = rl[v & kOtIdxMask];  // rule-major: (rule, offset)
-        bad |= ru > rv || (ru == rv && (u >> kOtIdxBits) >= (v >> kOtIdxBits));
-      }
+      const int32_t ru = rule_of(u), rv2 = rule_of(v);
+      const uint32_t ou = u >> IB, ov = v >> IB;
+      if (one) bad |= ou > ov || (ou == ov && ru >= rv2);
+      else if ((ou >> kOtSlabBits) == (ov >> kOtSlabBits)) bad |= ru > rv2 || (ru == rv2 && ou >= ov);  // rule-major
     }
   }
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
@@ -526,7 +542,10 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 // SEARCH: each element finds its portion by a binary search of ps (Q
 // portions) instead of reading the owner map (no ot_owners pass)
 // PACK: key = offset << kOtRuleBits | rule (rules < 2^kOtRuleBits), no rl
-template <bool RULES, bool SEARCH = false, bool PACK = false, int IT = kOtItems>
+// SEARCH 2: the lane's first element finds its portion by a binary search,
+// each later item (64 elements on) walks forward from there (portions are
+// consecutive, so a few steps at most)
+template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems>
 __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                           const int32_t* ps, const int32_t* psrc, const int32_t* own,
                                           int32_t c0, int n_el, uint32_t (&key)[IT], int32_t* rl, int Q = 0) {
@@ -534,12 +553,29 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
   const int ebase = w * (64 * IT);
   uint32_t tv[IT];
   int32_t rv[IT];
+  int qw = 0, qa = 0, qb = 0;  // SEARCH 2: the current portion and its bounds ps[qw], ps[qw + 1]
+  if (SEARCH == 2) {
+    const int e0 = ebase + lane < n_el ? ebase + lane : n_el - 1;
+    qw = ot_find(ps, Q, c0 + e0);
+    qa = ps[qw];
+    qb = ps[qw + 1];
+  }
 #pragma unroll
   for (int j = 0; j < IT; j++) {
     const int e = ebase + j * 64 + lane;
     const int ec = e < n_el ? e : n_el - 1;
-    const int q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
-    const uint32_t src = uint32_t(psrc[q] + (c0 + ec - ps[q]));
+    int q;
+    if (SEARCH == 2) {
+      while (qb <= c0 + ec && qw + 1 < Q) {
+        qw++;
+        qa = qb;
+        qb = ps[qw + 1];
+      }
+      q = qw;
+    } else {
+      q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
+    }
+    const uint32_t src = uint32_t(psrc[q] + (c0 + ec - (SEARCH == 2 ? qa : ps[q])));
     tv[j] = tin[src];
     if (RULES) rv[j] = rin[src];
   }
@@ -597,7 +633,7 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 }
 
 #ifndef CG_OT_OWN_SEARCH
-#define CG_OT_OWN_SEARCH 0
+#define CG_OT_OWN_SEARCH 2  // the merge's portion per element: 0 owner map, 1 binary search, 2 search + walk
 #endif
 #ifndef CG_OT_MID_WPE
 #define CG_OT_MID_WPE 4  // min waves per SIMD of k_ot_mid (8-wave blocks: 2 per SIMD each)
@@ -625,10 +661,10 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   uint32_t key[IT];
   ot_portions<NW>(M, portion, ps, psrc, wsum);
 #if CG_OT_OWN_SEARCH
-  ot_gather<true, true, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M);
+  ot_gather<true, CG_OT_OWN_SEARCH, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M);
 #else
   ot_owners<NW, IT>(ps, M, 0, n_el, own, wsum);
-  ot_gather<true, false, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl);
+  ot_gather<true, 0, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl);
 #endif
   constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
   ot_sort<NW, 256, false, IB, IT>(key, n_el, lo, 0, passes, pk, s);
@@ -1154,14 +1190,13 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   int rc = order_setup(c, node_off, N, cap, st, &Tmax);
   if (rc) return rc;
   uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
-  if (in16)
-    hipLaunchKernelGGL(k_ot_tile<true>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
-                       c->ts_base.p + N, err);
-  else
-    hipLaunchKernelGGL(k_ot_tile<false>, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p,
-                       c->ts_tile_node.p, c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p,
-                       c->ts_base.p + N, err);
+  const bool pack = CG_OT_TILE_PACK && c->pn_R <= (int64_t(1) << kOtRuleBits);
+  auto tile = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p, c->ts_tile_node.p,
+                       c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p, c->ts_base.p + N, err);
+  };
+  if (in16) pack ? tile(k_ot_tile<true, true>) : tile(k_ot_tile<true, false>);
+  else pack ? tile(k_ot_tile<false, true>) : tile(k_ot_tile<false, false>);
   return order_tail(c, node_off, N, t0, st, err, c->pn_R);
 }
 
