@@ -245,6 +245,10 @@ struct cg_ctx {
   int node_order = CG_NODE_ORDER_RULE;  // cg_set_node_order
   bool pn_time_ordered = false;         // the last per-node result is in (time, rule) order
   int32_t pn_B = 0, pn_K = 0;  // rules per band, bands of the cached segment bounds (0: none)
+  // the time-order merge's dense nodes run on their own stream beside the
+  // sparse ones (fork / join events on st)
+  hipStream_t st_ot = nullptr;
+  hipEvent_t ot_fork = nullptr, ot_join = nullptr;
 
   void free_all() {
     for (AsyncSet& a : as) a.release();
@@ -253,6 +257,10 @@ struct cg_ctx {
       if (e) (void)hipEventDestroy(e), e = nullptr;
     if (st_cs) (void)hipStreamDestroy(st_cs);
     st_cs = nullptr;
+    if (ot_fork) (void)hipEventDestroy(ot_fork), ot_fork = nullptr;
+    if (ot_join) (void)hipEventDestroy(ot_join), ot_join = nullptr;
+    if (st_ot) (void)hipStreamDestroy(st_ot);
+    st_ot = nullptr;
     plan_dev.release();
     run_anchor.release(); run_off.release(); offsets.release(); times.release();
     block_run.release(); nb_in.release(); nb_out.release(); run_count.release();
@@ -338,8 +346,8 @@ struct FusedOrderArgs {
 int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int64_t* err);
 // err: a device word the kernels set when a sorted chunk is out of (time,
 // rule) order (the sorts' ranks rest on lane-ordered LDS atomics; checked)
-int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
-                        bool in16, int64_t* err);
+int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
+                        hipStream_t st, bool in16, int64_t* err);
 constexpr const char* kOrderCheckMsg =
     "time-order pass: a sorted chunk came out of (time, rule) order (its LDS-atomic ranks were not in lane order)";
 // the mapped pinned per-node result words: [0] node events, [1] size error, [2] order check

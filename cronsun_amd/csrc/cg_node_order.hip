@@ -545,14 +545,27 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 // SEARCH 2: the lane's first element finds its portion by a binary search,
 // each later item (64 elements on) walks forward from there (portions are
 // consecutive, so a few steps at most)
-template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems>
+// BUF: the loads as raw buffer loads (32-bit offsets against a descriptor
+// over n_src elements; an index past it reads 0): one VGPR per address
+// instead of two, and no 64-bit address arithmetic per item
+#ifndef CG_OT_BUF
+#define CG_OT_BUF 1
+#endif
+template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems, bool BUF = false>
 __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                           const int32_t* ps, const int32_t* psrc, const int32_t* own,
-                                          int32_t c0, int n_el, uint32_t (&key)[IT], int32_t* rl, int Q = 0) {
+                                          int32_t c0, int n_el, uint32_t (&key)[IT], int32_t* rl, int Q = 0,
+                                          uint32_t n_src = 0) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * IT);
   uint32_t tv[IT];
   int32_t rv[IT];
+  __amdgpu_buffer_rsrc_t ra, rb;
+  if constexpr (BUF) {
+    constexpr int kRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
+    ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(tin), 0, int(n_src * 2u), kRsrcWord3);
+    rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(rin), 0, int(n_src * 4u), kRsrcWord3);
+  }
   int qw = 0, qa = 0, qb = 0;  // SEARCH 2: the current portion and its bounds ps[qw], ps[qw + 1]
   if (SEARCH == 2) {
     const int e0 = ebase + lane < n_el ? ebase + lane : n_el - 1;
@@ -576,8 +589,13 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
       q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
     }
     const uint32_t src = uint32_t(psrc[q] + (c0 + ec - (SEARCH == 2 ? qa : ps[q])));
-    tv[j] = tin[src];
-    if (RULES) rv[j] = rin[src];
+    if constexpr (BUF) {
+      tv[j] = __builtin_amdgcn_raw_buffer_load_b16(ra, int(src * 2u), 0, 0);
+      if (RULES) rv[j] = __builtin_amdgcn_raw_buffer_load_b32(rb, int(src * 4u), 0, 0);
+    } else {
+      tv[j] = tin[src];
+      if (RULES) rv[j] = rin[src];
+    }
   }
 #pragma unroll
   for (int j = 0; j < IT; j++) {
@@ -635,6 +653,9 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 #ifndef CG_OT_OWN_SEARCH
 #define CG_OT_OWN_SEARCH 2  // the merge's portion per element: 0 owner map, 1 binary search, 2 search + walk
 #endif
+#ifndef CG_OT_RUN_SLABS
+#define CG_OT_RUN_SLABS 0  // > 0: a merge run holds at most this many slabs (4: always one 8-bit pass)
+#endif
 #ifndef CG_OT_MID_WPE
 #define CG_OT_MID_WPE 4  // min waves per SIMD of k_ot_mid (8-wave blocks: 2 per SIMD each)
 #endif
@@ -660,11 +681,12 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   int32_t* own = reinterpret_cast<int32_t*>(pk);
   uint32_t key[IT];
   ot_portions<NW>(M, portion, ps, psrc, wsum);
+  const uint32_t n_src = uint32_t(M) * kOtTile;  // the node's tiles (M <= kOtMaxTiles)
 #if CG_OT_OWN_SEARCH
-  ot_gather<true, CG_OT_OWN_SEARCH, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M);
+  ot_gather<true, CG_OT_OWN_SEARCH, PACK, IT, CG_OT_BUF>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M, n_src);
 #else
   ot_owners<NW, IT>(ps, M, 0, n_el, own, wsum);
-  ot_gather<true, 0, PACK, IT>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl);
+  ot_gather<true, 0, PACK, IT, CG_OT_BUF>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, 0, n_src);
 #endif
   constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
   ot_sort<NW, 256, false, IB, IT>(key, n_el, lo, 0, passes, pk, s);
@@ -684,11 +706,18 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   ot_sync<NW>();
 }
 
-// Per node: its slabs in runs that fit one chunk, each merged by
-// ot_merge_chunk.  A slab of more than a chunk is queued: to k_ot_mid when it
+// Per node with e_lo <= events < e_hi: its slabs in runs that fit one chunk,
+// each merged by ot_merge_chunk.  Two launches split the nodes by density:
+// 4-wave blocks (4096-event chunks) for nodes averaging at most
+// CG_OT_DENSE_PER_SLAB events per slab, 8-wave blocks (8192; a persistent
+// grid taking nodes by ticket, on its own stream beside the 4-wave launch)
+// for denser ones (same-box A/Bs, profiles/r04_ab_merge_shape.txt: 8-wave
+// chunks for every node are 6-9 % faster on config 3's ~4.6 k events per
+// slab and 11-13 % slower on pernode's ~1.6 k; the split at 4096 takes
+// config 3 from ~600 to 555 ms per step and leaves pernode unchanged).  A slab of more than a chunk is queued: to k_ot_mid when it
 // fits k_ot_mid's chunk (mid / mid_n), else to k_ot_big (big / big_n);
 // entries (node << 8 | slab).
-template <int NW, bool PACK, int IT = kOtItems>
+template <int NW, bool PACK, int IT = kOtItems, bool DYN = false>  // DYN: nodes by ticket (persistent grid)
 __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
@@ -697,6 +726,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
                                                        int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                        int64_t* __restrict__ big, unsigned* __restrict__ big_n,
                                                        int64_t* __restrict__ mid, unsigned* __restrict__ mid_n,
+                                                       int64_t e_lo, int64_t e_hi, unsigned* __restrict__ ticket,
                                                        int64_t* __restrict__ err) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
   constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems;
@@ -707,21 +737,29 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
   __shared__ int32_t psrc[kOtMaxTiles];       // node-relative (M <= kOtMaxTiles: < 2^20)
   __shared__ int64_t slab_off[kOtSlabs + 1];  // node-relative first position of each slab
   __shared__ int32_t wsum[NW];
-  const int32_t n = blockIdx.x;
-  if (n >= N) return;
+  __shared__ int32_t tk;
+  auto next = [&]() -> int32_t {  // DYN: the next node by ticket, once every thread is done with the last
+    if (!DYN) return N;
+    ot_sync<NW>();
+    if (threadIdx.x == 0) tk = int32_t(atomicAdd(ticket, 1u));
+    ot_sync<NW>();
+    return tk;
+  };
+  for (int32_t n = DYN ? next() : int32_t(blockIdx.x); n < N; n = next()) {
   const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta, lo_n = node_off[n];
-  if (M == 0) return;
+  if (M == 0) continue;
+  const int64_t e_n = node_off[n + 1] - lo_n;
+  if (e_n < e_lo || e_n >= e_hi) continue;  // the other merge launch's node
   if (M == 1) {  // one tile: already in order
-    const int64_t e = node_off[n + 1] - lo_n;
-    for (int64_t p = threadIdx.x; p < e; p += kThreads) {
+    for (int64_t p = threadIdx.x; p < e_n; p += kThreads) {
       __builtin_nontemporal_store(t0 + 1 + int64_t(tin[lo_n + p]), tout + lo_n + p);
       __builtin_nontemporal_store(rin[lo_n + p], rout + lo_n + p);
     }
-    return;
+    continue;
   }
   if (M > kOtMaxTiles) {  // every slab to k_ot_big
     for (int j = threadIdx.x; j < kOtSlabs; j += kThreads) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | j;
-    return;
+    continue;
   }
   for (int j = threadIdx.x; j <= kOtSlabs; j += kThreads) slab_off[j] = slab_tab[int64_t(n) * kOtPre + j];
   ot_sync<NW>();
@@ -729,7 +767,9 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
   // slab of more than a chunk)
   auto run_end = [&](int j0) {
     int j1 = j0;
-    while (j1 < kOtSlabs && slab_off[j1 + 1] - slab_off[j0] <= kChunk) j1++;
+    while (j1 < kOtSlabs && (CG_OT_RUN_SLABS == 0 || j1 - j0 < CG_OT_RUN_SLABS) &&
+           slab_off[j1 + 1] - slab_off[j0] <= kChunk)
+      j1++;
     return j1;
   };
   // thread q owns tile q (M <= kOtMaxTiles <= threads): its slab prefix at the
@@ -767,6 +807,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
     jb = jb2;
     pa = pa2;
     pb = pb2;
+  }
   }
 }
 
@@ -1128,8 +1169,9 @@ namespace {
 int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipStream_t st, int64_t* Tmax) {
   *Tmax = cap / kOtTile + N + 1;
   const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
-  // ts_off: [k_ot_big queue N*kOtSlabs][big, mid counters][slab_tab N*kOtPre][k_ot_mid queue N*kOtSlabs]
-  const int64_t tab = 2 * int64_t(N) * kOtSlabs + 1 + int64_t(N) * kOtPre;
+  // ts_off: [k_ot_big queue N*kOtSlabs][big, mid, dense-node counters: 2 words][slab_tab N*kOtPre]
+  // [k_ot_mid queue N*kOtSlabs]
+  const int64_t tab = 2 * int64_t(N) * kOtSlabs + 2 + int64_t(N) * kOtPre;
   // growing a buffer frees the old one: earlier windows' kernels finish first
   if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(*Tmax) ||
       c->ts_hist.cap < size_t(*Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
@@ -1148,30 +1190,52 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
   return CG_OK;
 }
 
-int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, hipStream_t st, int64_t* err, int64_t R) {
+#ifndef CG_OT_DENSE_PER_SLAB
+#define CG_OT_DENSE_PER_SLAB 4096  // average events per 64-s slab above which a node takes the 8-wave merge
+#endif
+int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st, int64_t* err,
+               int64_t R) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
-  unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);  // [0] big, [1] mid
-  HIPCHK(hipMemsetAsync(big_n, 0, 8, st));
-  int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 1;
+  // [0] big, [1] mid, [2] the dense merge's node ticket
+  unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
+  HIPCHK(hipMemsetAsync(big_n, 0, 16, st));
+  int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 2;
   int64_t* mid = slab_tab + int64_t(N) * kOtPre;
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
   const int cus = std::max(1, c->write_blocks / kWriteBlocksPerCU);
-  // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
-  if (CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits)) {
-    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, true, kOtMergeItems>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
-                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
-                       c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, err);
-    hipLaunchKernelGGL((k_ot_mid<kOtMidWaves, true>), dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, st, toff,
-                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p,
-                       c->node_rule.p, mid, big_n + 1, err);
-  } else {
-    hipLaunchKernelGGL((k_ot_merge<kOtMergeWaves, false, kOtMergeItems>), dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff,
-                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p,
-                       c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, err);
-    hipLaunchKernelGGL((k_ot_mid<kOtMidWaves, false>), dim3(unsigned(cus * 2)), dim3(64 * kOtMidWaves), 0, st, toff,
-                       c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p,
-                       c->node_rule.p, mid, big_n + 1, err);
+  // nodes split by density between a 4-wave and an 8-wave merge; the dense
+  // nodes' merge runs on its own stream beside the sparse one (few dense
+  // nodes after all the sparse ones would run as a tail at low occupancy)
+  const int64_t dense_min = int64_t(CG_OT_DENSE_PER_SLAB) * std::max<int64_t>(1, (H + 63) / 64);
+  if (!c->st_ot) {
+    HIPCHK(hipStreamCreateWithFlags(&c->st_ot, hipStreamNonBlocking));
+    HIPCHK(hipEventCreateWithFlags(&c->ot_fork, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ot_join, hipEventDisableTiming));
   }
+  HIPCHK(hipEventRecord(c->ot_fork, st));
+  HIPCHK(hipStreamWaitEvent(c->st_ot, c->ot_fork, 0));
+  // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
+  auto merges = [&](auto m4, auto m8, auto mid_k) {
+    // the dense merge: a persistent grid (2 blocks per CU) taking nodes by ticket
+    hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * 2))), dim3(64 * kOtMidWaves), 0,
+                       c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
+                       c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, dense_min, INT64_MAX,
+                       big_n + 2, err);
+    hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
+                       node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
+                       mid, big_n + 1, int64_t(0), dense_min, nullptr, err);
+    (void)hipEventRecord(c->ot_join, c->st_ot);
+    (void)hipStreamWaitEvent(st, c->ot_join, 0);
+    hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, st, toff, c->node_rule2.p,
+                       c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid,
+                       big_n + 1, err);
+  };
+  if (CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits))
+    merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems>, k_ot_merge<kOtMidWaves, true, kOtItems, true>,
+           k_ot_mid<kOtMidWaves, true>);
+  else
+    merges(k_ot_merge<kOtMergeWaves, false, kOtMergeItems>, k_ot_merge<kOtMidWaves, false, kOtItems, true>,
+           k_ot_mid<kOtMidWaves, false>);
   hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
                      c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
                      c->ts_off.p, big_n, err);
@@ -1183,8 +1247,8 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, hipStr
 // The tile sort + merge of the per-node lists already in c->node_time /
 // c->node_rule (node offsets node_off[N+1] on the device): used by
 // cg_node_result_order_by_time.
-int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, hipStream_t st,
-                        bool in16, int64_t* err) {
+int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
+                        hipStream_t st, bool in16, int64_t* err) {
   if (N == 0 || cap == 0) return CG_OK;
   int64_t Tmax = 0;
   int rc = order_setup(c, node_off, N, cap, st, &Tmax);
@@ -1197,7 +1261,7 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   };
   if (in16) pack ? tile(k_ot_tile<true, true>) : tile(k_ot_tile<true, false>);
   else pack ? tile(k_ot_tile<false, true>) : tile(k_ot_tile<false, false>);
-  return order_tail(c, node_off, N, t0, st, err, c->pn_R);
+  return order_tail(c, node_off, N, t0, H, st, err, c->pn_R);
 }
 
 // The per-node writer and tile sort in one (k_node_tile), then the merge: the
@@ -1214,7 +1278,7 @@ int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int6
   hipLaunchKernelGGL(k_node_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec, a.recs,
                      a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
                      reinterpret_cast<uint16_t*>(c->node_time2.p), c->node_rule2.p, c->ts_hist.p, n_tiles, err);
-  return order_tail(c, a.node_off, a.N, a.t0, st, err, c->pn_R);
+  return order_tail(c, a.node_off, a.N, a.t0, 4096, st, err, c->pn_R);  // windows <= 4096 s
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
@@ -1256,7 +1320,7 @@ int order_by_time_locked(cg_ctx* c, bool in16) {
     if ((rc = pn_ensure_res(c))) return rc;
     c->pn_res_host[2] = 0;
     (void)hipEventRecord(c->pev[0], st);
-    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, st, in16, c->pn_res_dev + 2))) return rc;
+    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, H, st, in16, c->pn_res_dev + 2))) return rc;
     (void)hipEventRecord(c->pev[1], st);
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
     if (c->pn_res_host[2]) return cg_fail(CG_EHIP, kOrderCheckMsg);

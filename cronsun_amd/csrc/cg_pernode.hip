@@ -1378,7 +1378,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
       hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
                          0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
                          K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
-      if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, st, true, a.res_dev + 2))) return rc;
+      if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, t1 - t0, st, true, a.res_dev + 2))) return rc;
     } else {
       hipLaunchKernelGGL((k_node_write<0, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
                          0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
