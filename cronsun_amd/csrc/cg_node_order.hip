@@ -212,7 +212,8 @@ constexpr int kOtRuleBits = 20;
 // chunk index bits of a packed word (offset << kOtIdxBits | index): up to
 // 8192 events (k_ot_mid's chunk: 8 waves x 64 x 16)
 constexpr int kOtIdxBits = 13;
-constexpr int kOtMidWaves = 8;  // k_ot_mid: waves per slab
+constexpr int kOtMidWaves = 8;    // k_ot_mid: waves per slab (slabs of <= 8192 events)
+constexpr int kOtMid2Waves = 16;  // its 16-wave form (slabs of <= 16384 events; one block per CU)
 static_assert(kOtMergeWaves <= 8 && 12 + kOtIdxBits <= 32, "packed words");
 constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
 constexpr int kOtSlabBits = 6;               // slab = offset >> kOtSlabBits (64 s): one 6-bit digit
@@ -284,7 +285,33 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[IT], int n, int32_t
     }
   }
   ot_sync<NW>();
-  if (threadIdx.x < 64) {  // lane d: digits d*P .. d*P + P - 1
+  if (NW * P > 16 && threadIdx.x < 64) {  // many waves: the counts re-read from LDS, not held in registers
+    const int d0 = threadIdx.x * P;
+    int32_t sum = 0;
+#pragma unroll
+    for (int i = 0; i < P; i++)
+#pragma unroll
+      for (int ww = 0; ww < NW; ww++) sum += s.run[ww][d0 + i];
+    int32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(inc, o, 64);
+      if (threadIdx.x >= o) inc += y;
+    }
+    int32_t acc = inc - sum;
+    if constexpr (D == 64) {
+      s.dbase[d0] = acc;
+      if (d0 == 63) s.dbase[64] = inc;
+    }
+#pragma unroll
+    for (int i = 0; i < P; i++)
+#pragma unroll
+      for (int ww = 0; ww < NW; ww++) {
+        const int32_t v = s.run[ww][d0 + i];
+        s.run[ww][d0 + i] = acc;
+        acc += v;
+      }
+  } else if (threadIdx.x < 64) {  // lane d: digits d*P .. d*P + P - 1
     const int d0 = threadIdx.x * P;
     int32_t r[P][NW], sum = 0;
 #pragma unroll
@@ -653,6 +680,15 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 #ifndef CG_OT_OWN_SEARCH
 #define CG_OT_OWN_SEARCH 2  // the merge's portion per element: 0 owner map, 1 binary search, 2 search + walk
 #endif
+#ifndef CG_OT_MID2
+#define CG_OT_MID2 1  // 0: slabs of 8193..16384 events to k_ot_big, not k_ot_mid's 16-wave form (A/B)
+#endif
+#ifndef CG_OT_MERGE_RUNS
+// 1: the merge / k_ot_big ranks add once per run of equal digits in
+// neighbouring lanes (ot_rank RUNS): events of a rule-major portion often
+// share a second with their neighbours (minutely rules all at :00)
+#define CG_OT_MERGE_RUNS 0
+#endif
 #ifndef CG_OT_RUN_SLABS
 #define CG_OT_RUN_SLABS 0  // > 0: a merge run holds at most this many slabs (4: always one 8-bit pass)
 #endif
@@ -689,7 +725,7 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   ot_gather<true, 0, PACK, IT, CG_OT_BUF>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, 0, n_src);
 #endif
   constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
-  ot_sort<NW, 256, false, IB, IT>(key, n_el, lo, 0, passes, pk, s);
+  ot_sort<NW, 256, bool(CG_OT_MERGE_RUNS), IB, IT>(key, n_el, lo, 0, passes, pk, s);
   bool bad = false;
   for (int p = threadIdx.x; p < n_el; p += 64 * NW) {
     const uint32_t v = pk[p];
@@ -726,10 +762,11 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
                                                        int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                        int64_t* __restrict__ big, unsigned* __restrict__ big_n,
                                                        int64_t* __restrict__ mid, unsigned* __restrict__ mid_n,
+                                                       int64_t* __restrict__ mid2, unsigned* __restrict__ mid2_n,
                                                        int64_t e_lo, int64_t e_hi, unsigned* __restrict__ ticket,
                                                        int64_t* __restrict__ err) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
-  constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems;
+  constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems, kMid2Chunk = 64 * kOtMid2Waves * kOtItems;
   __shared__ OtRank<NW, 256> s;
   __shared__ uint32_t pk[kChunk + kChunk / 32];  // the owner list while gathering (padded), then the sorted words
   __shared__ int32_t rl[PACK ? 1 : kChunk];
@@ -786,7 +823,9 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
     const int32_t pb2 = pq[jb2 <= kOtSlabs ? jb2 : kOtSlabs];  // in flight while this run is merged
     if (jb == ja) {  // one slab of more than a chunk
       if (threadIdx.x == 0) {
-        if (CG_OT_MID && slab_off[ja + 1] - slab_off[ja] <= kMidChunk) mid[atomicAdd(mid_n, 1u)] = (int64_t(n) << 8) | ja;
+        const int64_t sz = slab_off[ja + 1] - slab_off[ja];
+        if (CG_OT_MID && sz <= kMidChunk) mid[atomicAdd(mid_n, 1u)] = (int64_t(n) << 8) | ja;
+        else if (CG_OT_MID2 && sz <= kMid2Chunk) mid2[atomicAdd(mid2_n, 1u)] = (int64_t(n) << 8) | ja;
         else big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | ja;
       }
     } else if (slab_off[jb] > slab_off[ja]) {
@@ -935,7 +974,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
         ot_gather<true>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc, own, c0, n_el, key, rl);
-        ot_sort<4, 64>(key, n_el, uint32_t(j) << kOtSlabBits, 0, 1, pk, s);
+        ot_sort<4, 64, bool(CG_OT_MERGE_RUNS)>(key, n_el, uint32_t(j) << kOtSlabBits, 0, 1, pk, s);
         bool bad = false;
         for (int p = threadIdx.x; p < n_el; p += 256) {
           const uint32_t v = pk[p];
@@ -1169,9 +1208,9 @@ namespace {
 int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipStream_t st, int64_t* Tmax) {
   *Tmax = cap / kOtTile + N + 1;
   const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
-  // ts_off: [k_ot_big queue N*kOtSlabs][big, mid, dense-node counters: 2 words][slab_tab N*kOtPre]
-  // [k_ot_mid queue N*kOtSlabs]
-  const int64_t tab = 2 * int64_t(N) * kOtSlabs + 2 + int64_t(N) * kOtPre;
+  // ts_off: [k_ot_big queue N*kOtSlabs][big, mid, dense-node, mid2 counters: 2 words][slab_tab N*kOtPre]
+  // [k_ot_mid queue N*kOtSlabs][its 16-wave form's queue N*kOtSlabs]
+  const int64_t tab = 3 * int64_t(N) * kOtSlabs + 2 + int64_t(N) * kOtPre;
   // growing a buffer frees the old one: earlier windows' kernels finish first
   if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(*Tmax) ||
       c->ts_hist.cap < size_t(*Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
@@ -1196,11 +1235,12 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
 int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st, int64_t* err,
                int64_t R) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
-  // [0] big, [1] mid, [2] the dense merge's node ticket
+  // [0] big, [1] mid, [2] the dense merge's node ticket, [3] mid2
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
   HIPCHK(hipMemsetAsync(big_n, 0, 16, st));
   int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 2;
   int64_t* mid = slab_tab + int64_t(N) * kOtPre;
+  int64_t* mid2 = mid + int64_t(N) * kOtSlabs;
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
   const int cus = std::max(1, c->write_blocks / kWriteBlocksPerCU);
   // nodes split by density between a 4-wave and an 8-wave merge; the dense
@@ -1215,27 +1255,30 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   HIPCHK(hipEventRecord(c->ot_fork, st));
   HIPCHK(hipStreamWaitEvent(c->st_ot, c->ot_fork, 0));
   // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
-  auto merges = [&](auto m4, auto m8, auto mid_k) {
+  auto merges = [&](auto m4, auto m8, auto mid_k, auto mid2_k) {
     // the dense merge: a persistent grid (2 blocks per CU) taking nodes by ticket
     hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * 2))), dim3(64 * kOtMidWaves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
-                       c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, dense_min, INT64_MAX,
-                       big_n + 2, err);
+                       c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
+                       dense_min, INT64_MAX, big_n + 2, err);
     hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
-                       mid, big_n + 1, int64_t(0), dense_min, nullptr, err);
+                       mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err);
     (void)hipEventRecord(c->ot_join, c->st_ot);
     (void)hipStreamWaitEvent(st, c->ot_join, 0);
     hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, st, toff, c->node_rule2.p,
                        c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid,
                        big_n + 1, err);
+    hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
+                       c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
+                       big_n + 3, err);
   };
   if (CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits))
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems>, k_ot_merge<kOtMidWaves, true, kOtItems, true>,
-           k_ot_mid<kOtMidWaves, true>);
+           k_ot_mid<kOtMidWaves, true>, k_ot_mid<kOtMid2Waves, true>);
   else
     merges(k_ot_merge<kOtMergeWaves, false, kOtMergeItems>, k_ot_merge<kOtMidWaves, false, kOtItems, true>,
-           k_ot_mid<kOtMidWaves, false>);
+           k_ot_mid<kOtMidWaves, false>, k_ot_mid<kOtMid2Waves, false>);
   hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
                      c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
                      c->ts_off.p, big_n, err);

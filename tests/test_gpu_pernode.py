@@ -342,6 +342,47 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
         assert 4096 < node_off[1] < 2 * 4096 and node_off[1] < 64 * 4096 // 8
 
 
+@pytest.mark.parametrize("writer", ["pass", "direct"])
+@pytest.mark.parametrize("case", ["mid", "dense", "mid2"])
+def test_per_node_time_ordered_slab_classes(eng, writer, case):
+    """Each path of the merge by slab size, on one node over 1 h, against the
+    oracle's (time, rule) lists:
+    mid    a sparse node (<= 4096 events per 64-s slab on average, 4-wave
+           merge) with one heavy slab: 100 rules every second of minute 5
+           put 6 k events into slab 0 -> k_ot_mid (8-wave, 8192 events);
+    dense  100 every-second rules among 200: ~6.5 k events per slab on
+           average -> the 8-wave merge (persistent grid, own stream);
+    mid2   200 every-second rules among 400: ~13 k per slab -> k_ot_mid's
+           16-wave form (16384 events)."""
+    mix = PROGRESSION_MIX[1:]
+    if case == "mid":
+        specs = ["* 5 * * * *" if i % 2 == 0 else mix[i % len(mix)] for i in range(200)]
+    else:
+        R = 200 if case == "dense" else 400
+        specs = [PROGRESSION_MIX[0] if i % 2 == 0 else mix[i % len(mix)] for i in range(R)]
+    rin = progression_rules(len(specs), 1)
+    scheds = [cron.Parse(x) for x in specs]
+    t0 = synth.T0_2026 + 11 * DAY + 297  # minute 5 of the hour at offsets 2..61: all in slab 0
+    t1 = t0 + 3600
+    node_off, off2, time2, rule2 = _ordered_per_node(eng, writer, scheds, product_zone("UTC"), t0, t1, rin)
+    assert np.array_equal(off2, node_off)
+    arr = O.sched_array(oracle_parse_all(specs))
+    eo, et = O.expand_batch(arr, t0, t1, oracle_zone("UTC"))
+    exp_t, exp_r = O.node_list(eo, et, list(range(len(specs))))
+    order = np.lexsort((exp_r, exp_t))
+    assert node_off[1] == len(exp_t)
+    assert np.array_equal(time2, exp_t[order])
+    assert np.array_equal(rule2, exp_r[order])
+    per_slab = np.bincount((exp_t - t0 - 1) // 64)
+    avg = len(exp_t) / np.ceil(3600 / 64)
+    if case == "mid":
+        assert avg <= 4096 and 4096 < per_slab.max() <= 8192
+    elif case == "dense":
+        assert avg > 4096 and per_slab.max() <= 8192
+    else:
+        assert 8192 < per_slab.max() <= 16384
+
+
 @pytest.mark.parametrize("zone,t0", [("UTC", synth.T0_2026 + 64 * DAY + 1234),
                                      ("America/New_York", 1772953200 - 36 * 3600)])
 def test_per_node_progressions_vs_oracle(eng, zone, t0):
