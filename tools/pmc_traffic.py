@@ -29,9 +29,33 @@ def _rows(d, pattern):
     return out
 
 
+_MULTI = set()  # kernel base names with several template instances in the inputs
+
+
+def _parts(name):
+    m = re.search(r"\b(k_[A-Za-z0-9_]+)(<[^()]*>)?", name)
+    if not m:
+        return name.split("(")[0], ""
+    return m.group(1), (m.group(2) or "").replace(" ", "")
+
+
 def _short(name):
-    m = re.search(r"\b(k_[A-Za-z0-9_]+)", name)
-    return m.group(1) if m else name.split("(")[0]
+    """The kernel's base name; with its template arguments when the inputs
+    hold several instances of it (e.g. k_ot_merge<4,...> and <8,...>)."""
+    base, targs = _parts(name)
+    return base + targs if base in _MULTI else base
+
+
+def _scan_instances(dirs):
+    inst = defaultdict(set)
+    for d in dirs:
+        if not d:
+            continue
+        for pattern, col in (("*kernel_stats.csv", "Name"), ("*counter_collection.csv", "Kernel_Name")):
+            for r in _rows(d, pattern):
+                base, targs = _parts(r.get(col, ""))
+                inst[base].add(targs)
+    _MULTI.update(b for b, t in inst.items() if len(t) > 1)
 
 
 def counters(d, counter):
@@ -64,6 +88,7 @@ def main():
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     res = {"kernels": {}}
+    _scan_instances([a.kt, a.fetch, a.write, a.sq])
     if a.sq:
         names = sorted({r["Counter_Name"] for r in _rows(a.sq, "*counter_collection.csv")})
         for n in names:
