@@ -327,7 +327,13 @@ int pn_async_drain(cg_ctx* c);
 bool pn_async_pending(const cg_ctx* c);  // an asynchronous expansion not yet waited for
 // time-order tile sort + merge of c->node_time / c->node_rule (windows <= 4096 s;
 // cg_node_order.hip), enqueued on st without a host sync
-// (in16: the lists' times are 16-bit offsets t - t0 - 1, written by k_node_write<.., true>)
+// in_mode: what the writer left in c->node_time / c->node_rule -- kInTimes
+// int64 times + rules; kIn16 16-bit offsets t - t0 - 1 + rules
+// (k_node_write<.., kOut16>); kInPacked one word per event, offset << 20 |
+// rule, in c->node_rule (k_node_write<.., kOutPacked>; rules < 2^20)
+constexpr int kInTimes = 0, kIn16 = 1, kInPacked = 2;
+// the time-order writer may emit kInPacked for R rules (indices < 2^20)
+bool pn_pack_ok(int64_t R);
 // The per-node lists of a window <= 4096 s in (time, rule) order straight
 // from the segment records (cg_node_order.hip: k_node_tile writes the tiles,
 // then the merge), enqueued on st without a host sync
@@ -347,13 +353,13 @@ int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int6
 // err: a device word the kernels set when a sorted chunk is out of (time,
 // rule) order (the sorts' ranks rest on lane-ordered LDS atomics; checked)
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
-                        hipStream_t st, bool in16, int64_t* err);
+                        hipStream_t st, int in_mode, int64_t* err);
 constexpr const char* kOrderCheckMsg =
     "time-order pass: a sorted chunk came out of (time, rule) order (its LDS-atomic ranks were not in lane order)";
 // the mapped pinned per-node result words: [0] node events, [1] size error, [2] order check
 int pn_ensure_res(cg_ctx* c);
 // the time-order pass over the last (rule-major) per-node result; c->mu held
-int order_by_time_locked(cg_ctx* c, bool in16 = false);
+int order_by_time_locked(cg_ctx* c, int in_mode = 0);
 // kernels of the per-node CSR gather (cg_pernode.hip), enqueued on st:
 // node n's events [src_off[n], src_off[n+1]) of src to dst_start[n] onwards /
 // n contiguous events / the last per-node result's counts per node

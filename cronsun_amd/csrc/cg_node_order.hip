@@ -395,7 +395,10 @@ __device__ __forceinline__ bool ot_out_of_order(uint32_t u, uint32_t v, const in
 // rule, so no rule array in LDS (17 KB per block instead of 34: more blocks
 // per CU); the sorts are stable, so the rule-major order inside a slab (and
 // the rule order of equal offsets) carries through without the index.
-template <bool IN16, bool PACK>  // IN16: times as 16-bit offsets t - t0 - 1 (else int64 times, their low words read)
+// IN: 0 int64 times (their low words read) + rules, 1 16-bit offsets
+// t - t0 - 1 + rules, 2 packed words offset << 20 | rule (in `rule`).
+// PACK: the output is the packed words too (in rule_out; toff_out unused).
+template <int IN, bool PACK>
 __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(const int64_t* __restrict__ time, const int32_t* __restrict__ rule,
                                                   const int32_t* __restrict__ tile_node,
                                                   const int64_t* __restrict__ tile_base,
@@ -422,9 +425,16 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
   for (int j = 0; j < kOtItems; j++) {  // every load issued before any is used
     const int e = ebase + j * 64 + lane;
     const int64_t i = r.lo + (e < n ? e : n - 1);
-    if constexpr (IN16) tv[j] = uint32_t(reinterpret_cast<const uint16_t*>(time)[i]) + b;
-    else tv[j] = tlo[2 * i];
+    if constexpr (IN == 1) tv[j] = uint32_t(reinterpret_cast<const uint16_t*>(time)[i]) + b;
+    else if constexpr (IN == 0) tv[j] = tlo[2 * i];
     rv[j] = rule[i];
+  }
+  if constexpr (IN == 2) {
+#pragma unroll
+    for (int j = 0; j < kOtItems; j++) {
+      tv[j] = (uint32_t(rv[j]) >> kOtRuleBits) + b;
+      rv[j] = int32_t(uint32_t(rv[j]) & ((1u << kOtRuleBits) - 1u));
+    }
   }
 #pragma unroll
   for (int j = 0; j < kOtItems; j++) {
@@ -447,8 +457,12 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
   bool bad = false;
   for (int p = threadIdx.x; p < n; p += 256) {
     const uint32_t v = pk[p];
-    toff_out[r.lo + p] = uint16_t(v >> IB);
-    __builtin_nontemporal_store(rule_of(v), rule_out + r.lo + p);
+    if constexpr (PACK) {
+      __builtin_nontemporal_store(int32_t(v), rule_out + r.lo + p);  // the word itself: offset << 20 | rule
+    } else {
+      toff_out[r.lo + p] = uint16_t(v >> IB);
+      __builtin_nontemporal_store(rule_of(v), rule_out + r.lo + p);
+    }
     // the ranks rest on lane-ordered LDS atomics (ot_rank): check the order
     // they produced -- a node's only tile is final: (offset, rule) ascending;
     // a partitioned tile keeps rule order inside each slab
@@ -578,7 +592,9 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 #ifndef CG_OT_BUF
 #define CG_OT_BUF 1
 #endif
-template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems, bool BUF = false>
+// PIN: the source is one array of packed words offset << 20 | rule (rin; tin
+// unused), 4 B per event instead of 2 + 4
+template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems, bool BUF = false, bool PIN = false>
 __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                           const int32_t* ps, const int32_t* psrc, const int32_t* own,
                                           int32_t c0, int n_el, uint32_t (&key)[IT], int32_t* rl, int Q = 0,
@@ -616,12 +632,21 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
       q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
     }
     const uint32_t src = uint32_t(psrc[q] + (c0 + ec - (SEARCH == 2 ? qa : ps[q])));
-    if constexpr (BUF) {
+    if constexpr (PIN) {  // one word: split below
+      rv[j] = BUF ? __builtin_amdgcn_raw_buffer_load_b32(rb, int(src * 4u), 0, 0) : rin[src];
+    } else if constexpr (BUF) {
       tv[j] = __builtin_amdgcn_raw_buffer_load_b16(ra, int(src * 2u), 0, 0);
       if (RULES) rv[j] = __builtin_amdgcn_raw_buffer_load_b32(rb, int(src * 4u), 0, 0);
     } else {
       tv[j] = tin[src];
       if (RULES) rv[j] = rin[src];
+    }
+  }
+  if constexpr (PIN) {
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+      tv[j] = uint32_t(rv[j]) >> kOtRuleBits;
+      rv[j] = int32_t(uint32_t(rv[j]) & ((1u << kOtRuleBits) - 1u));
     }
   }
 #pragma unroll
@@ -707,7 +732,7 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 // (portion(q, &src) -> count, thread q's tile; src node-relative), gathered,
 // sorted in LDS by rel = offset - lo (`passes` 8-bit passes) and stored at
 // tout_o / rout_o in (time, rule) order.  Ends synchronised.
-template <int NW, bool PACK, int IT, class Portion>
+template <int NW, bool PACK, int IT, bool PIN, class Portion>
 __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_n, const int32_t* __restrict__ rin_n,
                                                int M, int n_el, uint32_t lo, int passes, Portion&& portion,
                                                int64_t t0, int64_t* __restrict__ tout_o,
@@ -719,10 +744,10 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   ot_portions<NW>(M, portion, ps, psrc, wsum);
   const uint32_t n_src = uint32_t(M) * kOtTile;  // the node's tiles (M <= kOtMaxTiles)
 #if CG_OT_OWN_SEARCH
-  ot_gather<true, CG_OT_OWN_SEARCH, PACK, IT, CG_OT_BUF>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M, n_src);
+  ot_gather<true, CG_OT_OWN_SEARCH, PACK, IT, CG_OT_BUF, PIN>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M, n_src);
 #else
   ot_owners<NW, IT>(ps, M, 0, n_el, own, wsum);
-  ot_gather<true, 0, PACK, IT, CG_OT_BUF>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, 0, n_src);
+  ot_gather<true, 0, PACK, IT, CG_OT_BUF, PIN>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, 0, n_src);
 #endif
   constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
   ot_sort<NW, 256, bool(CG_OT_MERGE_RUNS), IB, IT>(key, n_el, lo, 0, passes, pk, s);
@@ -753,7 +778,7 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
 // config 3 from ~600 to 555 ms per step and leaves pernode unchanged).  A slab of more than a chunk is queued: to k_ot_mid when it
 // fits k_ot_mid's chunk (mid / mid_n), else to k_ot_big (big / big_n);
 // entries (node << 8 | slab).
-template <int NW, bool PACK, int IT = kOtItems, bool DYN = false>  // DYN: nodes by ticket (persistent grid)
+template <int NW, bool PACK, int IT = kOtItems, bool DYN = false, bool PIN = false>  // DYN: nodes by ticket (persistent grid)
 __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
@@ -789,8 +814,10 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
   if (e_n < e_lo || e_n >= e_hi) continue;  // the other merge launch's node
   if (M == 1) {  // one tile: already in order
     for (int64_t p = threadIdx.x; p < e_n; p += kThreads) {
-      __builtin_nontemporal_store(t0 + 1 + int64_t(tin[lo_n + p]), tout + lo_n + p);
-      __builtin_nontemporal_store(rin[lo_n + p], rout + lo_n + p);
+      const uint32_t w = uint32_t(rin[lo_n + p]);  // PIN: a packed word
+      const int64_t off = PIN ? int64_t(w >> kOtRuleBits) : int64_t(tin[lo_n + p]);
+      __builtin_nontemporal_store(t0 + 1 + off, tout + lo_n + p);
+      __builtin_nontemporal_store(PIN ? int32_t(w & ((1u << kOtRuleBits) - 1u)) : int32_t(w), rout + lo_n + p);
     }
     continue;
   }
@@ -833,7 +860,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
       // rel = offset - the run's first second (< 64 * (jb - ja)): one 8-bit
       // pass for up to 4 slabs
       const int64_t o = lo_n + slab_off[ja];
-      ot_merge_chunk<NW, PACK, IT>(
+      ot_merge_chunk<NW, PACK, IT, PIN>(
           tin + lo_n, rin + lo_n, int(M), int(slab_off[jb] - slab_off[ja]), uint32_t(ja) << kOtSlabBits,
           jb - ja > 4 ? 2 : 1,
           [&](int q, int32_t* src) {
@@ -853,7 +880,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
 // The slabs k_ot_merge queued for a bigger chunk (more than its own, at most
 // 64 * kOtMidWaves * kOtItems events), one per workgroup turn: the same
 // gather + one-pass LDS sort with NW waves (a slab of 64 s: one 8-bit pass).
-template <int NW, bool PACK, int IT = kOtItems>
+template <int NW, bool PACK, int IT = kOtItems, bool PIN = false>
 __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                     const int64_t* __restrict__ tile_base,
                                                     const int64_t* __restrict__ node_off,
@@ -882,7 +909,7 @@ __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_
       if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
       continue;
     }
-    ot_merge_chunk<NW, PACK, IT>(
+    ot_merge_chunk<NW, PACK, IT, PIN>(
         tin + lo_n, rin + lo_n, int(M), int(n_el), uint32_t(j) << kOtSlabBits, 1,
         [&](int q, int32_t* src) {
           const int32_t* pt = pre + (ta + q) * kOtPre;
@@ -896,6 +923,7 @@ __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_
 // The slabs k_ot_merge queued, one per workgroup turn: the slab's
 // histogram of its 16 seconds over all its portions first, then its chunks
 // in order, each sorted in LDS and stored at its seconds' running bases.
+template <bool PIN>
 __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                  const int64_t* __restrict__ tile_base,
                                                  const int64_t* __restrict__ node_off,
@@ -948,7 +976,8 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
       for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
-        ot_gather<false>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc, own, c0, n_el, key, rl);
+        ot_gather<false, 0, false, kOtItems, false, PIN>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc,
+                                                         own, c0, n_el, key, rl);
 #pragma unroll
         for (int jj = 0; jj < kOtItems; jj++)
           if (ebase + jj * 64 + lane < n_el) atomicAdd(&hist[(key[jj] >> kOtIdxBits) & kSec], 1);
@@ -973,7 +1002,8 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
       for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
-        ot_gather<true>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc, own, c0, n_el, key, rl);
+        ot_gather<true, 0, false, kOtItems, false, PIN>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc,
+                                                        own, c0, n_el, key, rl);
         ot_sort<4, 64, bool(CG_OT_MERGE_RUNS)>(key, n_el, uint32_t(j) << kOtSlabBits, 0, 1, pk, s);
         bool bad = false;
         for (int p = threadIdx.x; p < n_el; p += 256) {
@@ -1232,8 +1262,9 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
 #ifndef CG_OT_DENSE_PER_SLAB
 #define CG_OT_DENSE_PER_SLAB 4096  // average events per 64-s slab above which a node takes the 8-wave merge
 #endif
+// pin: the tiles were stored as packed words offset << 20 | rule (in node_rule2)
 int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st, int64_t* err,
-               int64_t R) {
+               int64_t R, bool pin) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
   // [0] big, [1] mid, [2] the dense merge's node ticket, [3] mid2
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
@@ -1273,15 +1304,23 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
                        c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
                        big_n + 3, err);
   };
-  if (CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits))
+  const bool pack = CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
+  if (pack && pin)
+    merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,
+           k_ot_merge<kOtMidWaves, true, kOtItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,
+           k_ot_mid<kOtMid2Waves, true, kOtItems, true>);
+  else if (pack)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems>, k_ot_merge<kOtMidWaves, true, kOtItems, true>,
            k_ot_mid<kOtMidWaves, true>, k_ot_mid<kOtMid2Waves, true>);
   else
     merges(k_ot_merge<kOtMergeWaves, false, kOtMergeItems>, k_ot_merge<kOtMidWaves, false, kOtItems, true>,
            k_ot_mid<kOtMidWaves, false>, k_ot_mid<kOtMid2Waves, false>);
-  hipLaunchKernelGGL(k_ot_big, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff,
-                     c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p,
-                     c->ts_off.p, big_n, err);
+  auto big = [&](auto k) {
+    hipLaunchKernelGGL(k, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff, c->node_rule2.p,
+                       c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
+                       err);
+  };
+  pin ? big(k_ot_big<true>) : big(k_ot_big<false>);
   return cg_hip_check(hipGetLastError(), "time-order kernels");
 }
 
@@ -1291,20 +1330,27 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
 // c->node_rule (node offsets node_off[N+1] on the device): used by
 // cg_node_result_order_by_time.
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
-                        hipStream_t st, bool in16, int64_t* err) {
+                        hipStream_t st, int in_mode, int64_t* err) {
   if (N == 0 || cap == 0) return CG_OK;
   int64_t Tmax = 0;
   int rc = order_setup(c, node_off, N, cap, st, &Tmax);
   if (rc) return rc;
   uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
-  const bool pack = CG_OT_TILE_PACK && c->pn_R <= (int64_t(1) << kOtRuleBits);
+  // the tiles stored as packed words when every rule index is below 2^20
+  const bool pack = CG_OT_TILE_PACK && CG_OT_PACK && c->pn_R <= (int64_t(1) << kOtRuleBits);
   auto tile = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p, c->ts_tile_node.p,
                        c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p, c->ts_base.p + N, err);
   };
-  if (in16) pack ? tile(k_ot_tile<true, true>) : tile(k_ot_tile<true, false>);
-  else pack ? tile(k_ot_tile<false, true>) : tile(k_ot_tile<false, false>);
-  return order_tail(c, node_off, N, t0, H, st, err, c->pn_R);
+  if (in_mode == kInPacked) {
+    if (!pack) return cg_fail(CG_EINVAL, "time order: packed lists need rule indices below 2^20");
+    tile(k_ot_tile<2, true>);
+  } else if (in_mode == kIn16) {
+    pack ? tile(k_ot_tile<1, true>) : tile(k_ot_tile<1, false>);
+  } else {
+    pack ? tile(k_ot_tile<0, true>) : tile(k_ot_tile<0, false>);
+  }
+  return order_tail(c, node_off, N, t0, H, st, err, c->pn_R, pack);
 }
 
 // The per-node writer and tile sort in one (k_node_tile), then the merge: the
@@ -1321,7 +1367,7 @@ int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int6
   hipLaunchKernelGGL(k_node_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec, a.recs,
                      a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
                      reinterpret_cast<uint16_t*>(c->node_time2.p), c->node_rule2.p, c->ts_hist.p, n_tiles, err);
-  return order_tail(c, a.node_off, a.N, a.t0, 4096, st, err, c->pn_R);  // windows <= 4096 s
+  return order_tail(c, a.node_off, a.N, a.t0, 4096, st, err, c->pn_R, false);  // windows <= 4096 s; 16-bit tiles
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
@@ -1339,12 +1385,19 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   return order_by_time_locked(c);
 }
 
+#ifndef CG_OT_PIN
+#define CG_OT_PIN 1  // 0: the time-order writer emits 16-bit offsets + rules, not packed words (A/B)
+#endif
+bool pn_pack_ok(int64_t R) {
+  return CG_OT_PIN && CG_OT_TILE_PACK && CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
+}
+
 bool order_lsd_only() {
   static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;
   return lsd_only;
 }
 
-int order_by_time_locked(cg_ctx* c, bool in16) {
+int order_by_time_locked(cg_ctx* c, int in_mode) {
   int rc = CG_OK;
   const int64_t En = c->pn_E;
   const int32_t N = int32_t(c->pn_N);
@@ -1363,7 +1416,7 @@ int order_by_time_locked(cg_ctx* c, bool in16) {
     if ((rc = pn_ensure_res(c))) return rc;
     c->pn_res_host[2] = 0;
     (void)hipEventRecord(c->pev[0], st);
-    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, H, st, in16, c->pn_res_dev + 2))) return rc;
+    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, H, st, in_mode, c->pn_res_dev + 2))) return rc;
     (void)hipEventRecord(c->pev[1], st);
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
     if (c->pn_res_host[2]) return cg_fail(CG_EHIP, kOrderCheckMsg);

@@ -544,9 +544,12 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 }
 constexpr int kNodeMajorDefault = 0;  // writer task order: 0 band-major, 1 node-major
 
-// OFF16: the times go out as 16-bit offsets t - t0 - 1 (windows <= 4096 s
-// whose lists the time-order tile sort reads next: 2 B per event instead of 8)
-template <int V, bool OFF16 = false>
+// OUT (windows <= 4096 s whose lists the time-order tile sort reads next):
+// kInTimes int64 times + int32 rules; kIn16 the times as 16-bit offsets
+// t - t0 - 1 (2 B per event instead of 8); kInPacked one word per event,
+// offset << 20 | rule, into out_rule (4 B per event instead of 2 + 4; rule
+// indices < 2^20)
+template <int V, int OUT = kInTimes>
 __global__ __launch_bounds__(256) void k_node_write(
     const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
     const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, int64_t t0,
@@ -602,9 +605,14 @@ __global__ __launch_bounds__(256) void k_node_write(
     int64_t* __restrict__ ot = out_time + abase;
     uint16_t* __restrict__ o16 = reinterpret_cast<uint16_t*>(out_time) + abase;
     int32_t* __restrict__ orl = out_rule + abase;
-    auto put_time = [&](int32_t q, int64_t val) {
-      if constexpr (OFF16) out_store<V>(o16 + q, uint16_t(val - t0 - 1));
+    auto put = [&](int32_t q, int64_t val, int32_t rv) {
+      if constexpr (OUT == kInPacked) {
+        out_store<V>(orl + q, int32_t((uint32_t(val - t0 - 1) << 20) | uint32_t(rv)));
+        return;
+      }
+      if constexpr (OUT == kIn16) out_store<V>(o16 + q, uint16_t(val - t0 - 1));
       else out_store<V>(ot + q, val);
+      if (!(V & 8)) out_store<V>(orl + q, rv);
     };
     int32_t pq = -1, prule = 0;  // a block carried into the next chunk
     int64_t ptime = 0;
@@ -654,8 +662,7 @@ __global__ __launch_bounds__(256) void k_node_write(
         }
         if (b + 64 <= we || we == q_hi) {  // complete, or the segment's last block
           if ((b >= q_lo && b + 64 <= q_hi) || (q >= q_lo && q < q_hi)) {  // whole, or a segment edge
-            put_time(q, val);
-            if (!(V & 8)) out_store<V>(orl + q, rv);
+            put(q, val, rv);
           }
           pq = -1;
         } else {  // carried into the next chunk
@@ -681,16 +688,14 @@ __global__ __launch_bounds__(256) void k_node_write(
           int64_t val = t0 + int64_t(dl) + int64_t(b + lane - q_lo) * sv;
           const int64_t step = int64_t(64) * sv;
           for (; b < bend; b += 64, val += step) {
-            put_time(b + lane, val);
-            if (!(V & 8)) out_store<V>(orl + b + lane, rv);
+            put(b + lane, val, rv);
           }
         } else {
           for (; b < bend; b += 64) {
             const int32_t gi = b + lane + dl - q_lo;
             int64_t val = (V & 1) ? int64_t(gi) : tb[gi];
             asm volatile("" : "+v"(val));
-            put_time(b + lane, val);
-            if (!(V & 8)) out_store<V>(orl + b + lane, rv);
+            put(b + lane, val, rv);
           }
         }
       }
@@ -1108,6 +1113,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   // writer fused with the tile sort, k_node_tile, then the merge
   const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
   const bool fused = off16 && CG_NODE_TILE_FUSED;
+  // packed words (offset << 20 | rule) when every rule index fits 20 bits
+  const int in_mode = !off16 ? kInTimes : (pn_pack_ok(R) ? kInPacked : kIn16);
   c->pn_res_host[2] = 0;
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
@@ -1117,12 +1124,17 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
                               int64_t(c->times.cap), c->node_off.p, N, K, B, cap, t0};
       if (NK > 0 && cap > 0 && (rc = order_fused_enqueue(c, fa, st, c->pn_res_dev + 2))) return rc;
     } else if (NK > 0 && cap > 0 && off16) {
-      hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
-                         0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p, c->times.p,
-                         N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
+      if (in_mode == kInPacked)
+        hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
+                           dim3(256), 0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,
+                           c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
+      else
+        hipLaunchKernelGGL((k_node_write<0, kIn16>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
+                           dim3(256), 0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,
+                           c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
     } else if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
-  hipLaunchKernelGGL((k_node_write<V, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
+  hipLaunchKernelGGL((k_node_write<V, kInTimes>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
                      0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,      \
                      c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p,     \
                      c->node_rule.p, node_major)
@@ -1174,7 +1186,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   // passes) after the writer; if it fails nothing is readable (the lists may
   // hold the writer's 16-bit offsets)
   if (c->node_order == CG_NODE_ORDER_TIME) {
-    if ((rc = order_by_time_locked(c, off16))) {
+    if ((rc = order_by_time_locked(c, in_mode))) {
       c->pn_E = 0;
       *n_events = 0;
     }
@@ -1374,13 +1386,22 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
       const FusedOrderArgs fa{a.seg_pos.p, c->seg_pair.p, a.seg_nrec.p, a.recs.p, a.rm.offsets.p, a.times.p,
                               rm_cap, a.node_off.p, N, K, B, node_cap, t0};
       if ((rc = order_fused_enqueue(c, fa, st, a.res_dev + 2))) return rc;
-    } else if (timed) {  // 16-bit offsets, then the tile sort + merge on the same stream
-      hipLaunchKernelGGL((k_node_write<0, true>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
-                         0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
-                         K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
-      if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, t1 - t0, st, true, a.res_dev + 2))) return rc;
+    } else if (timed) {  // packed words (or 16-bit offsets), then the tile sort + merge on the same stream
+      const int in_mode = pn_pack_ok(R) ? kInPacked : kIn16;
+      if (in_mode == kInPacked)
+        hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
+                           dim3(256), 0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p,
+                           a.times.p, N, K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p,
+                           kNodeMajorDefault);
+      else
+        hipLaunchKernelGGL((k_node_write<0, kIn16>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
+                           dim3(256), 0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p,
+                           a.times.p, N, K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p,
+                           kNodeMajorDefault);
+      if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, t1 - t0, st, in_mode, a.res_dev + 2)))
+        return rc;
     } else {
-      hipLaunchKernelGGL((k_node_write<0, false>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
+      hipLaunchKernelGGL((k_node_write<0, kInTimes>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
                          0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
                          K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
     }
