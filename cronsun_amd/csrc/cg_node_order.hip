@@ -1295,11 +1295,13 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
     hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
                        mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err);
-    (void)hipEventRecord(c->ot_join, c->st_ot);
-    (void)hipStreamWaitEvent(st, c->ot_join, 0);
+    // k_ot_mid's queue is filled by the 4-wave merge only (the 8-wave merge's
+    // chunk holds any slab of <= 8192 events): it runs beside the dense merge
     hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, st, toff, c->node_rule2.p,
                        c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid,
                        big_n + 1, err);
+    (void)hipEventRecord(c->ot_join, c->st_ot);
+    (void)hipStreamWaitEvent(st, c->ot_join, 0);
     hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
                        c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
                        big_n + 3, err);
