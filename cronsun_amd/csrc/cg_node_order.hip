@@ -377,6 +377,15 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[IT], int n, uint32_t lo,
   ot_sync<NW>();
 }
 
+// pk[p - 1] for the element p this lane holds, where a wave's lanes hold
+// consecutive elements: the left lane's v by DPP (wave_shr:1, no LDS access),
+// lane 0 reads LDS (p > 0)
+__device__ __forceinline__ uint32_t ot_prev(const uint32_t* pk, int p, uint32_t v) {
+  uint32_t u = uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x138, 0xf, 0xf, false));  // wave_shr:1
+  if ((threadIdx.x & 63) == 0 && p > 0) u = pk[p - 1];
+  return u;
+}
+
 // two neighbours u, v of a sorted chunk (packed offset << 12 | index, rules in
 // rl by index) out of (time, rule) order: a rule fires once per second, so
 // equal offsets need strictly ascending rules
@@ -466,8 +475,8 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
     // the ranks rest on lane-ordered LDS atomics (ot_rank): check the order
     // they produced -- a node's only tile is final: (offset, rule) ascending;
     // a partitioned tile keeps rule order inside each slab
+    const uint32_t u = ot_prev(pk, p, v);
     if (p > 0) {
-      const uint32_t u = pk[p - 1];
       const int32_t ru = rule_of(u), rv2 = rule_of(v);
       const uint32_t ou = u >> IB, ov = v >> IB;
       if (one) bad |= ou > ov || (ou == ov && ru >= rv2);
@@ -609,12 +618,13 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
     ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint16_t*>(tin), 0, int(n_src * 2u), kRsrcWord3);
     rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(rin), 0, int(n_src * 4u), kRsrcWord3);
   }
-  int qw = 0, qa = 0, qb = 0;  // SEARCH 2: the current portion and its bounds ps[qw], ps[qw + 1]
+  int qw = 0, qa = 0, qb = 0, qs = 0;  // SEARCH 2: the current portion, its bounds ps[qw], ps[qw + 1], psrc[qw]
   if (SEARCH == 2) {
     const int e0 = ebase + lane < n_el ? ebase + lane : n_el - 1;
     qw = ot_find(ps, Q, c0 + e0);
     qa = ps[qw];
     qb = ps[qw + 1];
+    qs = psrc[qw];
   }
 #pragma unroll
   for (int j = 0; j < IT; j++) {
@@ -626,12 +636,13 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
         qw++;
         qa = qb;
         qb = ps[qw + 1];
+        qs = psrc[qw];
       }
       q = qw;
     } else {
       q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
     }
-    const uint32_t src = uint32_t(psrc[q] + (c0 + ec - (SEARCH == 2 ? qa : ps[q])));
+    const uint32_t src = SEARCH == 2 ? uint32_t(qs + (c0 + ec - qa)) : uint32_t(psrc[q] + (c0 + ec - ps[q]));
     if constexpr (PIN) {  // one word: split below
       rv[j] = BUF ? __builtin_amdgcn_raw_buffer_load_b32(rb, int(src * 4u), 0, 0) : rin[src];
     } else if constexpr (BUF) {
@@ -757,10 +768,12 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
     __builtin_nontemporal_store(t0 + 1 + int64_t(v >> IB), tout_o + p);
     if (PACK) {
       __builtin_nontemporal_store(int32_t(v & ((1u << kOtRuleBits) - 1u)), rout_o + p);
-      if (p > 0) bad |= pk[p - 1] >= v;  // (time, rule) order of the chunk: the words ascend
+      const uint32_t u = ot_prev(pk, p, v);
+      if (p > 0) bad |= u >= v;  // (time, rule) order of the chunk: the words ascend
     } else {
       __builtin_nontemporal_store(rl[v & kOtIdxMask], rout_o + p);
-      if (p > 0) bad |= ot_out_of_order(pk[p - 1], v, rl);  // (time, rule) order of the chunk
+      const uint32_t u = ot_prev(pk, p, v);
+      if (p > 0) bad |= ot_out_of_order(u, v, rl);  // (time, rule) order of the chunk
     }
   }
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
