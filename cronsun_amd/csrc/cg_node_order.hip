@@ -1291,10 +1291,19 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   // nodes' merge runs on its own stream beside the sparse one (few dense
   // nodes after all the sparse ones would run as a tail at low occupancy)
   const int64_t dense_min = int64_t(CG_OT_DENSE_PER_SLAB) * std::max<int64_t>(1, (H + 63) / 64);
-  if (!c->st_ot) {
-    HIPCHK(hipStreamCreateWithFlags(&c->st_ot, hipStreamNonBlocking));
-    HIPCHK(hipEventCreateWithFlags(&c->ot_fork, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ot_join, hipEventDisableTiming));
+  if (!c->st_ot) {  // created together: the ctx holds all three or none
+    hipStream_t so = nullptr;
+    hipEvent_t ef = nullptr, ej = nullptr;
+    if (hipStreamCreateWithFlags(&so, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&ef, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ej, hipEventDisableTiming) != hipSuccess) {
+      if (ef) (void)hipEventDestroy(ef);
+      if (so) (void)hipStreamDestroy(so);
+      return cg_fail(CG_EHIP, "time order: stream / event creation failed");
+    }
+    c->st_ot = so;
+    c->ot_fork = ef;
+    c->ot_join = ej;
   }
   HIPCHK(hipEventRecord(c->ot_fork, st));
   HIPCHK(hipStreamWaitEvent(c->st_ot, c->ot_fork, 0));
