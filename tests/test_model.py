@@ -1,7 +1,8 @@
 """cronsun's Job/JobRule/Group resolution on the host (C++ cg_jobset behind
 cronsun_amd.model) vs the oracle's restatement of job.go:274-288, 591-630,
 group.go:111-119 and web/job.go:222-257.  The reference has no tests for this
-code, so parity here is pinned by the oracle only."""
+code, so parity here rests on the oracle and on the hand-derived
+fixtures of tests/golden/rule_nodes_cases.py (tests/test_rule_nodes_fixtures.py)."""
 import numpy as np
 import pytest
 
