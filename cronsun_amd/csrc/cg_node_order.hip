@@ -236,7 +236,11 @@ template <int NW, int D>  // D digits: 64 or 256
 struct OtRank {
   int32_t run[NW][D];  // per wave: its events of each digit, then their first position
   int32_t dbase[65];   // D == 64: exclusive prefix of the digit totals; [64] = events
+  int32_t wtot[4];     // CG_OT_SCAN_ALL: the digit-scan waves' totals
 };
+#ifndef CG_OT_SCAN_ALL
+#define CG_OT_SCAN_ALL 1  // a 256-digit scan by 256 threads, one digit each (fewer live VGPRs: no merge spills)
+#endif
 
 // Stable positions of the n valid items (item j of wave w, lane l = element
 // w*64*kOtItems + j*64 + l) by the digit dg[j] < D: earlier elements with
@@ -285,7 +289,32 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[IT], int n, int32_t
     }
   }
   ot_sync<NW>();
-  if (NW * P > 16 && threadIdx.x < 64) {  // many waves: the counts re-read from LDS, not held in registers
+  if constexpr (CG_OT_SCAN_ALL && D == 256 && NW >= 4) {  // thread d < 256: digit d
+    const int d = threadIdx.x;
+    int32_t c[NW], sum = 0;
+#pragma unroll
+    for (int ww = 0; ww < NW; ww++) {
+      c[ww] = d < D ? s.run[ww][d] : 0;
+      sum += c[ww];
+    }
+    int32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int32_t y = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63 && w < 4) s.wtot[w] = inc;
+    ot_sync<NW>();
+    int32_t acc = inc - sum;
+    for (int ww = 0; ww < w && ww < 4; ww++) acc += s.wtot[ww];
+    if (d < D) {
+#pragma unroll
+      for (int ww = 0; ww < NW; ww++) {
+        s.run[ww][d] = acc;
+        acc += c[ww];
+      }
+    }
+  } else if (NW * P > 16 && threadIdx.x < 64) {  // many waves: the counts re-read from LDS, not held in registers
     const int d0 = threadIdx.x * P;
     int32_t sum = 0;
 #pragma unroll
