@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round-4 final (e), after the all-thread rank scan: the time-order bench lines (CPU baselines), then kernel
+# traces + HBM traffic of both time-order workloads -> gpurun_out/r4fe
+set -o pipefail
+O=gpurun_out/r4fe
+mkdir -p $O
+for w in pernode_to config3_to; do
+  case $w in
+    pernode_to) args="--workload pernode --time-order --steps 10";;
+    config3_to) args="--workload config3 --time-order --steps 1 --warmup 1";;
+  esac
+  timeout -k 10 400 python -u bench.py $args > $O/$w.json 2> $O/$w.err || { echo "bench $w failed"; tail -20 $O/$w.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/$w.json')); print('$w', '%.4g' % d['value'], 'ms/step %.3f' % d['ms_per_step'], 'frac %.3f' % d['roofline']['frac'], d['verified'], d['verify']['every_step']['mismatches'])"
+done
+bash tools/pmc_config3_order.sh r4fe/c3o > /dev/null || exit 1
+bash tools/pmc_time_order.sh r4fe/pto > /dev/null || exit 1
+echo profiles done
