@@ -1301,6 +1301,9 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
   return CG_OK;
 }
 
+#ifndef CG_OT_DENSE_BPC
+#define CG_OT_DENSE_BPC 2  // blocks per CU of the dense merge's persistent grid
+#endif
 #ifndef CG_OT_DENSE_PER_SLAB
 #define CG_OT_DENSE_PER_SLAB 4096  // average events per 64-s slab above which a node takes the 8-wave merge
 #endif
@@ -1339,7 +1342,7 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
   auto merges = [&](auto m4, auto m8, auto mid_k, auto mid2_k) {
     // the dense merge: a persistent grid (2 blocks per CU) taking nodes by ticket
-    hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * 2))), dim3(64 * kOtMidWaves), 0,
+    hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtMidWaves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
                        dense_min, INT64_MAX, big_n + 2, err);
