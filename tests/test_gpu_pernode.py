@@ -560,3 +560,52 @@ def test_per_node_bands_past_2_30_fires():
     dr.free()
     sp.free()
     e2.close()
+
+
+@pytest.mark.parametrize("writer", ["pass", "direct"])
+def test_per_node_time_ordered_over_2_20_rules(writer):
+    """More than 2^20 rules: the time order cannot pack (offset, rule) into one
+    32-bit word, so the writer emits 16-bit offsets + rules ("direct") or the
+    pass reads the int64 lists ("pass"), and the tile sort and merges keep an
+    LDS rule array -- the path every smaller test skips.  1.1 M rules on 64
+    nodes, 220 every-second and 1100 every-10-s rules among never-firing ones,
+    10 minutes; four nodes' lists against the oracle's, sorted by (time, rule)."""
+    from cronsun_amd.engine import Engine
+    R, N = (1 << 20) + 50_000, 64
+    kinds = ["0 0 0 1 1 *", "* * * * * *", "*/10 * * * * *"]
+    kind = np.zeros(R, np.int64)
+    kind[::5000] = 1
+    kind[1::1000] = 2
+    specs = [kinds[k] for k in kind.tolist()]
+    arr, status = cron.parse_batch(specs, threads=16)
+    assert not np.any(status)
+    rin = progression_rules(R, N)
+    t0 = synth.T0_2026 + 20 * DAY + 123  # January 25: the yearly rules never fire
+    t1 = t0 + 600
+    eng = Engine(0)
+    try:
+        sp = eng.upload_c(arr, R)
+        dr = eng.upload_rules(rin)
+        if writer == "direct":
+            eng.set_node_order(_lib.NODE_ORDER_TIME)
+        E, _ = eng.expand_per_node_rules_device(sp, product_zone("UTC"), t0, t1, dr, _lib.EXCLUDE_NONE)
+        if writer == "pass":
+            eng.node_order_by_time()
+        off, time, rule = eng.node_result(N, E)
+    finally:
+        eng.set_node_order(_lib.NODE_ORDER_RULE)
+        eng.close()
+    assert E > 100_000
+    parsed = [O.parse(k)[0] for k in kinds]
+    r_all = np.arange(R)
+    for n in (0, 1, 37, 63):
+        rules_n = r_all[(r_all % N == n) | ((7 * r_all + 1) % N == n)]
+        oarr = O.sched_array([parsed[k] for k in kind[rules_n].tolist()])
+        eo, et = O.expand_batch(oarr, t0, t1, oracle_zone("UTC"))
+        exp_t, exp_p = O.node_list(eo, et, list(range(len(rules_n))))
+        exp_r = rules_n[exp_p]
+        order = np.lexsort((exp_r, exp_t))
+        a, b = int(off[n]), int(off[n + 1])
+        assert b - a == len(exp_t), n
+        assert np.array_equal(time[a:b], exp_t[order]), n
+        assert np.array_equal(rule[a:b], exp_r[order]), n
