@@ -816,8 +816,10 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
 // grid taking nodes by ticket, on its own stream beside the 4-wave launch)
 // for denser ones (same-box A/Bs, profiles/r04_ab_merge_shape.txt: 8-wave
 // chunks for every node are 6-9 % faster on config 3's ~4.6 k events per
-// slab and 11-13 % slower on pernode's ~1.6 k; the split at 4096 takes
-// config 3 from ~600 to 555 ms per step and leaves pernode unchanged).  A slab of more than a chunk is queued: to k_ot_mid when it
+// slab and 11-13 % slower on pernode's ~1.6 k; the split at 4096 took
+// config 3 from ~600 to 555 ms per step and left pernode unchanged; with the
+// all-thread rank scan (no spills in the 8-wave merge) a split at 2048 is
+// 1.6 % faster on pernode and equal on config 3, profiles/r04_ab_dense_2048.txt).  A slab of more than a chunk is queued: to k_ot_mid when it
 // fits k_ot_mid's chunk (mid / mid_n), else to k_ot_big (big / big_n);
 // entries (node << 8 | slab).
 template <int NW, bool PACK, int IT = kOtItems, bool DYN = false, bool PIN = false>  // DYN: nodes by ticket (persistent grid)
@@ -1305,7 +1307,7 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
 #define CG_OT_DENSE_BPC 2  // blocks per CU of the dense merge's persistent grid
 #endif
 #ifndef CG_OT_DENSE_PER_SLAB
-#define CG_OT_DENSE_PER_SLAB 4096  // average events per 64-s slab above which a node takes the 8-wave merge
+#define CG_OT_DENSE_PER_SLAB 2048  // average events per 64-s slab above which a node takes the 8-wave merge
 #endif
 // pin: the tiles were stored as packed words offset << 20 | rule (in node_rule2)
 int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st, int64_t* err,
