@@ -210,10 +210,16 @@ constexpr int kOtMergeItems = CG_OT_MERGE_ITEMS;  // k_ot_merge: events per thre
 // rule (the word order is the (time, rule) order; no rule array in LDS)
 constexpr int kOtRuleBits = 20;
 // chunk index bits of a packed word (offset << kOtIdxBits | index): up to
-// 8192 events (k_ot_mid's chunk: 8 waves x 64 x 16)
-constexpr int kOtIdxBits = 13;
+// 16384 events (k_ot_mid's 16-wave chunk: 16 waves x 64 x 16)
+constexpr int kOtIdxBits = 14;
 constexpr int kOtMidWaves = 8;    // k_ot_mid: waves per slab (slabs of <= 8192 events)
 constexpr int kOtMid2Waves = 16;  // its 16-wave form (slabs of <= 16384 events; one block per CU)
+#ifndef CG_OT_DENSE_WAVES
+#define CG_OT_DENSE_WAVES 8
+#endif
+constexpr int kOtDenseWaves = CG_OT_DENSE_WAVES;  // the dense nodes' merge: waves per block (8 or 16)
+static_assert(64 * kOtMid2Waves * kOtItems <= (1 << kOtIdxBits) && 64 * kOtDenseWaves * kOtItems <= (1 << kOtIdxBits),
+              "every chunk's element index fits the packed words' index bits");
 static_assert(kOtMergeWaves <= 8 && 12 + kOtIdxBits <= 32, "packed words");
 constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
 constexpr int kOtSlabBits = 6;               // slab = offset >> kOtSlabBits (64 s): one 6-bit digit
@@ -1344,7 +1350,7 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
   auto merges = [&](auto m4, auto m8, auto mid_k, auto mid2_k) {
     // the dense merge: a persistent grid (2 blocks per CU) taking nodes by ticket
-    hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtMidWaves), 0,
+    hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtDenseWaves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
                        dense_min, INT64_MAX, big_n + 2, err);
@@ -1365,13 +1371,13 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   const bool pack = CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
   if (pack && pin)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,
-           k_ot_merge<kOtMidWaves, true, kOtItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,
+           k_ot_merge<kOtDenseWaves, true, kOtItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,
            k_ot_mid<kOtMid2Waves, true, kOtItems, true>);
   else if (pack)
-    merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems>, k_ot_merge<kOtMidWaves, true, kOtItems, true>,
+    merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems>, k_ot_merge<kOtDenseWaves, true, kOtItems, true>,
            k_ot_mid<kOtMidWaves, true>, k_ot_mid<kOtMid2Waves, true>);
   else
-    merges(k_ot_merge<kOtMergeWaves, false, kOtMergeItems>, k_ot_merge<kOtMidWaves, false, kOtItems, true>,
+    merges(k_ot_merge<kOtMergeWaves, false, kOtMergeItems>, k_ot_merge<kOtDenseWaves, false, kOtItems, true>,
            k_ot_mid<kOtMidWaves, false>, k_ot_mid<kOtMid2Waves, false>);
   auto big = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff, c->node_rule2.p,

@@ -568,13 +568,16 @@ def test_per_node_time_ordered_over_2_20_rules(writer):
     32-bit word, so the writer emits 16-bit offsets + rules ("direct") or the
     pass reads the int64 lists ("pass"), and the tile sort and merges keep an
     LDS rule array -- the path every smaller test skips.  1.1 M rules on 64
-    nodes, 220 every-second and 1100 every-10-s rules among never-firing ones,
-    10 minutes; four nodes' lists against the oracle's, sorted by (time, rule)."""
+    nodes, 134 every-second rules (all on nodes 0 and 1: ~8.6 k events per
+    64-s slab there, the dense merge and k_ot_mid's 16-wave form, whose
+    16384-event chunks need 14 index bits) and 1100 every-10-s rules among
+    never-firing ones, 10 minutes; four nodes' lists against the oracle's,
+    sorted by (time, rule)."""
     from cronsun_amd.engine import Engine
     R, N = (1 << 20) + 50_000, 64
     kinds = ["0 0 0 1 1 *", "* * * * * *", "*/10 * * * * *"]
     kind = np.zeros(R, np.int64)
-    kind[::5000] = 1
+    kind[::8192] = 1
     kind[1::1000] = 2
     specs = [kinds[k] for k in kind.tolist()]
     arr, status = cron.parse_batch(specs, threads=16)
