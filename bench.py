@@ -364,7 +364,8 @@ def main():
                     # slice to rank 0 over its own link, in chunks under the budget)
                     n_off, n_time, n_rule = eng.node_result_tensors(rin.n_nodes)
                     g = shard.gather_node_csr(n_off.to(cdev), n_time.to(cdev), n_rule.to(cdev),
-                                              shard_info["lo"], dist, engine=eng, budget_bytes=args.gather_budget)
+                                              shard_info["lo"], dist, engine=eng, budget_bytes=args.gather_budget,
+                                              order="time" if args.time_order else "rule")
                     if g is not None:
                         last["gathered_events"] = int(g[1].numel())
                     del g

@@ -59,7 +59,7 @@ class cg_csr(C.Structure):
                 ("times_cap", C.c_int64), ("n_events", C.c_int64)]
 
 
-ABI_VERSION = 2  # CG_ABI_VERSION of include/cronsun_gpu.h
+ABI_VERSION = 3  # CG_ABI_VERSION of include/cronsun_gpu.h
 
 
 class cg_rules_in(C.Structure):
@@ -86,12 +86,16 @@ def _preload_torch_hip():
 
 
 def preload_torch_rccl():
-    """Import torch (when installed) before the library first loads RCCL
-    (cg_comm_*): torch links the same librccl.so, and a process that loads it
-    through the library first and imports torch afterwards aborts at exit
-    (glibc heap check in the shared libraries' teardown; tools/probe_comm_exit.py:
-    torch first, or no torch at all, exit cleanly).  A C or Go host without
-    torch is unaffected."""
+    """Convenience only: import torch (when installed) before the first
+    cg_comm call.  The library itself keeps one RCCL per process whatever the
+    order: it uses an RCCL already mapped, else loads the librccl.so beside the
+    HIP runtime it runs on (torch's copy under PyTorch-ROCm, which a later
+    torch import then maps as the same file) by full path with local symbol
+    scope, and refuses (CG_EINVAL) when a different RCCL appears later.  Round
+    4 loaded "librccl.so" by name with global scope, which resolved to
+    /opt/rocm's copy through LD_LIBRARY_PATH and was then bound by torch's
+    libraries in place of their own: a heap abort at exit
+    (tools/probe_comm_exit.py comm_torch)."""
     if importlib.util.find_spec("torch") is not None:
         import torch  # noqa: F401
 
@@ -154,6 +158,7 @@ def _declare(L):
         "cg_node_counts_to_device": ([vp, vp], C.c_int),
         "cg_node_checksum_enqueue": ([vp, vp, C.c_int32, vp], C.c_int),
         "cg_node_csr_place": ([vp, C.c_int32, vp, vp, vp, C.c_int32, vp, vp, vp], C.c_int),
+        "cg_node_csr_merge_ranks": ([vp, C.c_int32, C.c_int32, vp, vp, vp, i64], C.c_int),
         "cg_expand_per_node_rules_device_async": ([vp, vp, vp, i64, i64, vp, C.c_int], C.c_int),
         "cg_expand_per_node_wait": ([vp, P(i64), P(i64)], C.c_int),
         "cg_node_result_copy_range": ([vp, i64, i64, vp, vp], C.c_int),
@@ -174,6 +179,7 @@ def _declare(L):
         "cg_comm_allgather_i64": ([vp, vp, sz, vp], C.c_int),
         "cg_comm_node_offsets": ([vp, vp, vp], C.c_int),
         "cg_comm_gather_node_csr": ([vp, C.c_int, i64, i64, vp, vp, vp, i64, P(i64)], C.c_int),
+        "cg_comm_gather_plan": ([vp, C.c_int32, C.c_int32, C.c_int32, i64, vp, i64, P(i64)], C.c_int),
         "cg_jobset_new": ([P(vp)], C.c_int),
         "cg_jobset_free": ([vp], None),
         "cg_jobset_add_group": ([vp, C.c_char_p, vp, sz], C.c_int),

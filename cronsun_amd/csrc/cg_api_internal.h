@@ -234,7 +234,15 @@ struct cg_ctx {
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
+  // a per-node result is readable (node_off [pn_N+1], pn_E events): cleared
+  // when a per-node call starts or fails, set when one succeeds -- pn_N and
+  // node_off may be stale otherwise (the gather / node offsets check it)
+  bool pn_valid = false;
   int64_t pn_R = INT64_MAX;  // rule count of the per-node lists being ordered (the merge packs rules below 2^20)
+  // time-ordered gather (merge_ranks_enqueue): per-node run bounds, the tile
+  // prefix over runs, and a scratch copy of one node group
+  DBuf<int64_t> mr_rb, mr_tp, mr_t;
+  DBuf<int32_t> mr_r;
   int64_t* pn_res_host = nullptr;  // mapped pinned: per-node event total of the last call
   int64_t* pn_res_dev = nullptr;
   // the rule->node join + transpose depend only on (rule set, exclude mode):
@@ -277,6 +285,7 @@ struct cg_ctx {
     rule_info.release();
     ts_cnt.release(); ts_tile_node.release(); ts_hist.release(); node_rule2.release();
     ts_base.release(); ts_off.release(); node_time2.release(); ts_node_off.release(); ts_rec.release();
+    mr_rb.release(); mr_tp.release(); mr_t.release(); mr_r.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);
     pn_res_host = nullptr;
     pn_res_dev = nullptr;
@@ -363,12 +372,23 @@ int order_by_time_locked(cg_ctx* c, int in_mode = 0);
 // kernels of the per-node CSR gather (cg_pernode.hip), enqueued on st:
 // node n's events [src_off[n], src_off[n+1]) of src to dst_start[n] onwards /
 // n contiguous events / the last per-node result's counts per node
-int launch_node_place(cg_ctx* c, hipStream_t st, int32_t N, const int64_t* src_off, const int64_t* src_time,
-                      const int32_t* src_rule, int32_t rule_add, const int64_t* dst_start, int64_t* dst_time,
-                      int32_t* dst_rule);
+// (event i of src_off's numbering at src_*[i - src_shift])
+int launch_node_place(cg_ctx* c, hipStream_t st, int32_t N, const int64_t* src_off, int64_t src_shift,
+                      const int64_t* src_time, const int32_t* src_rule, int32_t rule_add, const int64_t* dst_start,
+                      int64_t* dst_time, int32_t* dst_rule);
 int launch_span_place(cg_ctx* c, hipStream_t st, int64_t n, const int64_t* src_time, const int32_t* src_rule,
                       int32_t rule_add, int64_t* dst_time, int32_t* dst_rule);
 int launch_node_counts(cg_ctx* c, hipStream_t st, int64_t* d_counts);
+// Time-ordered gather: every node's list in d_time / d_rule holds W runs (the
+// ranks' slices in rank = job-ID order, each in (time, rule) order); h_rb
+// [N*(W+1)] (host) are the run bounds, node-major: run g of node n is
+// [h_rb[n*(W+1)+g], h_rb[n*(W+1)+g+1]).  Merges every node's runs in place
+// into (time, rule) order, one group of nodes of at most scratch_ev events at
+// a time (a larger node alone) through a scratch copy (scr_t / scr_r), on st;
+// returns after the stream has drained.
+int merge_ranks_locked(cg_ctx* c, hipStream_t st, int32_t N, int32_t W, const int64_t* h_rb, int64_t* d_time,
+                       int32_t* d_rule, int64_t scratch_ev, DBuf<int64_t>& scr_t, DBuf<int32_t>& scr_r);
+constexpr int kMergeMaxRanks = 64;
 // CG_ORDER_LSD set: order every window by the LSD passes (int64 times; the
 // writer must not emit 16-bit offsets then)
 bool order_lsd_only();

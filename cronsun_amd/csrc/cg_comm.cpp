@@ -4,15 +4,23 @@
 // SURVEY.md §8e).  Rules shard by job-ID range with no data-path collective:
 // the reference's nodes each filter every job (node/node.go:121-141), here a
 // rank evaluates one range of jobs for every node, and node n's global list
-// is the ranks' slices in rank (= job-ID) order.
+// is the ranks' slices in rank (= job-ID) order -- or, for time-ordered
+// results, those slices merged by (time, rule) (the byTime order of the node's
+// Cron, node/cron/cron.go:64-79,220).
 //
-// RCCL is loaded at run time: the RCCL already in the process (torch's) or
-// the one beside the HIP runtime this library links (its runpath), else
-// /opt/rocm/lib -- so the library has no link-time dependency on RCCL and a
-// process that also runs torch.distributed over RCCL holds one copy.
+// RCCL is loaded at run time, one copy per process: the RCCL already mapped
+// (e.g. torch's), else the librccl.so beside the HIP runtime this library
+// runs on (with PyTorch-ROCm: torch's own copy, so a torch imported later maps
+// the same file), else /opt/rocm/lib -- always by full path and RTLD_LOCAL, so
+// the name "librccl.so" never resolves a later DT_NEEDED to our copy and our
+// symbols never interpose on another copy's users.  A second, different RCCL
+// mapped afterwards makes every cg_comm call fail (cg_last_error names both)
+// instead of mixing the two.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <link.h>
 #include <rccl/rccl.h>
+#include <sys/stat.h>
 
 #include <algorithm>
 #include <cstring>
@@ -27,10 +35,13 @@ namespace {
 
 struct Rccl {
   bool ok = false;
-  std::string err;
+  std::string err, path;
+  dev_t dev = 0;
+  ino_t ino = 0;
   decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
   decltype(&ncclCommInitRank) CommInitRank = nullptr;
   decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclCommAbort) CommAbort = nullptr;
   decltype(&ncclAllGather) AllGather = nullptr;
   decltype(&ncclSend) Send = nullptr;
   decltype(&ncclRecv) Recv = nullptr;
@@ -39,19 +50,73 @@ struct Rccl {
   decltype(&ncclGetErrorString) GetErrorString = nullptr;
 };
 
+bool is_rccl_name(const char* path) {
+  const char* b = strrchr(path, '/');
+  b = b ? b + 1 : path;
+  return strncmp(b, "librccl.so", 10) == 0;
+}
+
+// every RCCL file mapped in this process (distinct files)
+struct Mapped {
+  std::vector<std::string> paths;
+  std::vector<std::pair<dev_t, ino_t>> ids;
+};
+Mapped mapped_rccl() {
+  Mapped m;
+  dl_iterate_phdr(
+      [](dl_phdr_info* info, size_t, void* arg) -> int {
+        Mapped& mm = *static_cast<Mapped*>(arg);
+        if (!info->dlpi_name || !*info->dlpi_name || !is_rccl_name(info->dlpi_name)) return 0;
+        struct stat sb;
+        if (stat(info->dlpi_name, &sb) != 0) return 0;
+        for (auto& id : mm.ids)
+          if (id.first == sb.st_dev && id.second == sb.st_ino) return 0;
+        mm.ids.push_back({sb.st_dev, sb.st_ino});
+        mm.paths.push_back(info->dlpi_name);
+        return 0;
+      },
+      &m);
+  return m;
+}
+
+// the directory of the HIP runtime this library runs on
+std::string hip_runtime_dir() {
+  Dl_info di;
+  if (!dladdr(reinterpret_cast<void*>(static_cast<hipError_t (*)(void**, size_t)>(&hipMalloc)), &di) || !di.dli_fname) return "";
+  std::string p = di.dli_fname;
+  const size_t s = p.rfind('/');
+  return s == std::string::npos ? "" : p.substr(0, s);
+}
+
 const Rccl& rccl() {
   static Rccl r;
   static std::once_flag once;
   std::call_once(once, [] {
-    // torch's copy is "librccl.so" (no soname; libtorch_hip needs that name)
-    void* h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);  // this library's runpath: beside its HIP runtime
-    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    void* h = nullptr;
+    const Mapped m = mapped_rccl();
+    if (!m.paths.empty()) {  // already in the process (torch.distributed's)
+      h = dlopen(m.paths[0].c_str(), RTLD_NOW | RTLD_NOLOAD);
+      if (h) r.path = m.paths[0];
+    }
+    std::vector<std::string> cand;
+    const std::string hd = hip_runtime_dir();
+    if (!hd.empty()) cand.push_back(hd + "/librccl.so");
+    cand.push_back("/opt/rocm/lib/librccl.so.1");
+    for (size_t i = 0; !h && i < cand.size(); i++) {
+      struct stat sb;
+      if (stat(cand[i].c_str(), &sb) != 0) continue;
+      h = dlopen(cand[i].c_str(), RTLD_NOW | RTLD_LOCAL);
+      if (h) r.path = cand[i];
+    }
     if (!h) {
       const char* e = dlerror();
-      r.err = std::string("RCCL not loadable: ") + (e ? e : "librccl.so.1 not found");
+      r.err = std::string("RCCL not loadable: ") + (e ? e : "no librccl.so beside the HIP runtime or in /opt/rocm/lib");
       return;
+    }
+    struct stat sb;
+    if (stat(r.path.c_str(), &sb) == 0) {
+      r.dev = sb.st_dev;
+      r.ino = sb.st_ino;
     }
     bool all = true;
     auto sym = [&](auto& f, const char* name) {
@@ -61,6 +126,7 @@ const Rccl& rccl() {
     sym(r.GetUniqueId, "ncclGetUniqueId");
     sym(r.CommInitRank, "ncclCommInitRank");
     sym(r.CommDestroy, "ncclCommDestroy");
+    sym(r.CommAbort, "ncclCommAbort");
     sym(r.AllGather, "ncclAllGather");
     sym(r.Send, "ncclSend");
     sym(r.Recv, "ncclRecv");
@@ -68,12 +134,26 @@ const Rccl& rccl() {
     sym(r.GroupEnd, "ncclGroupEnd");
     sym(r.GetErrorString, "ncclGetErrorString");
     if (!all) {
-      r.err = "RCCL library lacks an expected symbol";
+      r.err = "RCCL library " + r.path + " lacks an expected symbol";
       return;
     }
     r.ok = true;
   });
   return r;
+}
+
+// RCCL usable, and no other RCCL file mapped beside ours (a second copy --
+// e.g. a torch imported after the first cg_comm call that found its RCCL
+// elsewhere -- would mix two libraries' state in one process)
+int rccl_ready() {
+  const Rccl& r = rccl();
+  if (!r.ok) return cg_fail(CG_ENODEV, r.err);
+  const Mapped m = mapped_rccl();
+  for (size_t i = 0; i < m.ids.size(); i++)
+    if (m.ids[i].first != r.dev || m.ids[i].second != r.ino)
+      return cg_fail(CG_EINVAL, "two RCCL libraries in this process: " + r.path + " (used by cg_comm) and " +
+                                    m.paths[i] + " (mapped later); load the host's RCCL before the first cg_comm call");
+  return CG_OK;
 }
 
 int nccl_check(ncclResult_t e, const char* what) {
@@ -91,17 +171,32 @@ int nccl_check(ncclResult_t e, const char* what) {
 
 struct cg_comm {
   cg_ctx* ctx = nullptr;
-  ncclComm_t nc = nullptr;
+  ncclComm_t nc = nullptr;  // null after an abort
   int world = 0, rank = 0;
   DBuf<int64_t> scratch;       // small all-gathers
   DBuf<int64_t> cnt;           // [world * N] per-node counts
   DBuf<int64_t> off_all;       // [world * (N+1)] every rank's node offsets
   DBuf<int64_t> starts;        // [world * N] destinations of every rank's slices
-  DBuf<int64_t> stage_t;       // root: one chunk of peer times
+  DBuf<int64_t> stage_t;       // root: one chunk of peer times (and the merge's scratch)
   DBuf<int32_t> stage_r;       // root: and rules
 };
 
 namespace {
+
+int comm_usable(cg_comm* m) {
+  int rc = rccl_ready();
+  if (rc) return rc;
+  if (!m->nc) return cg_fail(CG_EHIP, "cg_comm: the communicator was aborted by an earlier failed transfer");
+  return CG_OK;
+}
+
+// A transfer failed after every rank agreed to run it: peers may be blocked in
+// the matching send/receive, so the communicator is aborted (their RCCL calls
+// then fail instead of waiting forever) and refuses every later call.
+void abort_comm(cg_comm* m) {
+  if (m->nc) (void)rccl().CommAbort(m->nc);
+  m->nc = nullptr;
+}
 
 // c->mu held.  all[g*n + i] = rank g's mine[i], through device scratch.
 int allgather_locked(cg_comm* m, const int64_t* mine, size_t n, int64_t* all) {
@@ -110,8 +205,12 @@ int allgather_locked(cg_comm* m, const int64_t* mine, size_t n, int64_t* all) {
   int rc = m->scratch.ensure(std::max<size_t>(tot, 1));
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(m->scratch.p + size_t(m->rank) * n, mine, n * 8, hipMemcpyHostToDevice, c->st));
-  NCCLCHK(rccl().AllGather(m->scratch.p + size_t(m->rank) * n, m->scratch.p, n, ncclInt64, m->nc, c->st),
-          "ncclAllGather");
+  rc = nccl_check(rccl().AllGather(m->scratch.p + size_t(m->rank) * n, m->scratch.p, n, ncclInt64, m->nc, c->st),
+                  "ncclAllGather");
+  if (rc) {
+    abort_comm(m);
+    return rc;
+  }
   HIPCHK(hipMemcpyAsync(all, m->scratch.p, tot * 8, hipMemcpyDeviceToHost, c->st));
   return cg_hip_check(hipStreamSynchronize(c->st), "allgather sync");
 }
@@ -124,8 +223,12 @@ int node_counts_locked(cg_comm* m, int64_t N, std::vector<int64_t>& host_cnt) {
   if ((rc = m->cnt.ensure(std::max<int64_t>(N * m->world, 1)))) return rc;
   if (N > 0) {
     if ((rc = launch_node_counts(c, c->st, m->cnt.p + int64_t(m->rank) * N))) return rc;
-    NCCLCHK(rccl().AllGather(m->cnt.p + int64_t(m->rank) * N, m->cnt.p, size_t(N), ncclInt64, m->nc, c->st),
-            "ncclAllGather(node counts)");
+    rc = nccl_check(rccl().AllGather(m->cnt.p + int64_t(m->rank) * N, m->cnt.p, size_t(N), ncclInt64, m->nc, c->st),
+                    "ncclAllGather(node counts)");
+    if (rc) {
+      abort_comm(m);
+      return rc;
+    }
   }
   host_cnt.assign(size_t(N * m->world), 0);
   if (N > 0) HIPCHK(hipMemcpyAsync(host_cnt.data(), m->cnt.p, size_t(N * m->world) * 8, hipMemcpyDeviceToHost, c->st));
@@ -136,11 +239,12 @@ int node_counts_locked(cg_comm* m, int64_t N, std::vector<int64_t>& host_cnt) {
 // [n0, n1) whose peer events (every rank but root) fit cap_ev, and a node
 // with more than cap_ev peer events in k parts (part j of peer g: its events
 // [c*j/k, c*(j+1)/k) of that node, so a part holds at most
-// P/k + world - 1 <= cap_ev events).  (cronsun_amd/shard.py restates it.)
+// P/k + world - 1 <= cap_ev events).  (cronsun_amd/shard.py restates it;
+// cg_comm_gather_plan exposes this one.)
 struct Chunk {
   int64_t n0, n1, j, k;
 };
-std::vector<Chunk> gather_plan(const std::vector<int64_t>& cnt, int world, int64_t N, int root, int64_t cap_ev) {
+std::vector<Chunk> gather_plan(const int64_t* cnt, int world, int64_t N, int root, int64_t cap_ev) {
   std::vector<Chunk> out;
   std::vector<int64_t> P(size_t(N), 0);
   for (int g = 0; g < world; g++)
@@ -169,26 +273,26 @@ extern "C" {
 
 int cg_comm_unique_id(uint8_t id[CG_COMM_ID_BYTES]) {
   if (!id) return cg_fail(CG_EINVAL, "cg_comm_unique_id: null");
-  const Rccl& r = rccl();
-  if (!r.ok) return cg_fail(CG_ENODEV, r.err);
+  int rc = rccl_ready();
+  if (rc) return rc;
   static_assert(sizeof(ncclUniqueId) == CG_COMM_ID_BYTES, "unique id size");
   ncclUniqueId u;
-  NCCLCHK(r.GetUniqueId(&u), "ncclGetUniqueId");
+  NCCLCHK(rccl().GetUniqueId(&u), "ncclGetUniqueId");
   std::memcpy(id, &u, CG_COMM_ID_BYTES);
   return CG_OK;
 }
 
 int cg_comm_init(cg_ctx* c, int world, int rank, const uint8_t id[CG_COMM_ID_BYTES], cg_comm** out) {
   if (!c || !id || !out || world < 1 || rank < 0 || rank >= world) return cg_fail(CG_EINVAL, "cg_comm_init: bad argument");
-  const Rccl& r = rccl();
-  if (!r.ok) return cg_fail(CG_ENODEV, r.err);
+  int rc = rccl_ready();
+  if (rc) return rc;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipGetLastError();
   HIPCHK(hipSetDevice(c->device));
   ncclUniqueId u;
   std::memcpy(&u, id, CG_COMM_ID_BYTES);
   ncclComm_t nc = nullptr;
-  NCCLCHK(r.CommInitRank(&nc, world, u, rank), "ncclCommInitRank");
+  NCCLCHK(rccl().CommInitRank(&nc, world, u, rank), "ncclCommInitRank");
   cg_comm* m = new cg_comm();
   m->ctx = c;
   m->nc = nc;
@@ -217,6 +321,8 @@ void cg_comm_free(cg_comm* m) {
 
 int cg_comm_allgather_i64(cg_comm* m, const int64_t* mine, size_t n, int64_t* all) {
   if (!m || (n && (!mine || !all))) return cg_fail(CG_EINVAL, "cg_comm_allgather_i64: null");
+  int rc = comm_usable(m);
+  if (rc) return rc;
   cg_ctx* c = m->ctx;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipGetLastError();
@@ -227,19 +333,23 @@ int cg_comm_allgather_i64(cg_comm* m, const int64_t* mine, size_t n, int64_t* al
 
 int cg_comm_node_offsets(cg_comm* m, int64_t* node_start, int64_t* node_base) {
   if (!m) return cg_fail(CG_EINVAL, "cg_comm_node_offsets: null");
+  int rc = comm_usable(m);
+  if (rc) return rc;
   cg_ctx* c = m->ctx;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipGetLastError();
   HIPCHK(hipSetDevice(c->device));
   // every rank's node count and whether it has a readable result
-  const int64_t mine[2] = {c->pn_N, pn_async_pending(c) ? 1 : 0};
+  const bool ok = c->pn_valid && !pn_async_pending(c);
+  const int64_t mine[2] = {c->pn_N, ok ? 1 : 0};
   std::vector<int64_t> meta(size_t(2 * m->world));
-  int rc = allgather_locked(m, mine, 2, meta.data());
-  if (rc) return rc;
+  if ((rc = allgather_locked(m, mine, 2, meta.data()))) return rc;
   for (int q = 0; q < m->world; q++) {
+    if (!meta[size_t(2 * q + 1)])
+      return cg_fail(CG_EINVAL, "cg_comm_node_offsets: rank " + std::to_string(q) +
+                                    " has no readable per-node result (none yet, a failed call, or pipelined "
+                                    "windows pending)");
     if (meta[size_t(2 * q)] != c->pn_N) return cg_fail(CG_EINVAL, "cg_comm_node_offsets: ranks differ in node count");
-    if (meta[size_t(2 * q + 1)])
-      return cg_fail(CG_EINVAL, "cg_comm_node_offsets: a rank has pipelined per-node windows pending");
   }
   const int64_t N = c->pn_N;
   std::vector<int64_t> cnt;
@@ -260,34 +370,59 @@ int cg_comm_node_offsets(cg_comm* m, int64_t* node_start, int64_t* node_base) {
   return CG_OK;
 }
 
+int cg_comm_gather_plan(const int64_t* counts, int32_t world, int32_t n_nodes, int32_t root, int64_t budget_bytes,
+                        int64_t* chunks, int64_t cap, int64_t* n_chunks) {
+  if (!counts || world < 1 || n_nodes < 0 || root < 0 || root >= world || (cap > 0 && !chunks) || !n_chunks)
+    return cg_fail(CG_EINVAL, "cg_comm_gather_plan: bad argument");
+  const int64_t cap_ev = budget_bytes / 12;
+  if (world > 1 && cap_ev < 2 * int64_t(world)) return cg_fail(CG_EINVAL, "cg_comm_gather_plan: budget below 24 bytes per rank");
+  const std::vector<Chunk> plan = gather_plan(counts, world, n_nodes, root, cap_ev);
+  *n_chunks = int64_t(plan.size());
+  if (int64_t(plan.size()) > cap)
+    return cg_fail(CG_ECAPACITY, "cg_comm_gather_plan: " + std::to_string(plan.size()) + " chunks");
+  for (size_t i = 0; i < plan.size(); i++) {
+    chunks[4 * i] = plan[i].n0;
+    chunks[4 * i + 1] = plan[i].n1;
+    chunks[4 * i + 2] = plan[i].j;
+    chunks[4 * i + 3] = plan[i].k;
+  }
+  return CG_OK;
+}
+
 int cg_comm_gather_node_csr(cg_comm* m, int root, int64_t rule_base, int64_t budget_bytes, int64_t* d_node_off,
                             int64_t* d_time, int32_t* d_rule, int64_t cap, int64_t* n_events) {
-  constexpr int kMeta = 6;  // node count, events, ok, rule_base, cap, budget
+  constexpr int kMeta = 7;  // node count, events, ok, rule_base, cap, budget, time-ordered
   if (!m || root < 0 || root >= m->world) return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: bad argument");
+  int rc = comm_usable(m);
+  if (rc) return rc;
   cg_ctx* c = m->ctx;
   const int W = m->world, me = m->rank;
   std::lock_guard<std::mutex> g(c->mu);
   (void)hipGetLastError();
   HIPCHK(hipSetDevice(c->device));
-  // every rank's preconditions travel with one all-gather, so every rank
-  // returns the same status instead of leaving its peers blocked in a transfer
-  const bool local_ok = !pn_async_pending(c) && !c->pn_time_ordered && rule_base >= 0 && rule_base <= INT32_MAX &&
+  // Agreement 1: every rank's preconditions travel with one all-gather, so
+  // every rank returns the same status instead of leaving its peers blocked
+  // in a transfer
+  const bool local_ok = c->pn_valid && !pn_async_pending(c) && rule_base >= 0 && rule_base <= INT32_MAX &&
                         (me != root || ((d_node_off && d_time && d_rule) || c->pn_N == 0)) && budget_bytes > 0;
-  const int64_t mine[kMeta] = {c->pn_N, c->pn_E, local_ok ? 1 : 0, rule_base, cap, budget_bytes};
+  const int64_t mine[kMeta] = {c->pn_N, c->pn_E, local_ok ? 1 : 0, rule_base, cap, budget_bytes,
+                               c->pn_time_ordered ? 1 : 0};
   std::vector<int64_t> meta(size_t(kMeta * W));
-  int rc = allgather_locked(m, mine, kMeta, meta.data());
-  if (rc) return rc;
+  if ((rc = allgather_locked(m, mine, kMeta, meta.data()))) return rc;
   const int64_t N = c->pn_N;
   int64_t total = 0;
   for (int q = 0; q < W; q++) {
     const int64_t* mq = &meta[size_t(kMeta * q)];
-    if (mq[0] != N) return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: ranks differ in node count");
     if (!mq[2])
       return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: rank " + std::to_string(q) +
-                                    " has no gatherable result (pending windows, a time-ordered result, a bad "
+                                    " has no gatherable result (none yet, a failed call, pending windows, a bad "
                                     "rule_base or budget, or null output buffers on root)");
+    if (mq[0] != N) return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: ranks differ in node count");
+    if (mq[6] != meta[6])
+      return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: ranks differ in list order (some results time-ordered)");
     total += mq[1];
   }
+  const bool timed = meta[6] != 0;
   if (n_events) *n_events = total;
   const int64_t root_cap = meta[size_t(kMeta * root + 4)];
   if (total > root_cap)
@@ -300,7 +435,7 @@ int cg_comm_gather_node_csr(cg_comm* m, int root, int64_t rule_base, int64_t bud
   if (W > 1 && cap_ev < 2 * int64_t(W))
     return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: budget below 24 bytes per rank");
   std::vector<int64_t> cnt;
-  if ((rc = node_counts_locked(m, N, cnt))) return rc;
+  if ((rc = node_counts_locked(m, N, cnt))) return rc;  // a collective: every rank reaches it
   // every rank's node offsets, and the destinations of every rank's slices
   std::vector<int64_t> off(size_t(W * (N + 1))), st(size_t(W * N)), base(size_t(N + 1));
   for (int q = 0; q < W; q++) {
@@ -320,90 +455,137 @@ int cg_comm_gather_node_csr(cg_comm* m, int root, int64_t rule_base, int64_t bud
     }
   }
   base[size_t(N)] = b;
-  const std::vector<Chunk> plan = gather_plan(cnt, W, N, root, cap_ev);
-  hipStream_t s = c->st;
-  if (me == root) {
-    if (N > 0) {
-      if ((rc = m->off_all.ensure(size_t(W * (N + 1)))) || (rc = m->starts.ensure(size_t(W * N)))) return rc;
-      HIPCHK(hipMemcpyAsync(m->off_all.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s));
-      HIPCHK(hipMemcpyAsync(m->starts.p, st.data(), st.size() * 8, hipMemcpyHostToDevice, s));
-      HIPCHK(hipMemcpyAsync(d_node_off, base.data(), base.size() * 8, hipMemcpyHostToDevice, s));
+  const std::vector<Chunk> plan = gather_plan(cnt.data(), W, N, root, cap_ev);
+  // peer q's piece of a chunk: its events [lo, hi) of its own CSR
+  auto piece = [&](const Chunk& ch, int q, int64_t* lo, int64_t* hi) {
+    const int64_t a = off[size_t(q * (N + 1) + ch.n0)];
+    if (ch.k == 1) {
+      *lo = a;
+      *hi = off[size_t(q * (N + 1) + ch.n1)];
+    } else {
+      const int64_t cq = cnt[size_t(q * N + ch.n0)];
+      *lo = a + cq * ch.j / ch.k;
+      *hi = a + cq * (ch.j + 1) / ch.k;
     }
+  };
+  hipStream_t s = c->st;
+  // Root prepares everything before the transfers: staging (also the merge's
+  // scratch), node offsets, slice destinations, its own slice.  Agreement 2
+  // carries every rank's status of that step, so no rank starts a transfer
+  // its peers will not join.
+  int prep = CG_OK;
+  std::string prep_msg;
+  if (me == root) {
     int64_t stage = 1;
     for (const Chunk& ch : plan) {
       int64_t ev = 0;
       for (int q = 0; q < W; q++) {
         if (q == root) continue;
-        const int64_t cq = cnt[size_t(q * N + ch.n0)];
-        ev += ch.k == 1 ? off[size_t(q * (N + 1) + ch.n1)] - off[size_t(q * (N + 1) + ch.n0)]
-                        : cq * (ch.j + 1) / ch.k - cq * ch.j / ch.k;
+        int64_t lo, hi;
+        piece(ch, q, &lo, &hi);
+        ev += hi - lo;
       }
       stage = std::max(stage, ev);
     }
-    if (!plan.empty() && ((rc = m->stage_t.ensure(size_t(stage))) || (rc = m->stage_r.ensure(size_t(stage)))))
-      return rc;
-    // root's own slice, straight from its result
-    if (N > 0 && (rc = launch_node_place(c, s, int32_t(N), c->node_off.p, c->node_time.p, c->node_rule.p,
-                                         int32_t(rule_base), m->starts.p + int64_t(root) * N, d_time, d_rule)))
-      return rc;
+    if (timed && W > 1) {  // the merge's scratch: at least the largest node
+      for (int64_t n = 0; n < N; n++) stage = std::max(stage, base[size_t(n + 1)] - base[size_t(n)]);
+      stage = std::max(stage, std::min(cap_ev, total));
+      prep = c->mr_rb.ensure(size_t(N) * (W + 1));
+      if (!prep) prep = c->mr_tp.ensure(size_t(N) * W + 1);
+    }
+    if (!prep && N > 0) prep = m->off_all.ensure(size_t(W * (N + 1)));
+    if (!prep && N > 0) prep = m->starts.ensure(size_t(W * N));
+    if (!prep && (!plan.empty() || (timed && W > 1))) prep = m->stage_t.ensure(size_t(stage));
+    if (!prep && (!plan.empty() || (timed && W > 1))) prep = m->stage_r.ensure(size_t(stage));
+    if (!prep && N > 0) {
+      prep = cg_hip_check(hipMemcpyAsync(m->off_all.p, off.data(), off.size() * 8, hipMemcpyHostToDevice, s), "copy");
+      if (!prep)
+        prep = cg_hip_check(hipMemcpyAsync(m->starts.p, st.data(), st.size() * 8, hipMemcpyHostToDevice, s), "copy");
+      if (!prep)
+        prep = cg_hip_check(hipMemcpyAsync(d_node_off, base.data(), base.size() * 8, hipMemcpyHostToDevice, s), "copy");
+      // root's own slice, straight from its result
+      if (!prep)
+        prep = launch_node_place(c, s, int32_t(N), c->node_off.p, 0, c->node_time.p, c->node_rule.p,
+                                 int32_t(rule_base), m->starts.p + int64_t(root) * N, d_time, d_rule);
+    }
+    if (prep) prep_msg = cg_last_error();
   }
+  {
+    const int64_t mine2[1] = {prep};
+    std::vector<int64_t> st2(static_cast<size_t>(W));
+    if ((rc = allgather_locked(m, mine2, 1, st2.data()))) return rc;
+    for (int q = 0; q < W; q++)
+      if (st2[size_t(q)] != CG_OK)
+        return q == me ? cg_fail(int(st2[size_t(q)]), prep_msg)
+                       : cg_fail(int(st2[size_t(q)]), "cg_comm_gather_node_csr: root (rank " + std::to_string(q) +
+                                                          ") could not prepare the gather");
+  }
+  // The transfers.  From here on no rank returns before it has issued every
+  // send / receive of the plan: a failure only stops root's placements (and
+  // aborts the communicator when RCCL itself failed).
+  int post = CG_OK;
   for (const Chunk& ch : plan) {
-    // peer q's piece: its events [lo, hi) of its own CSR
-    auto piece = [&](int q, int64_t* lo, int64_t* hi) {
-      const int64_t a = off[size_t(q * (N + 1) + ch.n0)];
-      if (ch.k == 1) {
-        *lo = a;
-        *hi = off[size_t(q * (N + 1) + ch.n1)];
-      } else {
-        const int64_t cq = cnt[size_t(q * N + ch.n0)];
-        *lo = a + cq * ch.j / ch.k;
-        *hi = a + cq * (ch.j + 1) / ch.k;
-      }
-    };
-    NCCLCHK(rccl().GroupStart(), "ncclGroupStart");
+    int rc2 = nccl_check(rccl().GroupStart(), "ncclGroupStart");
     if (me == root) {
       int64_t o = 0;
-      for (int q = 0; q < W; q++) {
+      for (int q = 0; q < W && !rc2; q++) {
         if (q == root) continue;
         int64_t lo, hi;
-        piece(q, &lo, &hi);
+        piece(ch, q, &lo, &hi);
         if (hi > lo) {
-          NCCLCHK(rccl().Recv(m->stage_t.p + o, size_t(hi - lo), ncclInt64, q, m->nc, s), "ncclRecv");
-          NCCLCHK(rccl().Recv(m->stage_r.p + o, size_t(hi - lo), ncclInt32, q, m->nc, s), "ncclRecv");
+          rc2 = nccl_check(rccl().Recv(m->stage_t.p + o, size_t(hi - lo), ncclInt64, q, m->nc, s), "ncclRecv");
+          if (!rc2) rc2 = nccl_check(rccl().Recv(m->stage_r.p + o, size_t(hi - lo), ncclInt32, q, m->nc, s), "ncclRecv");
         }
         o += hi - lo;
       }
-    } else {
+    } else if (!rc2) {
       int64_t lo, hi;
-      piece(me, &lo, &hi);
+      piece(ch, me, &lo, &hi);
       if (hi > lo) {
-        NCCLCHK(rccl().Send(c->node_time.p + lo, size_t(hi - lo), ncclInt64, root, m->nc, s), "ncclSend");
-        NCCLCHK(rccl().Send(c->node_rule.p + lo, size_t(hi - lo), ncclInt32, root, m->nc, s), "ncclSend");
+        rc2 = nccl_check(rccl().Send(c->node_time.p + lo, size_t(hi - lo), ncclInt64, root, m->nc, s), "ncclSend");
+        if (!rc2) rc2 = nccl_check(rccl().Send(c->node_rule.p + lo, size_t(hi - lo), ncclInt32, root, m->nc, s), "ncclSend");
       }
     }
-    NCCLCHK(rccl().GroupEnd(), "ncclGroupEnd");
-    if (me != root) continue;
+    const int rc3 = nccl_check(rccl().GroupEnd(), "ncclGroupEnd");  // always closes the group
+    if (rc2 || rc3) {
+      post = rc2 ? rc2 : rc3;
+      abort_comm(m);
+      break;
+    }
+    if (me != root || post) continue;
     // place the chunk (same stream: after the receives, before the next chunk's)
     int64_t o = 0;
-    for (int q = 0; q < W; q++) {
+    for (int q = 0; q < W && !post; q++) {
       if (q == root) continue;
       int64_t lo, hi;
-      piece(q, &lo, &hi);
+      piece(ch, q, &lo, &hi);
       const int32_t add = int32_t(meta[size_t(kMeta * q + 3)]);
       if (hi > lo) {
-        if (ch.k == 1) {
-          // src indexed by the peer's own positions: shift the stage base by lo
-          rc = launch_node_place(c, s, int32_t(ch.n1 - ch.n0), m->off_all.p + int64_t(q) * (N + 1) + ch.n0,
-                                 m->stage_t.p + o - lo, m->stage_r.p + o - lo, add,
-                                 m->starts.p + int64_t(q) * N + ch.n0, d_time, d_rule);
-        } else {
+        if (ch.k == 1)  // peer positions [lo, hi) staged at stage[o ..]
+          post = launch_node_place(c, s, int32_t(ch.n1 - ch.n0), m->off_all.p + int64_t(q) * (N + 1) + ch.n0, lo - o,
+                                   m->stage_t.p, m->stage_r.p, add, m->starts.p + int64_t(q) * N + ch.n0, d_time,
+                                   d_rule);
+        else {
           const int64_t dst = st[size_t(q * N + ch.n0)] + (lo - off[size_t(q * (N + 1) + ch.n0)]);
-          rc = launch_span_place(c, s, hi - lo, m->stage_t.p + o, m->stage_r.p + o, add, d_time + dst, d_rule + dst);
+          post = launch_span_place(c, s, hi - lo, m->stage_t.p + o, m->stage_r.p + o, add, d_time + dst, d_rule + dst);
         }
-        if (rc) return rc;
       }
       o += hi - lo;
     }
+  }
+  if (post) {
+    (void)hipStreamSynchronize(s);
+    return post;
+  }
+  if (me == root && timed && W > 1 && N > 0) {
+    // every node's slices are in (time, rule) order: merge them in place
+    std::vector<int64_t> rb(size_t(N) * (W + 1));
+    for (int64_t n = 0; n < N; n++) {
+      for (int q = 0; q < W; q++) rb[size_t(n * (W + 1) + q)] = st[size_t(q * N + n)];
+      rb[size_t(n * (W + 1) + W)] = base[size_t(n + 1)];
+    }
+    return merge_ranks_locked(c, s, int32_t(N), W, rb.data(), d_time, d_rule, int64_t(m->stage_t.cap), m->stage_t,
+                              m->stage_r);
   }
   return cg_hip_check(hipStreamSynchronize(s), "gather sync");
 }

@@ -1446,7 +1446,11 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
     c->kt[12] = 0.f;
     return CG_OK;
   }
-  return order_by_time_locked(c);
+  if ((rc = order_by_time_locked(c))) {  // a failed pass may leave the lists half permuted
+    c->pn_E = 0;
+    c->pn_valid = false;
+  }
+  return rc;
 }
 
 #ifndef CG_OT_PIN

@@ -706,15 +706,17 @@ __global__ __launch_bounds__(256) void k_node_write(
 
 // One rank's per-node slice placed into the gathered per-node CSR
 // (cg_node_csr_place): node n's events [src_off[n], src_off[n+1]) go to
-// dst_start[n] onwards, rules shifted to global indices.  One block per node
-// (grid-stride over nodes), four loads in flight per thread.
-__global__ __launch_bounds__(256) void k_node_place(const int64_t* __restrict__ src_off, int32_t N,
+// dst_start[n] onwards, rules shifted to global indices.  Event i of src_off's
+// numbering is src[i - src_shift] (a gather chunk staged from position
+// src_shift of the peer's CSR).  One block per node (grid-stride over nodes),
+// four loads in flight per thread.
+__global__ __launch_bounds__(256) void k_node_place(const int64_t* __restrict__ src_off, int32_t N, int64_t src_shift,
                                                      const int64_t* __restrict__ src_time,
                                                      const int32_t* __restrict__ src_rule, int32_t rule_add,
                                                      const int64_t* __restrict__ dst_start,
                                                      int64_t* __restrict__ dst_time, int32_t* __restrict__ dst_rule) {
   for (int64_t n = blockIdx.x; n < N; n += gridDim.x) {
-    const int64_t a = src_off[n], b = src_off[n + 1], d = dst_start[n] - a;
+    const int64_t a = src_off[n] - src_shift, b = src_off[n + 1] - src_shift, d = dst_start[n] - a;
     int64_t i = a + threadIdx.x;
     for (; i + 768 < b; i += 1024) {
       int64_t t[4];
@@ -745,6 +747,89 @@ __global__ __launch_bounds__(256) void k_span_place(int64_t n, const int64_t* __
   for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
     dst_time[i] = src_time[i];
     dst_rule[i] = src_rule[i] + rule_add;
+  }
+}
+
+// Time-ordered gather (cg_node_csr_merge_ranks, cg_comm_gather_node_csr on
+// time-ordered results).  A node's gathered list holds the ranks' slices in
+// rank (= job-ID) order, each already in (time, rule) order, and every rule of
+// rank g precedes every rule of rank g+1.  So an event's place in the node's
+// byTime list (cron.go:64-79,220; ties by rule) is its index in its own run
+// plus, for every other run q, the events of q before it: those with time <= t
+// when q < g (smaller rules), time < t when q > g.  One block per tile of
+// kMrTile events of one run: the tile's first and last times bound each other
+// run's searches to a window (found once per block), then every event
+// binary-searches the windows.  Reads a copy of the node group (src, index =
+// position - src_base), writes the merged lists in place.
+constexpr int kMrTile = 1024;
+
+template <bool LE>
+__device__ __forceinline__ int64_t mr_bound(const int64_t* __restrict__ t, int64_t lo, int64_t hi, int64_t v) {
+  // the first index in [lo, hi) whose time is > v (LE) or >= v
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    const int64_t x = t[mid];
+    if (LE ? x <= v : x < v)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(256) void k_merge_ranks(const int64_t* __restrict__ rb, const int64_t* __restrict__ tp,
+                                                      int64_t n_runs, int32_t W, int64_t tile0,
+                                                      const int64_t* __restrict__ src_t,
+                                                      const int32_t* __restrict__ src_r, int64_t src_base,
+                                                      int64_t* __restrict__ dst_t, int32_t* __restrict__ dst_r) {
+  __shared__ int64_t s_lo[kMergeMaxRanks], s_hi[kMergeMaxRanks];
+  __shared__ int64_t s_run;
+  const int64_t b = tile0 + blockIdx.x;
+  if (threadIdx.x == 0) {
+    // the run holding tile b: the last r with tp[r] <= b (runs without tiles
+    // share their successor's prefix)
+    int64_t lo = 0, hi = n_runs;
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (tp[mid] <= b)
+        lo = mid;
+      else
+        hi = mid;
+    }
+    s_run = lo;
+  }
+  __syncthreads();
+  const int64_t r = s_run;
+  const int64_t n = r / W;
+  const int g = int(r - n * W);
+  const int64_t* nb = rb + n * (W + 1);
+  const int64_t a = nb[g] - src_base, len = nb[g + 1] - nb[g];
+  const int64_t i0 = (b - tp[r]) * kMrTile;
+  const int64_t i1 = i0 + kMrTile < len ? i0 + kMrTile : len;
+  const int64_t tmin = src_t[a + i0], tmax = src_t[a + i1 - 1];
+  for (int q = threadIdx.x; q < W; q += blockDim.x) {
+    if (q == g) continue;
+    const int64_t qa = nb[q] - src_base, qb = nb[q + 1] - src_base;
+    if (q < g) {
+      s_lo[q] = mr_bound<true>(src_t, qa, qb, tmin);
+      s_hi[q] = mr_bound<true>(src_t, s_lo[q], qb, tmax);
+    } else {
+      s_lo[q] = mr_bound<false>(src_t, qa, qb, tmin);
+      s_hi[q] = mr_bound<false>(src_t, s_lo[q], qb, tmax);
+    }
+  }
+  __syncthreads();
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int64_t tv = src_t[a + i];
+    const int32_t rv = src_r[a + i];
+    int64_t pos = nb[0] + i;
+    for (int q = 0; q < W; q++) {
+      if (q == g) continue;
+      const int64_t k = q < g ? mr_bound<true>(src_t, s_lo[q], s_hi[q], tv) : mr_bound<false>(src_t, s_lo[q], s_hi[q], tv);
+      pos += k - (nb[q] - src_base);
+    }
+    dst_t[pos] = tv;
+    dst_r[pos] = rv;
   }
 }
 
@@ -1026,6 +1111,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   hipStream_t st = c->st;
   const bool cached = in.serial != 0 && in.serial == c->pn_cache_serial && mode == c->pn_cache_mode;
   c->pn_E = 0;  // no readable result until this call succeeds
+  c->pn_valid = false;
   c->pn_time_ordered = false;
   c->pn_R = R;
   (void)hipEventRecord(c->pev[0], st);
@@ -1164,6 +1250,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   (void)hipEventElapsedTime(&c->kt[7], c->pev[1], c->pev[2]);
   (void)hipEventElapsedTime(&c->kt[8], c->pev[2], c->pev[3]);
   c->pn_E = En;
+  c->pn_valid = true;
   c->pn_nnz = nnz;
   c->pn_N = N;
   c->pn_t0 = t0;
@@ -1175,6 +1262,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   if (fused) {  // written in (time, rule) order
     if (c->pn_res_host[2]) {
       c->pn_E = 0;
+      c->pn_valid = false;
       *n_events = 0;
       return cg_fail(CG_EHIP, kOrderCheckMsg);
     }
@@ -1188,6 +1276,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   if (c->node_order == CG_NODE_ORDER_TIME) {
     if ((rc = order_by_time_locked(c, in_mode))) {
       c->pn_E = 0;
+      c->pn_valid = false;
       *n_events = 0;
     }
     return rc;
@@ -1419,6 +1508,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
   c->pa_next = (k + 1) % cg_ctx::kPnSets;
   c->pa_last = k;
   c->pn_E = 0;  // nothing readable until cg_expand_per_node_wait
+  c->pn_valid = false;
   return CG_OK;
 }
 
@@ -1445,6 +1535,7 @@ int cg_expand_per_node_wait(cg_ctx* c, int64_t* n_events, int64_t* n_events_all)
       HIPCHK(hipMemcpyAsync(c->node_off.p, a.node_off.p, (int64_t(a.N) + 1) * 8, hipMemcpyDeviceToDevice, c->st));
       HIPCHK(hipStreamSynchronize(c->st));
       c->pn_E = En;
+      c->pn_valid = true;
       c->pn_time_ordered = a.timed;
       c->pn_N = a.N;
       c->pn_t0 = a.t0;
@@ -1635,7 +1726,7 @@ int cg_node_csr_place(cg_ctx* c, int32_t n_nodes, const int64_t* d_src_node_off,
   if (rc) return rc;
   if (n_nodes > 0)
     hipLaunchKernelGGL(k_node_place, dim3(unsigned(std::min<int64_t>(n_nodes, int64_t(c->write_blocks) * 2))),
-                       dim3(256), 0, c->st, d_src_node_off, n_nodes, d_src_time, d_src_rule, rule_add, d_dst_start,
+                       dim3(256), 0, c->st, d_src_node_off, n_nodes, int64_t(0), d_src_time, d_src_rule, rule_add, d_dst_start,
                        d_dst_time, d_dst_rule);
   if ((rc = cg_hip_check(hipGetLastError(), "k_node_place"))) return rc;
   return cg_hip_check(hipStreamSynchronize(c->st), "sync");
@@ -1644,12 +1735,12 @@ int cg_node_csr_place(cg_ctx* c, int32_t n_nodes, const int64_t* d_src_node_off,
 }  // extern "C"
 
 // placement launchers for the RCCL gather (cg_comm.cpp); enqueued on st
-int launch_node_place(cg_ctx* c, hipStream_t st, int32_t N, const int64_t* src_off, const int64_t* src_time,
-                      const int32_t* src_rule, int32_t rule_add, const int64_t* dst_start, int64_t* dst_time,
-                      int32_t* dst_rule) {
+int launch_node_place(cg_ctx* c, hipStream_t st, int32_t N, const int64_t* src_off, int64_t src_shift,
+                      const int64_t* src_time, const int32_t* src_rule, int32_t rule_add, const int64_t* dst_start,
+                      int64_t* dst_time, int32_t* dst_rule) {
   if (N > 0)
     hipLaunchKernelGGL(k_node_place, dim3(unsigned(std::min<int64_t>(N, int64_t(c->write_blocks) * 2))), dim3(256),
-                       0, st, src_off, N, src_time, src_rule, rule_add, dst_start, dst_time, dst_rule);
+                       0, st, src_off, N, src_shift, src_time, src_rule, rule_add, dst_start, dst_time, dst_rule);
   return cg_hip_check(hipGetLastError(), "k_node_place");
 }
 
@@ -1668,7 +1759,72 @@ int launch_node_counts(cg_ctx* c, hipStream_t st, int64_t* d_counts) {
   return cg_hip_check(hipGetLastError(), "k_node_counts");
 }
 
+int merge_ranks_locked(cg_ctx* c, hipStream_t st, int32_t N, int32_t W, const int64_t* h_rb, int64_t* d_time,
+                       int32_t* d_rule, int64_t scratch_ev, DBuf<int64_t>& scr_t, DBuf<int32_t>& scr_r) {
+  if (W <= 1 || N <= 0) return CG_OK;
+  if (W > kMergeMaxRanks) return cg_fail(CG_EINVAL, "time-ordered gather: more than 64 ranks");
+  const int64_t NW = int64_t(N) * W;
+  // tiles per run; a node with fewer than two non-empty runs is already merged
+  std::vector<int64_t> tp(size_t(NW + 1), 0);
+  int64_t big = 0;  // the largest node that needs a merge
+  for (int64_t n = 0; n < N; n++) {
+    const int64_t* nb = h_rb + n * (W + 1);
+    int nonempty = 0;
+    for (int q = 0; q < W; q++) {
+      if (nb[q + 1] < nb[q]) return cg_fail(CG_EINVAL, "time-ordered gather: run bounds not ascending");
+      nonempty += nb[q + 1] > nb[q];
+    }
+    if (n > 0 && nb[0] < h_rb[(n - 1) * (W + 1) + W])
+      return cg_fail(CG_EINVAL, "time-ordered gather: node lists overlap");
+    for (int q = 0; q < W; q++)
+      tp[size_t(n * W + q + 1)] = tp[size_t(n * W + q)] + (nonempty >= 2 ? (nb[q + 1] - nb[q] + kMrTile - 1) / kMrTile : 0);
+    if (nonempty >= 2) big = std::max(big, nb[W] - nb[0]);
+  }
+  if (tp[size_t(NW)] == 0) return CG_OK;
+  scratch_ev = std::max(scratch_ev, big);
+  int rc;
+  if ((rc = c->mr_rb.ensure(size_t(N) * (W + 1))) || (rc = c->mr_tp.ensure(size_t(NW + 1))) ||
+      (rc = scr_t.ensure(size_t(scratch_ev))) || (rc = scr_r.ensure(size_t(scratch_ev))))
+    return rc;
+  HIPCHK(hipMemcpyAsync(c->mr_rb.p, h_rb, size_t(N) * (W + 1) * 8, hipMemcpyHostToDevice, st));
+  HIPCHK(hipMemcpyAsync(c->mr_tp.p, tp.data(), tp.size() * 8, hipMemcpyHostToDevice, st));
+  // node groups of at most scratch_ev events; every group: a copy of its
+  // lists, then the tiles of its runs merge from the copy into place
+  int64_t n0 = 0;
+  while (n0 < N) {
+    const int64_t base = h_rb[n0 * (W + 1)];
+    int64_t n1 = n0 + 1;
+    while (n1 < N && h_rb[n1 * (W + 1) + W] - base <= scratch_ev) n1++;
+    const int64_t t0 = tp[size_t(n0 * W)], t1 = tp[size_t(n1 * W)];
+    if (t1 > t0) {
+      const int64_t ev = h_rb[(n1 - 1) * (W + 1) + W] - base;
+      HIPCHK(hipMemcpyAsync(scr_t.p, d_time + base, size_t(ev) * 8, hipMemcpyDeviceToDevice, st));
+      HIPCHK(hipMemcpyAsync(scr_r.p, d_rule + base, size_t(ev) * 4, hipMemcpyDeviceToDevice, st));
+      for (int64_t tb = t0; tb < t1; tb += int64_t(1) << 30) {
+        const int64_t nt = std::min<int64_t>(t1 - tb, int64_t(1) << 30);
+        hipLaunchKernelGGL(k_merge_ranks, dim3(unsigned(nt)), dim3(256), 0, st, c->mr_rb.p, c->mr_tp.p, NW, W, tb,
+                           scr_t.p, scr_r.p, base, d_time, d_rule);
+      }
+      HIPCHK(hipGetLastError());
+    }
+    n0 = n1;
+  }
+  // the host arrays above are read by the queued copies: drain before they go
+  return cg_hip_check(hipStreamSynchronize(st), "time-ordered gather merge");
+}
+
 extern "C" {
+
+int cg_node_csr_merge_ranks(cg_ctx* c, int32_t n_nodes, int32_t world, const int64_t* run_bounds, int64_t* d_time,
+                            int32_t* d_rule, int64_t budget_bytes) {
+  if (!c || n_nodes < 0 || world < 1 || budget_bytes < 12 || (n_nodes > 0 && world > 1 && (!run_bounds || !d_time || !d_rule)))
+    return cg_fail(CG_EINVAL, "cg_node_csr_merge_ranks: bad argument");
+  std::lock_guard<std::mutex> g(c->mu);
+  (void)hipGetLastError();
+  HIPCHK(hipSetDevice(c->device));
+  return merge_ranks_locked(c, c->st, n_nodes, world, run_bounds, d_time, d_rule, budget_bytes / 12, c->mr_t,
+                            c->mr_r);
+}
 
 int cg_node_checksum_enqueue(cg_ctx* c, const int32_t* d_nodes, int32_t k, uint64_t* d_out) {
   if (!c || k < 0 || (k > 0 && (!d_nodes || !d_out))) return cg_fail(CG_EINVAL, "cg_node_checksum_enqueue: bad argument");

@@ -77,7 +77,6 @@ class Comm:
 
     @staticmethod
     def unique_id():
-        _lib.preload_torch_rccl()
         buf = (C.c_uint8 * 128)()
         check(lib().cg_comm_unique_id(buf))
         return bytes(buf)
@@ -86,7 +85,6 @@ class Comm:
         if len(uid) != 128:
             raise ValueError("RCCL unique id must be 128 bytes")
         self.engine, self.world, self.rank = engine, int(world), int(rank)
-        _lib.preload_torch_rccl()
         h = C.c_void_p()
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         check(lib().cg_comm_init(engine._h, self.world, self.rank, buf, C.byref(h)))
@@ -574,6 +572,18 @@ class Engine:
                                       C.c_void_p(src_rule), int(rule_add), C.c_void_p(dst_start),
                                       C.c_void_p(dst_time), C.c_void_p(dst_rule)))
 
+    def node_csr_merge_ranks(self, n_nodes, world, run_bounds, d_time, d_rule, budget_bytes=1 << 31):
+        """Merge every node's rank slices of a gathered per-node CSR into
+        (time, rule) order in place (cg_node_csr_merge_ranks): run_bounds
+        [n_nodes, world + 1] (host int64; run g of node n is [rb[n, g],
+        rb[n, g + 1])), each run already in (time, rule) order; d_time /
+        d_rule device pointers on this engine's device."""
+        rb = np.ascontiguousarray(run_bounds, dtype=np.int64)
+        if rb.size != n_nodes * (world + 1):
+            raise ValueError("run_bounds must hold n_nodes * (world + 1) positions")
+        check(lib().cg_node_csr_merge_ranks(self._h, int(n_nodes), int(world), rb.ctypes.data, C.c_void_p(d_time),
+                                            C.c_void_p(d_rule), int(budget_bytes)))
+
     def node_counts_to_device(self, d_ptr):
         check(lib().cg_node_counts_to_device(self._h, C.c_void_p(d_ptr)))
 
@@ -617,8 +627,28 @@ def default_engine():
         return _default
 
 
+def comm_gather_plan(counts, root, budget_bytes):
+    """The library's chunk plan of the per-node CSR gather
+    (cg_comm_gather_plan; host only): counts [world, N] per-node event counts
+    of every rank.  Returns [(n0, n1, j, k)], as shard.node_gather_plan."""
+    cnt = np.ascontiguousarray(counts, dtype=np.int64)
+    world, N = cnt.shape
+    n = C.c_int64()
+    cap = max(1, 2 * N + 16)
+    while True:
+        out = np.zeros((cap, 4), dtype=np.int64)
+        rc = lib().cg_comm_gather_plan(cnt.ctypes.data, world, N, int(root), int(budget_bytes), out.ctypes.data,
+                                       cap, C.byref(n))
+        if rc == _lib.CG_ECAPACITY:
+            cap = int(n.value)
+            continue
+        check(rc)
+        return [tuple(int(x) for x in row) for row in out[:n.value]]
+
+
 def device_count():
     return lib().cg_device_count()
 
 
-__all__ = ["Engine", "Specs", "Dispatcher", "RulesIn", "Comm", "default_engine", "device_count", "CgError"]
+__all__ = ["Engine", "Specs", "Dispatcher", "RulesIn", "Comm", "default_engine", "device_count", "CgError",
+           "comm_gather_plan"]

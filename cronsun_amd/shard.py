@@ -20,7 +20,9 @@ with no data-path collective.  The only exchanges are small:
   gather_node_csr  the same for the per-node CSR (north_star's "gather the
                    final per-node CSR"): every node's global list is the
                    ranks' slices of it in job-ID order, as one process walking
-                   all jobs builds it (node/node.go:121-158 -> Job.Cmds); in
+                   all jobs builds it (node/node.go:121-158 -> Job.Cmds), or
+                   for time-ordered lists those slices merged by (time, rule)
+                   (merge_rank_runs; the node's byTime order); in
                    chunks of node ranges under a byte budget, so the
                    destination stages at most the budget beside its output
                    (the library's cg_comm_gather_node_csr does the same over
@@ -250,15 +252,50 @@ def _piece(off_g, cnt_g, chunk):
 DEFAULT_GATHER_BUDGET = 1 << 31  # bytes of peer events staged on dst per chunk
 
 
+def merge_rank_runs(run_bounds, out_time, out_rule, engine=None, budget_bytes=DEFAULT_GATHER_BUDGET):
+    """Merge every node's rank slices of a gathered per-node CSR into (time,
+    rule) order, in place (the byTime order of the node's Cron,
+    cron.go:64-79,220, over every job).  run_bounds: numpy int64 [N, world+1],
+    run g of node n = [rb[n, g], rb[n, g+1]), each run already in (time, rule)
+    order and rank g's rules below rank g+1's, so a stable sort by time per
+    node is the (time, rule) order.  Device tensors go through the library
+    (cg_node_csr_merge_ranks), host tensors through numpy."""
+    import torch
+    rb = np.asarray(run_bounds, dtype=np.int64)
+    N, w1 = rb.shape
+    if w1 <= 2 or N == 0:
+        return
+    if out_time.is_cuda:
+        if engine is None:
+            if (out_time.device.index or 0) != 0:
+                raise ValueError("merge_rank_runs: pass the Engine of the tensors' device")
+            from .engine import default_engine
+            engine = default_engine()
+        torch.cuda.synchronize(out_time.device)  # the library runs on its own stream
+        engine.node_csr_merge_ranks(N, w1 - 1, rb, out_time.data_ptr(), out_rule.data_ptr(), budget_bytes)
+        return
+    t, r = out_time.numpy(), out_rule.numpy()
+    for n in range(N):
+        a, b = int(rb[n, 0]), int(rb[n, -1])
+        if b - a > 1:
+            o = np.argsort(t[a:b], kind="stable")
+            t[a:b], r[a:b] = t[a:b][o], r[a:b][o]
+
+
 def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst=0, engine=None,
-                    budget_bytes=DEFAULT_GATHER_BUDGET):
+                    budget_bytes=DEFAULT_GATHER_BUDGET, *, order):
     """Gather the per-node (time, rule) CSR of job-ID-range shards on rank `dst`.
 
     local_node_off: int64 tensor [N+1] (this rank's node offsets, from 0);
     local_time int64 [E_g] and local_rule int32 [E_g] (rule indices local to
     the rank's range, which starts at global rule `rule_base`), all on the
-    collective's device.  Returns (node_off [N+1], time [E], rule [E], global
-    rule indices) on `dst`, None elsewhere.
+    collective's device.  `order` (required) is the order of every rank's
+    lists: "rule" (rule-major, the default per-node order: the gathered list
+    is the ranks' slices in job-ID order) or "time" ((time, rule) order,
+    cg_set_node_order(TIME): the slices are then merged per node by (time,
+    global rule) -- concatenating them would not be in time order).  Returns
+    (node_off [N+1], time [E], rule [E], global rule indices) on `dst`, None
+    elsewhere.
 
     Sizes: one all-gather of the per-node counts (N int64 per rank, the
     collective node_offsets uses).  Payload: in chunks of node ranges
@@ -270,6 +307,8 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
     (cg_node_csr_place; rule indices made global there).  dst's own slice is
     placed straight from its buffers."""
     import torch
+    if order not in ("rule", "time"):
+        raise ValueError(f"gather_node_csr: order must be 'rule' or 'time', not {order!r}")
     world, rank = dist.get_world_size(), dist.get_rank()
     dev = local_time.device
     N = local_node_off.numel() - 1
@@ -333,4 +372,10 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
                 out_time[d:d + hi - lo] = stage_t[o:o + hi - lo]
                 out_rule[d:d + hi - lo] = stage_r[o:o + hi - lo] + int(bases[g])
             o += hi - lo
+    if order == "time" and world > 1:
+        rb = np.empty((N, world + 1), dtype=np.int64)
+        for g in range(world):
+            rb[:, g] = starts_h[g]
+        rb[:, world] = node_base.cpu().numpy()[1:]
+        merge_rank_runs(rb, out_time, out_rule, engine, budget_bytes)
     return node_base, out_time, out_rule

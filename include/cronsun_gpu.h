@@ -29,8 +29,10 @@
 extern "C" {
 #endif
 
-/* 2: cg_rules_in.rule_key (Job.Cmds' Job.ID+Rule.ID map key) */
-#define CG_ABI_VERSION 2
+/* 2: cg_rules_in.rule_key (Job.Cmds' Job.ID+Rule.ID map key)
+ * 3: time-ordered per-node gather (cg_comm_gather_node_csr on time-ordered
+ *    results, cg_node_csr_merge_ranks), cg_comm_gather_plan */
+#define CG_ABI_VERSION 3
 
 #define CG_OK 0
 #define CG_EINVAL (-1)    /* bad argument */
@@ -456,6 +458,19 @@ int cg_node_counts_to_device(cg_ctx* ctx, int64_t* d_counts);
 int cg_node_csr_place(cg_ctx* ctx, int32_t n_nodes, const int64_t* d_src_node_off, const int64_t* d_src_time,
                       const int32_t* d_src_rule, int32_t rule_add, const int64_t* d_dst_start,
                       int64_t* d_dst_time, int32_t* d_dst_rule);
+/* Multi-GPU per-node gather, merge step for TIME-ORDERED slices (the byTime
+ * order every node's Cron keeps, node/cron/cron.go:64-79,220): after each
+ * rank's (time, rule)-ordered slice has been placed (cg_node_csr_place), node
+ * n's list in d_time / d_rule holds `world` runs in rank (= job-ID) order, run
+ * g = [run_bounds[n*(world+1)+g], run_bounds[n*(world+1)+g+1]) (HOST array of
+ * n_nodes*(world+1) positions, ascending).  Every node's runs are merged in
+ * place into (time, rule) order -- equal times by global rule index, which
+ * for job-ID-range shards is rank order -- the list one scheduler over all
+ * jobs would hold.  Works through a scratch copy of node groups of at most
+ * budget_bytes / 12 events (a larger node alone); world <= 64.  Returns after
+ * the merge (stream synchronised). */
+int cg_node_csr_merge_ranks(cg_ctx* ctx, int32_t n_nodes, int32_t world, const int64_t* run_bounds,
+                            int64_t* d_time, int32_t* d_rule, int64_t budget_bytes);
 
 /* Device-resident rule sets: a cg_rules_in validated and copied into HBM once
  * (as specs are by cg_specs_upload), then used by any number of per-node
@@ -497,8 +512,7 @@ int cg_expand_per_node_wait(cg_ctx* ctx, int64_t* n_events, int64_t* n_events_al
  * node filters every job itself, node/node.go:121-141; here a rank evaluates
  * one range of jobs for every node).  The only exchanges (north_star) are the
  * all-gather of per-node event counts / offsets and the gather of the final
- * per-node CSR.  RCCL is loaded at run time (librccl.so.1 beside the HIP
- * runtime the library links, else /opt/rocm/lib); CG_ENODEV if absent.
+ * per-node CSR.  RCCL is loaded at run time (see below); CG_ENODEV if absent.
  *
  *   cg_comm_unique_id   ncclGetUniqueId: rank 0 makes the id, the caller
  *                       hands it to every rank (any channel)
@@ -513,23 +527,45 @@ int cg_expand_per_node_wait(cg_ctx* ctx, int64_t* n_events, int64_t* n_events_al
  *                       node n lands in the job-ID-ordered global list),
  *                       node_base[N+1] the global node offsets (host; either
  *                       may be NULL)
- *   cg_comm_gather_node_csr  every rank's last per-node result (rule order)
- *                       gathered on `root` into the caller's DEVICE buffers
+ *   cg_comm_gather_node_csr  every rank's last per-node result gathered on
+ *                       `root` into the caller's DEVICE buffers
  *                       d_node_off [N+1], d_time / d_rule [cap] (root only;
  *                       ignored elsewhere): node n's global list is the ranks'
  *                       slices in rank (= job-ID) order, rule indices made
  *                       global by each rank's rule_base (its range's first
- *                       global rule).  The payload moves in chunks of whole
+ *                       global rule).  When every rank's result is in (time,
+ *                       rule) order (CG_NODE_ORDER_TIME), root merges each
+ *                       node's slices into one (time, rule)-ordered list
+ *                       (cg_node_csr_merge_ranks), the byTime list of one
+ *                       scheduler over every job; ranks mixing the two orders
+ *                       are refused.  The payload moves in chunks of whole
  *                       node ranges (a node larger than the budget in parts)
  *                       whose peer bytes (12 B per event) stay within
  *                       budget_bytes (the smallest any rank passes; at least
  *                       24 B per rank), so root's staging is bounded by it;
  *                       grouped ncclSend/ncclRecv per chunk, placed on root by
- *                       a kernel.  Every rank returns the same status:
- *                       CG_ECAPACITY when the total exceeds root's cap,
- *                       CG_EINVAL when a rank's result is time-ordered or the
- *                       node counts differ.  *n_events = the global total.
- * Collective calls must be made by every rank of the comm, in the same order. */
+ *                       a kernel (root's staging, also the merge's scratch:
+ *                       at most the budget, or the largest node when a time-
+ *                       ordered node exceeds it).  Every rank returns the same
+ *                       status: CG_ECAPACITY when the total exceeds root's
+ *                       cap, CG_EINVAL when a rank has no readable result, the
+ *                       node counts or list orders differ, and root's
+ *                       allocation failure on every rank.  A transfer that
+ *                       fails after all ranks agreed aborts the communicator
+ *                       (later calls fail with CG_EHIP).  *n_events = the
+ *                       global total.
+ *   cg_comm_gather_plan the gather's chunk plan, host only (no device, no
+ *                       communicator): counts [world * n_nodes] per-node event
+ *                       counts of every rank; chunks[4i..4i+3] = {n0, n1, j,
+ *                       k}: nodes [n0, n1) whole (k == 1), or part j of k of
+ *                       node n0, rank g's part being its events [c*j/k,
+ *                       c*(j+1)/k) of that node.  *n_chunks always set;
+ *                       CG_ECAPACITY when it exceeds cap.
+ * Collective calls must be made by every rank of the comm, in the same order.
+ * RCCL is loaded by full path with local symbol scope, one copy per process:
+ * one already mapped, else the librccl.so beside the HIP runtime the library
+ * runs on, else /opt/rocm/lib; when a different RCCL is mapped later the
+ * cg_comm calls fail with CG_EINVAL naming both. */
 typedef struct cg_comm cg_comm;
 #define CG_COMM_ID_BYTES 128
 int cg_comm_unique_id(uint8_t id[CG_COMM_ID_BYTES]);
@@ -540,6 +576,8 @@ int cg_comm_node_offsets(cg_comm* comm, int64_t* node_start, int64_t* node_base)
 int cg_comm_gather_node_csr(cg_comm* comm, int root, int64_t rule_base, int64_t budget_bytes,
                             int64_t* d_node_off, int64_t* d_time, int32_t* d_rule, int64_t cap,
                             int64_t* n_events);
+int cg_comm_gather_plan(const int64_t* counts, int32_t world, int32_t n_nodes, int32_t root,
+                        int64_t budget_bytes, int64_t* chunks, int64_t cap, int64_t* n_chunks);
 
 /* rule -> node CSR only (GPU join), host output */
 int cg_rule_nodes(cg_ctx* ctx, const cg_rules_in* rules, int mode, int64_t* rn_off /*[R+1]*/,

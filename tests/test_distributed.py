@@ -159,7 +159,7 @@ def _node_csr_oracle(rin, mode, specs, t0, t1):
             np.concatenate(rs).astype(np.int32))
 
 
-def _gather_worker(rank, world, port, outdir, mode, budget):
+def _gather_worker(rank, world, port, outdir, mode, budget, order="rule"):
     import torch
     import torch.distributed as dist
     from cronsun_amd import synth
@@ -175,8 +175,10 @@ def _gather_worker(rank, world, port, outdir, mode, budget):
     lo, hi = cuts[rank], cuts[rank + 1]
     part = rin.slice_rules(lo, hi)
     off, t, r = _node_csr_oracle(part, mode, specs[lo:hi], T0, T0 + DAY)
+    if order == "time":  # this rank's lists in (time, rule) order, as cg_set_node_order(TIME) leaves them
+        t, r = _time_order(off, t, r)
     g = shard.gather_node_csr(torch.from_numpy(off), torch.from_numpy(t), torch.from_numpy(r), lo, dist,
-                              budget_bytes=budget)
+                              budget_bytes=budget, order=order)
     cnt = torch.from_numpy(np.diff(off))
     allc = torch.zeros(world * rin.n_nodes, dtype=torch.int64)
     dist.all_gather_into_tensor(allc, cnt)
@@ -186,6 +188,16 @@ def _gather_worker(rank, world, port, outdir, mode, budget):
                  rule=g[2].numpy(), plan=np.array(plan, dtype=np.int64).reshape(-1, 4))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def _time_order(node_off, t, r):
+    """Every node's list of a rule-major per-node CSR in (time, rule) order."""
+    t, r = t.copy(), r.copy()
+    for n in range(len(node_off) - 1):
+        a, b = int(node_off[n]), int(node_off[n + 1])
+        o = np.lexsort((r[a:b], t[a:b]))
+        t[a:b], r[a:b] = t[a:b][o], r[a:b][o]
+    return t, r
 
 
 @pytest.mark.parametrize("mode,budget", [(0, shard.DEFAULT_GATHER_BUDGET), (2, shard.DEFAULT_GATHER_BUDGET),
@@ -241,3 +253,54 @@ def test_node_gather_plan_covers_every_event_within_budget(world, dst):
                 tot += hi - lo
             assert 0 < tot * 12 <= budget, (budget, ch)
         assert all(nxt[g] == offs[g, -1] for g in range(world) if g != dst)
+
+
+@pytest.mark.parametrize("world,budget", [(3, shard.DEFAULT_GATHER_BUDGET), (3, 12 * 700), (2, 12 * 3000)])
+def test_gather_node_csr_time_ordered_gloo(tmp_path, world, budget):
+    """Time-ordered per-node lists at N > 1 (the byTime order of every node's
+    Cron, cron.go:64-79,220): each rank's lists in (time, rule) order, gathered
+    on rank 0 and merged per node by (time, global rule) -- equal to the
+    unsharded lists in (time, rule) order.  Concatenating the ranks' slices
+    (order="rule") would not be."""
+    import torch.multiprocessing as mp
+    from cronsun_amd import synth
+    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path), 0, budget, "time"), nprocs=world, join=True)
+    got = np.load(tmp_path / "g0.npz")
+    rin = synth.multi_rule_jobs(160, seed=5, key_choices=2)
+    specs = synth.spec_mix(rin.n_rules, seed=6, mix=synth.MIX_LIGHT)
+    exp_off, exp_t, exp_r = _node_csr_oracle(rin, 0, specs, T0, T0 + DAY)
+    exp_t, exp_r = _time_order(exp_off, exp_t, exp_r)
+    assert np.array_equal(got["node_off"], exp_off)
+    assert np.array_equal(got["time"], exp_t)
+    assert np.array_equal(got["rule"], exp_r)
+
+
+def test_gather_node_csr_requires_order():
+    """The Python gather cannot tell the lists' order: the caller states it."""
+    with pytest.raises(TypeError):
+        shard.gather_node_csr(None, None, None, 0, None)
+    with pytest.raises(ValueError):
+        import torch
+        z = torch.zeros(1, dtype=torch.int64)
+        shard.gather_node_csr(z, z, z.to(torch.int32), 0, None, order="byTime")
+
+
+@pytest.mark.parametrize("world,dst", [(2, 0), (3, 1), (8, 0), (8, 5)])
+def test_library_gather_plan_equals_python(world, dst):
+    """The library's chunk plan (cg_comm_gather_plan: the plan
+    cg_comm_gather_node_csr executes over RCCL) equals shard.node_gather_plan
+    chunk for chunk at worlds 2/3/8, including split nodes and tiny budgets,
+    and rejects a budget below 24 bytes per rank as the Python plan does."""
+    from cronsun_amd import _lib
+    from cronsun_amd.engine import comm_gather_plan
+    rng = np.random.default_rng(100 + world + dst)
+    N = 700
+    allc = rng.integers(0, 40, (world, N))
+    allc[:, rng.integers(0, N, 7)] = rng.integers(500, 3000, (world, 7))
+    allc[:, rng.integers(0, N, 50)] = 0
+    for budget in (12 * 2 * world, 12 * 97, 12 * 1000, 12 * 5000, 12 * 10**9):
+        assert comm_gather_plan(allc, dst, budget) == shard.node_gather_plan(allc, dst, budget), budget
+    with pytest.raises(_lib.CgError):
+        comm_gather_plan(allc, dst, 12 * 2 * world - 12)
+    with pytest.raises(ValueError):
+        shard.node_gather_plan(allc, dst, 12 * 2 * world - 12)

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 def test_library_loads_and_binds_all_symbols():
     from cronsun_amd import _lib
     L = _lib.lib()
-    assert L.cg_abi_version() == _lib.ABI_VERSION == 2
+    assert L.cg_abi_version() == _lib.ABI_VERSION == 3
     assert set(_lib.SYMBOLS) == set(declared())
 
 

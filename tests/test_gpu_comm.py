@@ -6,7 +6,12 @@ gloo tests, tests/test_distributed.py, and run on the driver's 8-GPU node).
 World 1 runs every collective for real: the all-gather of host values, the
 per-node counts all-gather behind cg_comm_node_offsets, and the gather of the
 per-node CSR (root's own slice placed by the kernel into caller buffers),
-plus the status every rank must agree on (capacity, time-ordered input)."""
+plus the status every rank must agree on (capacity, no readable result), a
+time-ordered result gathered in time order, and a clean exit when torch is
+imported after the library loaded RCCL.  The time-ordered merge of several
+ranks' slices is checked on one GPU through cg_node_csr_merge_ranks
+(tests/test_gpu_pernode.py) and the C++ chunk plan against the Python one on
+CPU (tests/test_distributed.py)."""
 import numpy as np
 import pytest
 
@@ -60,12 +65,47 @@ def test_node_offsets_and_gather_world1(world1):
     with pytest.raises(_lib.CgError) as err:
         comm.gather_node_csr(0, 0, 1 << 30, o.data_ptr(), t.data_ptr(), r.data_ptr(), E - 1)
     assert err.value.code == _lib.CG_ECAPACITY
-    # a time-ordered result is refused (its slices would not merge by concatenation)
+    # a time-ordered result is gathered in time order (world 1: nothing to merge)
     eng.set_node_order(_lib.NODE_ORDER_TIME)
     try:
-        eng.expand_per_node(scheds, None, t0, t0 + 3600, rin, _lib.EXCLUDE_NONE)
-        with pytest.raises(_lib.CgError) as err:
-            comm.gather_node_csr(0, 0, 1 << 30, o.data_ptr(), t.data_ptr(), r.data_ptr(), E)
-        assert err.value.code == _lib.CG_EINVAL
+        node_off2, time2, rule2 = eng.expand_per_node(scheds, None, t0, t0 + 3600, rin, _lib.EXCLUDE_NONE)
+        assert np.array_equal(node_off2, node_off)
+        for budget in (24, 1 << 30):
+            t.fill_(-1)
+            torch.cuda.synchronize(dev)
+            assert comm.gather_node_csr(0, 7, budget, o.data_ptr(), t.data_ptr(), r.data_ptr(), E) == E
+            assert np.array_equal(t.cpu().numpy(), time2)
+            assert np.array_equal(r.cpu().numpy(), rule2 + 7)
     finally:
         eng.set_node_order(_lib.NODE_ORDER_RULE)
+
+
+def test_no_per_node_result_refused():
+    """A ctx whose last per-node call failed (or that has none) refuses the
+    gather and the node offsets on every rank (no stale offsets travel)."""
+    from cronsun_amd.engine import Comm, Engine
+    eng = Engine(0)
+    comm = Comm(eng, 1, 0, Comm.unique_id())
+    try:
+        for call in (lambda: comm.node_offsets(4), lambda: comm.gather_node_csr(0, 0, 1 << 20, 0, 0, 0, 0)):
+            with pytest.raises(_lib.CgError) as err:
+                call()
+            assert err.value.code == _lib.CG_EINVAL
+    finally:
+        comm.free()
+        eng.close()
+
+
+def test_comm_then_torch_exits_cleanly():
+    """RCCL loaded by the library first, torch imported afterwards: one RCCL
+    copy in the process and a clean exit (round 4 aborted in the heap check at
+    exit, tools/probe_comm_exit.py)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for mode in ("comm_torch", "torch_comm"):
+        p = subprocess.run([sys.executable, os.path.join(root, "tools", "probe_comm_exit.py"), mode],
+                           capture_output=True, text=True, timeout=150)
+        assert p.returncode == 0, (mode, p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+        assert f"done {mode}" in p.stdout and "rccl copies 1" in p.stdout, (mode, p.stdout[-2000:])

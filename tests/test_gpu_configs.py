@@ -163,7 +163,8 @@ def test_config4_sharded_ranges_stitch_to_unsharded():
         B.close()
 
 
-def test_config3_sharded_ranges_place_to_unsharded(config3):
+@pytest.mark.parametrize("order", ["rule", "time"])
+def test_config3_sharded_ranges_place_to_unsharded(config3, order):
     """North_star's second collective on one GPU: config 3 (1M jobs x 10k
     nodes, 1 h) split into 2/4/8 job-ID ranges, every range's per-node CSR
     computed alone on a second context and placed into the gathered per-node
@@ -172,12 +173,23 @@ def test_config3_sharded_ranges_place_to_unsharded(config3):
     exactly as shard.gather_node_csr does on rank 0 after the RCCL transfers.
     The placed CSR must equal the unsharded one (order-sensitive device
     checksums of times and rules), and a node sample is bit-exact against the
-    oracle (node.go:121-158 -> Job.Cmds over every job, in job-ID order)."""
+    oracle (node.go:121-158 -> Job.Cmds over every job, in job-ID order).
+    order "time": every range's lists in (time, rule) order
+    (cg_set_node_order(TIME), the byTime order of each node's Cron,
+    cron.go:64-79,220), placed and then merged per node by the library
+    (cg_node_csr_merge_ranks, what cg_comm_gather_node_csr runs on root):
+    equal to the unsharded time-ordered lists."""
     import torch
     from cronsun_amd.engine import Engine
     eng, sp, drules, rin, (t0, t1), (eo, et) = config3
     utc = cron.UTC()
-    En, _ = eng.expand_per_node_rules_device(sp, utc, t0, t1, drules, _lib.EXCLUDE_NONE)
+    timed = order == "time"
+    if timed:
+        eng.set_node_order(_lib.NODE_ORDER_TIME)
+    try:
+        En, _ = eng.expand_per_node_rules_device(sp, utc, t0, t1, drules, _lib.EXCLUDE_NONE)
+    finally:
+        eng.set_node_order(_lib.NODE_ORDER_RULE)
     node_off = np.empty(rin.n_nodes + 1, dtype=np.int64)
     from cronsun_amd._lib import check, lib
     check(lib().cg_node_result_copy(eng._h, node_off.ctypes.data, None, None, 0))
@@ -186,6 +198,8 @@ def test_config3_sharded_ranges_place_to_unsharded(config3):
     dev = torch.device("cuda", 0)
     N, R = rin.n_nodes, rin.n_rules
     B = Engine(0)
+    if timed:
+        B.set_node_order(_lib.NODE_ORDER_TIME)
     try:
         arr, _ = cron.parse_batch(synth.spec_mix(R, seed=0x5EED + 3, mix=synth.MIX_CONFIG2), threads=16)
         spB = B.upload_c(arr, R)
@@ -204,6 +218,7 @@ def test_config3_sharded_ranges_place_to_unsharded(config3):
                 B.node_counts_to_device(allc[g].data_ptr())
             assert int(allc.sum()) == En
             out_t.fill_(-1)
+            allc_h = allc.cpu().numpy()
             for g, ((lo, hi), (view, dr_g)) in enumerate(zip(ranges, parts)):
                 B.expand_per_node_rules_device(view, utc, t0, t1, dr_g, _lib.EXCLUDE_NONE)
                 n_off, n_time, n_rule = B.node_result_tensors(N)  # zero-copy views of B's result
@@ -213,6 +228,14 @@ def test_config3_sharded_ranges_place_to_unsharded(config3):
                 view.free()
                 dr_g.free()
             torch.cuda.synchronize(dev)
+            if timed:
+                # run g of node n: [node_base[n] + sum_{g' < g} count[g'][n], ...)
+                rb = np.empty((N, world + 1), dtype=np.int64)
+                rb[:, 0] = node_off[:-1]
+                rb[:, 1:] = node_off[:-1, None] + np.cumsum(allc_h.T, axis=1)
+                assert np.array_equal(rb[:, world], node_off[1:])
+                # a small budget: many node groups through the scratch copy
+                shard.merge_rank_runs(rb, out_t, out_r, engine=B, budget_bytes=12 << 24)
             assert np.array_equal(node_base.cpu().numpy(), node_off), world
             assert B.checksum(out_t.data_ptr(), En, 8) == ck_t, world
             assert B.checksum(out_r.data_ptr(), En, 4) == ck_r, world
@@ -220,6 +243,9 @@ def test_config3_sharded_ranges_place_to_unsharded(config3):
         roff, rules = O.node_rules(rin, _lib.EXCLUDE_NONE, nodes, threads=host_threads())
         for k, n in enumerate(nodes):
             exp_t, exp_r = O.node_list(eo, et, rules[roff[k]:roff[k + 1]])
+            if timed:  # (time, rule): the rule-major list sorted stably by time
+                o = np.argsort(exp_t, kind="stable")
+                exp_t, exp_r = exp_t[o], exp_r[o]
             a, b = int(node_off[n]), int(node_off[n + 1])
             assert np.array_equal(out_r[a:b].cpu().numpy(), exp_r), n
             assert np.array_equal(out_t[a:b].cpu().numpy(), exp_t), n
