@@ -20,6 +20,13 @@ Workloads (`--workload`, default config2 -- the headline line):
   config4  config 4 shape: 10M rules x 7 days over the job-ID-range shards of
            N GPUs (10M / N rules per rank, lighter spec mix); a step = one
            expansion per rank.  Fixed total work: `scaling` = "strong".
+           With --per-node (north_star's target, "per-node fire schedules for
+           10M rules x 7-day horizon"): config 3's node model (10k nodes, 500
+           groups) over the config-4 rule set, per-node lists of the rank's
+           job-ID range streamed in pipelined windows (`--window`, default
+           1 h for a rank of <= 2.5M rules, else 30 min, so a window's lists
+           fit HBM); a step = the whole 7 days; the per-node counts of every
+           window all-gathered at N > 1 (cg_comm_node_offsets with --lib-comm).
   config3  config 3 as specified: 1M jobs x 10k nodes, the config-2 spec mix,
            24 h -> per-node lists, streamed in 1 h windows (`--window`; the
            whole day's 62 G node events would not fit one GPU's HBM): a step
@@ -52,18 +59,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(name, kernel, rules, events):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3
-    PMC summary profiles/r*_<name> (written by tools/pmc_traffic.py) that was
-    measured on the same workload (same rules and events per launch)."""
+def pmc_traffic(tag, rules, events, kernels, per, scale=1):
+    """HBM bytes of one timed interval, from the newest committed rocprofv3
+    PMC summary profiles/rNN_pmc_traffic[_<tag>][_vK].json (written by
+    tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes) measured on the
+    same workload -- same tag (workload and list order), rules and events per
+    step: the bytes of every launch of the kernels named by the `kernels`
+    prefixes, per launch of `per` (e.g. a pipelined window's writer plus its
+    time-order pass), times `scale` (the windows of a step).  None when no
+    such profile is committed."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_" + name)), reverse=True):
+    import re
+    pat = re.compile(r"r\d+_pmc_traffic" + (("_" + re.escape(tag)) if tag else "") + r"(_v\d+)?\.json$")
+    paths = [p for p in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic*.json"))
+             if pat.search(os.path.basename(p))]
+
+    def key(p):  # newest round, then newest version
+        m = re.search(r"r(\d+)_.*?(?:_v(\d+))?\.json$", os.path.basename(p))
+        return (int(m.group(1)), int(m.group(2) or 0))
+    for path in sorted(paths, key=key, reverse=True):
         try:
             with open(path) as f:
                 d = json.load(f)
-            k = d["kernels"][kernel]
-            if d.get("rules") == rules and d.get("events") == events:
-                return float(k["hbm_bytes_per_launch"])
+            if d.get("rules") != rules or d.get("events") != events:
+                continue
+            ks = d["kernels"]
+            n_per = ks[per]["calls"]
+            tot = sum(v["hbm_bytes_per_launch"] * v["calls"] for k, v in ks.items()
+                      if k.startswith(tuple(kernels)) and "hbm_bytes_per_launch" in v)
+            return {"bytes": tot / n_per * scale, "profile": os.path.relpath(path, ROOT),
+                    "kernels": sorted(k for k in ks if k.startswith(tuple(kernels)))}
         except Exception:
             pass
     return None
@@ -130,6 +155,9 @@ def main():
     ap.add_argument("--tick", type=int, default=0,
                     help="config2/config4: advance T0 (and T1) by this many seconds every step, as a "
                          "scheduler's consecutive windows (0 = the same window every step)")
+    ap.add_argument("--per-node", action="store_true",
+                    help="config4: per-node lists over config 3's node model (north_star's 10M x 7 d "
+                         "per-node target) instead of the rule-major CSR")
     ap.add_argument("--time-order", action="store_true",
                     help="pernode/config3: every window's per-node lists in (time, rule) order "
                          "(cg_set_node_order(TIME): the order pass inside every per-node call, pipelined)")
@@ -205,7 +233,9 @@ def main():
         seed = 0x5EED + 4
     t0 = args.t0 or synth.T0_2026
     t1 = t0 + H
-    pn = wl in ("pernode", "config3")
+    if args.per_node and wl != "config4":
+        ap.error("--per-node applies to --workload config4 (pernode/config3 are per-node already)")
+    pn = wl in ("pernode", "config3") or args.per_node
     W = args.window or (3600 if wl == "config3" else H)
     xmode = {"none": 0, "rule": 1, "cumulative": 2}[args.exclude_mode]
     eng = Engine(local)
@@ -243,6 +273,11 @@ def main():
         sp = upload_range(lo, hi)
         specs = None
         shard_lo = lo
+        if shard_info is None:
+            shard_info = {"lo": lo, "hi": hi}
+        shard_info["global_rules"] = total
+        if pn and not args.window:
+            W = 3600 if R <= 2_500_000 else 1800  # a window's node lists within HBM
 
         def spec_of(i):  # local rule i of this rank's range
             return base_specs[(shard_lo + i) % base_n]
@@ -279,7 +314,10 @@ def main():
     if pn:
         # the global jobs x groups x nodes set (one rule per job), this rank's
         # job-ID range of it (the same 500 groups and 10k nodes everywhere)
-        rin = synth.rules_for_nodes(R * world, n_nodes=n_nodes, n_groups=500, seed=0x5EED + 3)
+        if wl == "config4":
+            rin = synth.rules_for_nodes(total, n_nodes=n_nodes, n_groups=500, seed=0x5EED + 4)
+        else:
+            rin = synth.rules_for_nodes(R * world, n_nodes=n_nodes, n_groups=500, seed=0x5EED + 3)
         if world > 1:
             rin = rin.slice_rules(shard_info["lo"], shard_info["hi"])
         drules = eng.upload_rules(rin)
@@ -343,8 +381,9 @@ def main():
                 last["En_last"] = En_w
                 kt_sum += np.array(eng.kernel_times())
                 nkt_sum += np.array(eng.node_kernel_times())
-                if args.time_order:
-                    last["order_ms"] = last.get("order_ms", 0.0) + eng.node_order_by_time()
+                if args.time_order:  # the pass's time: run here, or inside the per-node call
+                    last["order_ms"] = last.get("order_ms", 0.0) + (
+                        eng.node_order_by_time() if args.order_pass else eng.last_order_ms())
                 last.setdefault("first_nkt", eng.node_kernel_times())  # the uncached join
                 if world > 1 and args.gather_node_csr and lcomm is not None:
                     # the gather behind the C-ABI (cg_comm_gather_node_csr):
@@ -602,19 +641,39 @@ def main():
             dist.destroy_process_group()
         return
 
+    traffic_src = None
     if pn:
         # per-node CSR bytes: R*32 + nnz*4 + (R+1)*8 + E_n*(8+4) + (N+1)*8
-        # per window; dominant kernel k_node_write (its time summed over the windows)
+        # per window; the timed interval: k_node_write (its time summed over the
+        # windows) -- with --time-order the writer plus the time-order pass
+        # behind it (k_ot_*: in the pipelined windows the HIP events around the
+        # writer enclose the pass; synchronous windows add the pass's own time)
         nnz, nw = last["nnz"], last["windows"]
         algo_bytes = nw * (R * SPEC_BYTES + nnz * 4 + (R + 1) * 8 + (n_nodes + 1) * 8) + E * 12
         kname, ksec = "k_node_write", nkt[2] / 1e3
-        hz = f"{H // 3600}h" if H % 3600 == 0 else f"{H}s"
-        metric = f"per-node fire events materialised/sec (config 3: 1M jobs × 10k nodes, {hz})"
-        workload = (f"config 3: 1M jobs x 10k nodes (500 groups, GroupIDs/NodeIDs/ExcludeNodeIDs), "
-                    f"{'config-2' if wl == 'config3' else 'light'} spec mix, {hz} horizon in "
-                    f"{nw} window(s) of {W}s, {args.zone}, per GPU; exclude mode {args.exclude_mode}"
-                    + (" (job.go:591-630)" if xmode == 0 else ""))
-        traffic = pmc_traffic("pmc_traffic_pernode.json", kname, R, E) if wl == "pernode" else None
+        kernels = ["k_node_write"]
+        if args.time_order:
+            kname = "k_node_write + time-order pass (k_ot_tile, k_ot_merge/mid/big)"
+            kernels += ["k_ot_", "k_ts_"]
+            if not pn_pipelined:
+                ksec += last["order_ms"] / args.steps / 1e3
+        hz = f"{H // 3600}h" if H % 3600 == 0 else (f"{H // 86400}d" if H % 86400 == 0 else f"{H}s")
+        if wl == "config4":
+            metric = f"per-node fire events materialised/sec (config 4: 10M rules × 7d, per-node over 10k nodes)"
+            workload = (f"config 4 per node: 10M rules x {hz} (the 1M-rule light-mix block tiled 10x, job-ID "
+                        f"order) x 10k nodes (config 3's node model: 500 groups, GroupIDs/NodeIDs/"
+                        f"ExcludeNodeIDs), {nw} window(s) of {W}s, {args.zone}, job-ID-range shards over N "
+                        f"GPUs; exclude mode {args.exclude_mode}" + (" (job.go:591-630)" if xmode == 0 else ""))
+        else:
+            metric = f"per-node fire events materialised/sec (config 3: 1M jobs × 10k nodes, {hz})"
+            workload = (f"config 3: 1M jobs x 10k nodes (500 groups, GroupIDs/NodeIDs/ExcludeNodeIDs), "
+                        f"{'config-2' if wl == 'config3' else 'light'} spec mix, {hz} horizon in "
+                        f"{nw} window(s) of {W}s, {args.zone}, per GPU; exclude mode {args.exclude_mode}"
+                        + (" (job.go:591-630)" if xmode == 0 else ""))
+        tag = {"pernode": "pernode", "config3": "config3", "config4": "config4pn"}[wl] + \
+            ("_order" if args.time_order else "")
+        if args.zone == "UTC" and xmode == 0:
+            traffic_src = pmc_traffic(tag, R, E, kernels, "k_node_write", scale=nw)
     else:
         algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
         kname, ksec = "k_write_cf", kt[3] / 1e3
@@ -622,7 +681,9 @@ def main():
         workload = (f"config 2: 1M mixed cron rules x {H // 3600}h horizon, {args.zone}, per GPU "
                     f"(job-ID-range shards)" if wl == "config2" else
                     f"config 4: 10M rules x 7d horizon, light spec mix, {args.zone}, job-ID-range shards over N GPUs")
-        traffic = pmc_traffic("pmc_traffic.json", kname, R, E) if wl == "config2" else None
+        if wl == "config2" and args.zone == "UTC" and not args.tick:
+            traffic_src = pmc_traffic("", R, E, ["k_write_cf"], "k_write_cf")
+    traffic = traffic_src["bytes"] if traffic_src else None
     achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
 
     # the achievable store rate on this box, beside the nominal peak: a
@@ -637,7 +698,7 @@ def main():
         cpu = cpu_baseline_per_node(spec_of, rin, xmode, a_last, min(a_last + W, t1), args.zone)
     if world == 1 and args.cpu_sample != 0 and wl == "config2":
         cpu = cpu_baseline(specs, args.cpu_sample, t0, t1, args.cpu_threads, zone=args.zone)
-    if world == 1 and args.cpu_sample != 0 and wl == "config4":
+    if world == 1 and args.cpu_sample != 0 and wl == "config4" and not pn:
         # the 10M-rule set (rule i = base[i % 1M]); a strided sample sized for ~15 s
         cpu = cpu_baseline([spec_of(i) for i in range(R)], args.cpu_sample, t0, t1, args.cpu_threads,
                            zone=args.zone)
@@ -689,6 +750,8 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
+            "timed_interval_s": ksec,
             "algo_bytes_per_launch": algo_bytes,
             "store_ceiling": ceiling,
         },

@@ -564,6 +564,14 @@ class Engine:
         lib().cg_last_kernel_times(self._h, buf, 13)
         return buf[12]
 
+    def last_order_ms(self):
+        """ms of the last time-order pass (cg_last_kernel_times [12]): the pass
+        inside the last synchronous per-node call in CG_NODE_ORDER_TIME, or
+        the last cg_node_result_order_by_time."""
+        buf = (C.c_float * 13)()
+        check(lib().cg_last_kernel_times(self._h, buf, 13))
+        return buf[12]
+
     def node_csr_place(self, n_nodes, src_node_off, src_time, src_rule, rule_add, dst_start, dst_time, dst_rule):
         """Place one rank's per-node slice into the gathered per-node CSR on
         this engine's device (cg_node_csr_place); arguments are device
