@@ -707,12 +707,66 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
   }
 }
 
+#ifndef CG_OT_MID2
+#define CG_OT_MID2 1  // 0: slabs of 8193..16384 events to k_ot_big, not k_ot_mid's 16-wave form (A/B)
+#endif
+#ifndef CG_OT_MID
+#define CG_OT_MID 1  // 0: every slab of more than a merge chunk to k_ot_big (A/B)
+#endif
+#ifndef CG_OT_PIPE
+// 1: the packed merge pipelined -- the next chunk's gathers issued before the
+// current chunk's stores, every store instruction unconditional (a fixed
+// count), so waiting for the gathers does not drain the stores (gfx9: one
+// in-order vmcnt for loads and stores); big slabs queued by k_ot_slabs
+#define CG_OT_PIPE 0
+#endif
+// The packed words (offset << 20 | rule) of elements 0 .. n_el of the
+// portion list as keys, for the pipelined merge: no use of the loaded values
+// here (the waits for them come at the sort, after the previous chunk's
+// stores), lanes past n_el read out of the buffer's range (0).  Portions by
+// search + walk (ot_gather SEARCH 2), raw buffer loads.
+template <int IT>
+__device__ __forceinline__ void ot_gather_words(const int32_t* __restrict__ rin, const int32_t* ps, const int32_t* psrc,
+                                                int n_el, uint32_t (&key)[IT], int Q, uint32_t n_src) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ebase = w * (64 * IT);
+  constexpr int kRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(rin), 0, int(n_src * 4u), kRsrcWord3);
+  const int e0 = ebase + lane < n_el ? ebase + lane : n_el - 1;
+  int qw = ot_find(ps, Q, e0), qa = ps[qw], qb = ps[qw + 1], qs = psrc[qw];
+#pragma unroll
+  for (int j = 0; j < IT; j++) {
+    const int e = ebase + j * 64 + lane;
+    const int ec = e < n_el ? e : n_el - 1;
+    while (qb <= ec && qw + 1 < Q) {
+      qw++;
+      qa = qb;
+      qb = ps[qw + 1];
+      qs = psrc[qw];
+    }
+    const uint32_t off = e < n_el ? uint32_t(qs + (ec - qa)) * 4u : 0xFFFFFFF0u;
+    key[j] = uint32_t(__builtin_amdgcn_raw_buffer_load_b32(rb, int(off), 0, 0));
+  }
+}
+
 // Per node: the first node-relative position of each slab (events of the
 // earlier slabs over all its tiles), slab_off[n][0..kOtSlabs].  One wave per
-// node, kOtSlabs / 64 slabs per lane.
+// node, kOtSlabs / 64 slabs per lane.  With q.on (the pipelined merge), the
+// slabs no merge chunk of their node can hold are queued here, so the merge
+// loop issues no atomics: to k_ot_mid / its 16-wave form when they fit those
+// chunks, else to k_ot_big; every non-empty slab of a node of more than
+// kOtMaxTiles tiles to k_ot_big.  Entries (node << 8 | slab).
+struct OtQueues {
+  int64_t *big, *mid, *mid2;
+  unsigned *big_n, *mid_n, *mid2_n;
+  const int64_t* node_off;
+  int64_t dense_min;            // events from which a node takes the dense merge
+  int32_t chunk, dense_chunk;   // the two merges' chunks
+  int32_t on;
+};
 __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ tile_base,
                                                   const int32_t* __restrict__ pre, int32_t N,
-                                                  int64_t* __restrict__ slab_off) {
+                                                  int64_t* __restrict__ slab_off, OtQueues q) {
   constexpr int kSpl = kOtSlabs / 64;
   const int lane = threadIdx.x;
   const int32_t n = blockIdx.x;
@@ -746,13 +800,25 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
     run += c[i];
   }
   if (lane == 63) so[kOtSlabs] = run;
+  if (!q.on || M <= 1) return;  // one tile: sorted by k_ot_tile
+  constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems, kMid2Chunk = 64 * kOtMid2Waves * kOtItems;
+  const int64_t e_n = q.node_off[n + 1] - q.node_off[n];
+  const int64_t chunk = e_n >= q.dense_min ? q.dense_chunk : q.chunk;
+#pragma unroll
+  for (int i = 0; i < kSpl; i++) {
+    const int64_t e = (int64_t(n) << 8) | (kSpl * lane + i);
+    if (M > kOtMaxTiles) {
+      if (c[i] > 0) q.big[atomicAdd(q.big_n, 1u)] = e;
+    } else if (c[i] > chunk) {
+      if (CG_OT_MID && c[i] <= kMidChunk) q.mid[atomicAdd(q.mid_n, 1u)] = e;
+      else if (CG_OT_MID2 && c[i] <= kMid2Chunk) q.mid2[atomicAdd(q.mid2_n, 1u)] = e;
+      else q.big[atomicAdd(q.big_n, 1u)] = e;
+    }
+  }
 }
 
 #ifndef CG_OT_OWN_SEARCH
 #define CG_OT_OWN_SEARCH 2  // the merge's portion per element: 0 owner map, 1 binary search, 2 search + walk
-#endif
-#ifndef CG_OT_MID2
-#define CG_OT_MID2 1  // 0: slabs of 8193..16384 events to k_ot_big, not k_ot_mid's 16-wave form (A/B)
 #endif
 #ifndef CG_OT_MERGE_RUNS
 // 1: the merge / k_ot_big ranks add once per run of equal digits in
@@ -766,11 +832,11 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 #ifndef CG_OT_MID_WPE
 #define CG_OT_MID_WPE 4  // min waves per SIMD of k_ot_mid (8-wave blocks: 2 per SIMD each)
 #endif
-#ifndef CG_OT_MID
-#define CG_OT_MID 1  // 0: every slab of more than a merge chunk to k_ot_big (A/B)
-#endif
 #ifndef CG_OT_MERGE_WPE
 #define CG_OT_MERGE_WPE 4  // min waves per SIMD of the packed merge (its LDS allows 6 blocks per CU)
+#endif
+#ifndef CG_OT_DENSE_WPE
+#define CG_OT_DENSE_WPE 4  // the same for the dense nodes' merge (the persistent 8-wave grid)
 #endif
 
 // One chunk of n_el <= 64 * NW * kOtItems events of a node (tin_n / rin_n:
@@ -815,6 +881,78 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   ot_sync<NW>();
 }
 
+// One node's merge, pipelined (CG_OT_PIPE; packed words, rule indices <
+// 2^20): its slabs in runs of whole slabs that fit one chunk (the slabs no
+// chunk holds were queued by k_ot_slabs), run after run -- the next run's
+// portions and gathers are issued between this run's sort and its stores,
+// and the run after next's tile prefixes right after them, so the wait for a
+// chunk's gathers covers only loads issued before the previous chunk's
+// stores.  Every store instruction is unconditional (lanes past the chunk
+// store its last element again), so the compiler's vmcnt waits count a fixed
+// number of stores instead of draining them.  pq: this thread's tile's slab
+// prefix row (thread q owns tile q); bad collects order-check failures.
+template <int NW, int IT, bool PIN>
+__device__ __forceinline__ void ot_merge_node_pipe(const uint16_t* __restrict__ tin_n, const int32_t* __restrict__ rin_n,
+                                                   const int32_t* __restrict__ pq, int M, const int64_t* slab_off,
+                                                   int64_t t0, int64_t* __restrict__ tout_n,
+                                                   int32_t* __restrict__ rout_n, OtRank<NW, 256>& s, uint32_t* pk,
+                                                   int32_t* ps, int32_t* psrc, int32_t* wsum, bool& bad) {
+  constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
+  const uint32_t n_src = uint32_t(M) * kOtTile;
+  // the first run of whole slabs at or after j0 that a chunk holds: empty and
+  // queued slabs skipped, then every slab that still fits
+  auto next_run = [&](int j0, int& ja, int& jb) {
+    ja = j0;
+    while (ja < kOtSlabs && (slab_off[ja + 1] == slab_off[ja] || slab_off[ja + 1] - slab_off[ja] > kChunk)) ja++;
+    jb = ja;
+    while (jb < kOtSlabs && slab_off[jb + 1] - slab_off[ja] <= kChunk) jb++;
+  };
+  int ja, jb, ja2, jb2;
+  next_run(0, ja, jb);
+  if (ja >= kOtSlabs) return;
+  next_run(jb, ja2, jb2);
+  const int q = threadIdx.x;
+  int32_t pa = pq[ja], pb = pq[jb];
+  ot_portions<NW>(M, [&](int, int32_t* src) { *src = q * kOtTile + pa; return pb - pa; }, ps, psrc, wsum);
+  // the next run's tile prefixes are loaded before this run's gathers: the
+  // wait for the gathers (at the sort) covers them
+  pa = pq[ja2 < kOtSlabs ? ja2 : kOtSlabs];
+  pb = pq[jb2 < kOtSlabs ? jb2 : kOtSlabs];
+  uint32_t key[IT];
+  int n_el = int(slab_off[jb] - slab_off[ja]);
+  ot_gather_words<IT>(rin_n, ps, psrc, n_el, key, M, n_src);
+  ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
+  for (;;) {
+    // pk holds run [ja, jb) sorted; the next run's prefixes are in pa / pb
+    const int64_t o = slab_off[ja];
+    const int n_cur = n_el;
+    const bool more = ja2 < kOtSlabs;  // block-uniform
+    if (more) {
+      ot_portions<NW>(M, [&](int, int32_t* src) { *src = q * kOtTile + pa; return pb - pa; }, ps, psrc, wsum);
+      ja = ja2;
+      jb = jb2;
+      next_run(jb, ja2, jb2);
+      pa = pq[ja2 < kOtSlabs ? ja2 : kOtSlabs];
+      pb = pq[jb2 < kOtSlabs ? jb2 : kOtSlabs];
+      n_el = int(slab_off[jb] - slab_off[ja]);
+      ot_gather_words<IT>(rin_n, ps, psrc, n_el, key, M, n_src);
+    }
+#pragma unroll
+    for (int j = 0; j < IT; j++) {
+      const int p = threadIdx.x + j * kThreads;
+      const int pc = p < n_cur ? p : n_cur - 1;
+      const uint32_t v = pk[pc];
+      __builtin_nontemporal_store(t0 + 1 + int64_t(v >> kOtRuleBits), tout_n + o + pc);
+      __builtin_nontemporal_store(int32_t(v & ((1u << kOtRuleBits) - 1u)), rout_n + o + pc);
+      const uint32_t u = ot_prev(pk, p, v);
+      if (p > 0 && p < n_cur) bad |= u >= v;  // (time, rule) order of the chunk: the words ascend
+    }
+    ot_sync<NW>();
+    if (!more) break;
+    ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
+  }
+}
+
 // Per node with e_lo <= events < e_hi: its slabs in runs that fit one chunk,
 // each merged by ot_merge_chunk.  Two launches split the nodes by density:
 // 4-wave blocks (4096-event chunks) for nodes averaging at most
@@ -829,7 +967,7 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
 // fits k_ot_mid's chunk (mid / mid_n), else to k_ot_big (big / big_n);
 // entries (node << 8 | slab).
 template <int NW, bool PACK, int IT = kOtItems, bool DYN = false, bool PIN = false>  // DYN: nodes by ticket (persistent grid)
-__global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
+__global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERGE_WPE) : 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
                                                        const int32_t* __restrict__ pre, int32_t N, int64_t t0,
@@ -871,12 +1009,21 @@ __global__ __launch_bounds__(64 * NW, PACK ? CG_OT_MERGE_WPE : 4) void k_ot_merg
     }
     continue;
   }
-  if (M > kOtMaxTiles) {  // every slab to k_ot_big
-    for (int j = threadIdx.x; j < kOtSlabs; j += kThreads) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | j;
+  if (M > kOtMaxTiles) {  // every slab to k_ot_big (queued by k_ot_slabs in the pipelined form)
+    if (!(PACK && PIN && CG_OT_PIPE))
+      for (int j = threadIdx.x; j < kOtSlabs; j += kThreads) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | j;
     continue;
   }
   for (int j = threadIdx.x; j <= kOtSlabs; j += kThreads) slab_off[j] = slab_tab[int64_t(n) * kOtPre + j];
   ot_sync<NW>();
+  if constexpr (PACK && PIN && CG_OT_PIPE) {
+    const int32_t* __restrict__ pq = pre + (ta + (threadIdx.x < M ? threadIdx.x : 0)) * kOtPre;
+    bool bad = false;
+    ot_merge_node_pipe<NW, IT, PIN>(tin + lo_n, rin + lo_n, pq, int(M), slab_off, t0, tout + lo_n, rout + lo_n, s, pk,
+                                    ps, psrc, wsum, bad);
+    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
+    continue;
+  }
   // the longest run of whole slabs [j0, j1) that fits one chunk (j1 == j0: a
   // slab of more than a chunk)
   auto run_end = [&](int j0) {
@@ -1325,12 +1472,16 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   int64_t* slab_tab = c->ts_off.p + int64_t(N) * kOtSlabs + 2;
   int64_t* mid = slab_tab + int64_t(N) * kOtPre;
   int64_t* mid2 = mid + int64_t(N) * kOtSlabs;
-  hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
   const int cus = std::max(1, c->write_blocks / kWriteBlocksPerCU);
   // nodes split by density between a 4-wave and an 8-wave merge; the dense
   // nodes' merge runs on its own stream beside the sparse one (few dense
   // nodes after all the sparse ones would run as a tail at low occupancy)
   const int64_t dense_min = int64_t(CG_OT_DENSE_PER_SLAB) * std::max<int64_t>(1, (H + 63) / 64);
+  const bool pack = CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
+  OtQueues oq{c->ts_off.p, slab_tab + int64_t(N) * kOtPre, slab_tab + int64_t(N) * kOtPre + int64_t(N) * kOtSlabs,
+              big_n, big_n + 1, big_n + 3, node_off, dense_min, 64 * kOtMergeWaves * kOtMergeItems,
+              64 * kOtDenseWaves * kOtItems, (pack && pin && CG_OT_PIPE) ? 1 : 0};
+  hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab, oq);
   if (!c->st_ot) {  // created together: the ctx holds all three or none
     hipStream_t so = nullptr;
     hipEvent_t ef = nullptr, ej = nullptr;
@@ -1368,7 +1519,6 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
                        c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
                        big_n + 3, err);
   };
-  const bool pack = CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
   if (pack && pin)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,
            k_ot_merge<kOtDenseWaves, true, kOtItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,

@@ -370,6 +370,9 @@ __device__ __forceinline__ int32_t half_total(int32_t incl) {
 #define CG_SEG_PAIRS_PER_LANE 8
 #endif
 constexpr int kSegPairsPerLane = CG_SEG_PAIRS_PER_LANE;
+#ifndef CG_SEG_WPE
+#define CG_SEG_WPE 1  // min waves per SIMD of k_seg_records (caps its VGPRs; 1: no cap)
+#endif
 
 // Segment records, one wave per segment in band-major order (a band's
 // offsets stay in L2): the segment's event count, and for each of its
@@ -381,7 +384,7 @@ constexpr int kSegPairsPerLane = CG_SEG_PAIRS_PER_LANE;
 // then reads plain records instead of chasing pair -> rule -> offsets per
 // window.  Block 0 also resets the writer's tickets; err[0] is set if a
 // segment or a band outgrows the writer's 32-bit positions.
-__global__ __launch_bounds__(256) void k_seg_records(const int64_t* __restrict__ seg_pair,
+__global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* __restrict__ seg_pair,
                                                       const int32_t* __restrict__ nt_rule,
                                                       const int64_t* __restrict__ rule_off,
                                                       const RuleInfo* __restrict__ info, int32_t N,
