@@ -720,6 +720,13 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
 // in-order vmcnt for loads and stores); big slabs queued by k_ot_slabs
 #define CG_OT_PIPE 0
 #endif
+#ifndef CG_OT_EARLY_QUEUE
+// 1: k_ot_slabs queues the slabs no merge chunk holds (also without
+// CG_OT_PIPE), so k_ot_mid's two forms run beside the merges instead of after
+// them: the 16-wave form behind the dense merge on its stream, the 8-wave form
+// behind the sparse merge
+#define CG_OT_EARLY_QUEUE 1
+#endif
 // The packed words (offset << 20 | rule) of elements 0 .. n_el of the
 // portion list as keys, for the pipelined merge: no use of the loaded values
 // here (the waits for them come at the sort, after the previous chunk's
@@ -1010,7 +1017,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
     continue;
   }
   if (M > kOtMaxTiles) {  // every slab to k_ot_big (queued by k_ot_slabs in the pipelined form)
-    if (!(PACK && PIN && CG_OT_PIPE))
+    if (!(CG_OT_EARLY_QUEUE || (PACK && PIN && CG_OT_PIPE)))
       for (int j = threadIdx.x; j < kOtSlabs; j += kThreads) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | j;
     continue;
   }
@@ -1045,8 +1052,8 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
     const int jb2 = ja2 < kOtSlabs ? run_end(ja2) : ja2;
     const int32_t pa2 = jb == ja ? pq[ja2 <= kOtSlabs ? ja2 : kOtSlabs] : pb;
     const int32_t pb2 = pq[jb2 <= kOtSlabs ? jb2 : kOtSlabs];  // in flight while this run is merged
-    if (jb == ja) {  // one slab of more than a chunk
-      if (threadIdx.x == 0) {
+    if (jb == ja) {  // one slab of more than a chunk (queued by k_ot_slabs with CG_OT_EARLY_QUEUE)
+      if (!CG_OT_EARLY_QUEUE && threadIdx.x == 0) {
         const int64_t sz = slab_off[ja + 1] - slab_off[ja];
         if (CG_OT_MID && sz <= kMidChunk) mid[atomicAdd(mid_n, 1u)] = (int64_t(n) << 8) | ja;
         else if (CG_OT_MID2 && sz <= kMid2Chunk) mid2[atomicAdd(mid2_n, 1u)] = (int64_t(n) << 8) | ja;
@@ -1480,7 +1487,8 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   const bool pack = CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
   OtQueues oq{c->ts_off.p, slab_tab + int64_t(N) * kOtPre, slab_tab + int64_t(N) * kOtPre + int64_t(N) * kOtSlabs,
               big_n, big_n + 1, big_n + 3, node_off, dense_min, 64 * kOtMergeWaves * kOtMergeItems,
-              64 * kOtDenseWaves * kOtItems, (pack && pin && CG_OT_PIPE) ? 1 : 0};
+              64 * kOtDenseWaves * kOtItems, (CG_OT_EARLY_QUEUE || (pack && pin && CG_OT_PIPE)) ? 1 : 0};
+  const bool early = oq.on != 0;
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab, oq);
   if (!c->st_ot) {  // created together: the ctx holds all three or none
     hipStream_t so = nullptr;
@@ -1505,6 +1513,10 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
                        dense_min, INT64_MAX, big_n + 2, err);
+    if (early)  // k_ot_mid's 16-wave form behind the dense merge, beside the sparse one
+      hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, c->st_ot, toff, c->node_rule2.p,
+                         c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
+                         big_n + 3, err);
     hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
                        mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err);
@@ -1515,9 +1527,10 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
                        big_n + 1, err);
     (void)hipEventRecord(c->ot_join, c->st_ot);
     (void)hipStreamWaitEvent(st, c->ot_join, 0);
-    hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
-                       c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
-                       big_n + 3, err);
+    if (!early)
+      hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
+                         c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
+                         big_n + 3, err);
   };
   if (pack && pin)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,

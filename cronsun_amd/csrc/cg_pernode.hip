@@ -393,9 +393,18 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
                                                       int32_t* __restrict__ seg_nrec,
                                                       PairRec* __restrict__ recs,
                                                       uint32_t* __restrict__ tickets,
-                                                      int64_t* __restrict__ err) {
+                                                      int64_t* __restrict__ err, int32_t xg) {
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < kTicketGroups * kTicketStride; i += blockDim.x) tickets[i] = 0;
+  // xg > 1: the blocks of one residue b % xg (the same XCD under the
+  // round-robin dispatch, MI355X_MICROARCH.md; speed only) take the bands
+  // k == b % xg (mod xg), so each XCD's L2 holds the rule infos of its own
+  // one or two bands instead of every band the whole grid is working on
+  const int32_t grp = int32_t(blockIdx.x % unsigned(xg));
+  const int64_t nb_g = (int64_t(gridDim.x) - grp + xg - 1) / xg;
+  const int64_t lb = blockIdx.x / unsigned(xg);
+  const int64_t nbands = (int64_t(K) - grp + xg - 1) / xg;  // this group's bands
+  const int64_t NKg = nbands * N;
   // Two segments per wave, one per half-wave (consecutive nodes of a band),
   // software-pipelined: the kernel is latency-bound (segment bounds -> pair
   // rules -> rule infos -> records), so each iteration issues the bounds two
@@ -404,8 +413,7 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
   constexpr int L = 32;  // lanes per segment
   constexpr int P = kSegPairsPerLane;
   const int lane = threadIdx.x & 63, hl = lane & (L - 1);
-  const int64_t NK = int64_t(N) * K;
-  const int64_t nh = int64_t(gridDim.x) * (blockDim.x >> 6) * 2;
+  const int64_t nh = nb_g * (blockDim.x >> 6) * 2;
   const uint32_t below = (1u << hl) - 1u;  // lanes of this half before this one
   struct Seg {
     int64_t s, p0, p1;
@@ -413,8 +421,9 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
   auto bounds = [&](int64_t tw) -> Seg {
     const int64_t t = tw + (lane >> 5);
     Seg g{-1, 0, 0};
-    if (t < NK) {
-      const int32_t k = int32_t(t / N), n = int32_t(t - int64_t(k) * N);
+    if (t < NKg) {
+      const int32_t i = int32_t(t / N), n = int32_t(t - int64_t(i) * N);
+      const int32_t k = grp + xg * i;
       g.s = int64_t(n) * K + k;
       g.p0 = seg_pair[g.s];
       g.p1 = seg_pair[g.s + 1];
@@ -430,11 +439,11 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
       r[u] = pp < g.p1 ? nt_rule[pp] : -1;
     }
   };
-  int64_t tw = (blockIdx.x * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2;
+  int64_t tw = (lb * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2;
   Seg cur = bounds(tw), nxt = bounds(tw + nh);
   int32_t r[P], rn[P];
   rules(cur, 0, r);
-  for (; tw < NK; tw += nh) {
+  for (; tw < NKg; tw += nh) {
     const Seg nn = bounds(tw + 2 * nh);  // two ahead
     rules(nxt, 0, rn);                   // the next pair's first round
     int64_t run = 0;  // events of the segment so far
@@ -1093,6 +1102,13 @@ __global__ void k_band_max(const int64_t* __restrict__ off, int64_t R, int32_t B
   atomicMax(out, (unsigned long long)(off[b] - off[a]));
 }
 
+#ifndef CG_SEG_XCD
+#define CG_SEG_XCD 8  // k_seg_records' XCD band groups (1: every block on the bands in order)
+#endif
+// band groups of k_seg_records: one per XCD when there are enough bands to
+// balance them (else every XCD's blocks walk the bands in order)
+int32_t seg_xcd_groups(int32_t K) { return CG_SEG_XCD > 1 && K >= 4 * CG_SEG_XCD ? CG_SEG_XCD : 1; }
+
 int32_t band_rules(int64_t R, int64_t E) {
   const double per_rule = double(std::max<int64_t>(E, 1)) * 8.0 / double(std::max<int64_t>(R, 1));
   int64_t B = int64_t(double(CG_BAND_BYTES) / per_rule);
@@ -1171,7 +1187,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
                        c->nt_rule.p, c->offsets.p, c->rule_info.p, N, K, B, R, c->seg_cnt.p, c->seg_nrec.p,
                        c->recs.p, c->pn_tickets.p,
-                       c->pn_res_dev + 1);
+                       c->pn_res_dev + 1, seg_xcd_groups(K));
   launch_scan64(c->seg_cnt.p, c->seg_pos.p, NK, c->scan_tmp.p, st);
   hipLaunchKernelGGL(k_node_off_from_seg, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st,
                      c->seg_pos.p, N, K, c->node_off.p, c->pn_res_dev);
@@ -1457,7 +1473,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     if (!empty)
       hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, sc, c->seg_pair.p, c->nt_rule.p,
                          a.rm.offsets.p, a.rule_info.p, N, K, B, R, a.seg_cnt.p, a.seg_nrec.p, a.recs.p,
-                         a.tickets.p, a.res_dev + 1);
+                         a.tickets.p, a.res_dev + 1, seg_xcd_groups(K));
     else
       HIPCHK(hipMemsetAsync(a.seg_cnt.p, 0, NK * 8, sc));
     launch_scan64(a.seg_cnt.p, a.seg_pos.p, NK, a.seg_tmp.p, sc);

@@ -109,3 +109,52 @@ def test_comm_then_torch_exits_cleanly():
                            capture_output=True, text=True, timeout=150)
         assert p.returncode == 0, (mode, p.returncode, p.stdout[-2000:], p.stderr[-2000:])
         assert f"done {mode}" in p.stdout and "rccl copies 1" in p.stdout, (mode, p.stdout[-2000:])
+
+
+@pytest.mark.parametrize("world,budget", [(2, 12 * 5000), (3, 1 << 31), (8, 12 * 777), (64, 12 * 40000)])
+def test_merge_ranks_random(world, budget):
+    """cg_node_csr_merge_ranks (the time-ordered gather's merge, also run by
+    cg_comm_gather_node_csr on root): every node's rank runs, each in (time,
+    rule) order with rank g's rules below rank g+1's, merged in place into
+    (time, rule) order -- a stable sort by time of the node's list.  Many equal
+    times (ties across runs), empty runs, nodes with one non-empty run, a node
+    larger than the scratch budget, up to 64 ranks."""
+    import torch
+    rng = np.random.default_rng(world)
+    N = 300
+    cnt = rng.integers(0, 60, (N, world))
+    cnt[rng.random((N, world)) < 0.3] = 0
+    cnt[5] = 0
+    cnt[6, :] = 0
+    cnt[6, world // 2] = 500  # one non-empty run: nothing to merge
+    cnt[7] = 2000  # larger than the smallest budgets' groups
+    rb = np.zeros((N, world + 1), dtype=np.int64)
+    rb[:, 1:] = np.cumsum(cnt, axis=1)
+    base = np.concatenate([[0], np.cumsum(rb[:, -1])[:-1]])
+    rb += base[:, None]
+    E = int(rb[-1, -1])
+    t = np.empty(E, dtype=np.int64)
+    r = np.empty(E, dtype=np.int32)
+    for n in range(N):
+        for g in range(world):
+            a, b = rb[n, g], rb[n, g + 1]
+            tt = np.sort(rng.integers(1767571200, 1767571200 + 40, b - a))
+            rr = rng.integers(g * 1000, g * 1000 + 1000, b - a).astype(np.int32)
+            o = np.lexsort((rr, tt))
+            t[a:b], r[a:b] = tt[o], rr[o]
+    exp_t, exp_r = t.copy(), r.copy()
+    for n in range(N):
+        a, b = rb[n, 0], rb[n, -1]
+        o = np.argsort(t[a:b], kind="stable")
+        exp_t[a:b], exp_r[a:b] = t[a:b][o], r[a:b][o]
+    from cronsun_amd.engine import Engine
+    dev = torch.device("cuda", 0)
+    dt, dr = torch.from_numpy(t).to(dev), torch.from_numpy(r).to(dev)  # torch first (its own context)
+    torch.cuda.synchronize(dev)
+    eng = Engine(0)
+    try:
+        eng.node_csr_merge_ranks(N, world, rb, dt.data_ptr(), dr.data_ptr(), budget)
+    finally:
+        eng.close()
+    assert np.array_equal(dt.cpu().numpy(), exp_t)
+    assert np.array_equal(dr.cpu().numpy(), exp_r)
