@@ -725,7 +725,7 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
 // CG_OT_PIPE), so k_ot_mid's two forms run beside the merges instead of after
 // them: the 16-wave form behind the dense merge on its stream, the 8-wave form
 // behind the sparse merge
-#define CG_OT_EARLY_QUEUE 1
+#define CG_OT_EARLY_QUEUE 0
 #endif
 // The packed words (offset << 20 | rule) of elements 0 .. n_el of the
 // portion list as keys, for the pipelined merge: no use of the loaded values
