@@ -370,6 +370,9 @@ __device__ __forceinline__ int32_t half_total(int32_t incl) {
 #define CG_SEG_PAIRS_PER_LANE 8
 #endif
 constexpr int kSegPairsPerLane = CG_SEG_PAIRS_PER_LANE;
+#ifndef CG_SEG_NOINFO
+#define CG_SEG_NOINFO 0  // diagnostic timing only: no rule-info gathers (wrong records)
+#endif
 #ifndef CG_SEG_WPE
 #define CG_SEG_WPE 1  // min waves per SIMD of k_seg_records (caps its VGPRs; 1: no cap)
 #endif
@@ -413,15 +416,22 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
   constexpr int L = 32;  // lanes per segment
   constexpr int P = kSegPairsPerLane;
   const int lane = threadIdx.x & 63, hl = lane & (L - 1);
-  const int64_t nh = nb_g * (blockDim.x >> 6) * 2;
+  // every half-wave walks its own run of `per` consecutive segments (in band
+  // order): the blocks resident at any time cover a few consecutive bands, so
+  // their rule infos stay in L2 even when the grid is many times the blocks
+  // the CUs hold at once (a grid-stride walk spread the resident blocks over
+  // ~20 bands: half the info gathers missed L2, 72 GB per config-4 window)
+  const int64_t Hg = nb_g * (blockDim.x >> 6) * 2;
+  const int64_t per = (NKg + Hg - 1) / Hg;
+  const int64_t hid = (lb * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2 + (lane >> 5);
   const uint32_t below = (1u << hl) - 1u;  // lanes of this half before this one
   struct Seg {
     int64_t s, p0, p1;
   };
-  auto bounds = [&](int64_t tw) -> Seg {
-    const int64_t t = tw + (lane >> 5);
+  auto bounds = [&](int64_t u) -> Seg {
+    const int64_t t = hid * per + u;
     Seg g{-1, 0, 0};
-    if (t < NKg) {
+    if (u < per && t < NKg) {
       const int32_t i = int32_t(t / N), n = int32_t(t - int64_t(i) * N);
       const int32_t k = grp + xg * i;
       g.s = int64_t(n) * K + k;
@@ -439,12 +449,11 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
       r[u] = pp < g.p1 ? nt_rule[pp] : -1;
     }
   };
-  int64_t tw = (lb * int64_t(blockDim.x >> 6) + (threadIdx.x >> 6)) * 2;
-  Seg cur = bounds(tw), nxt = bounds(tw + nh);
+  Seg cur = bounds(0), nxt = bounds(1);
   int32_t r[P], rn[P];
   rules(cur, 0, r);
-  for (; tw < NKg; tw += nh) {
-    const Seg nn = bounds(tw + 2 * nh);  // two ahead
+  for (int64_t u = 0; u < per; u++) {
+    const Seg nn = bounds(u + 2);  // two ahead
     rules(nxt, 0, rn);                   // the next pair's first round
     int64_t run = 0;  // events of the segment so far
     int32_t nrec = 0;
@@ -454,7 +463,8 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
       if (pc > 0) rules(cur, pc, r);  // segments of more than L*P pairs
       RuleInfo g[P];
 #pragma unroll
-      for (int u = 0; u < P; u++) g[u] = r[u] >= 0 ? info[r[u]] : RuleInfo{0, 0, 0, 0};
+      for (int u = 0; u < P; u++)
+        g[u] = r[u] >= 0 ? (CG_SEG_NOINFO ? RuleInfo{1, 0, 0, 1} : info[r[u]]) : RuleInfo{0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < P; u++) {
         // events before this pair: half-wave inclusive scan of the counts
