@@ -329,14 +329,32 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
   if (tid == 0) off[nr] = rule_off[r0 + nr];
   __syncthreads();
   const int64_t e_end = off[nr];
-  for (int64_t e = off[0] + tid; e + 1 < e_end; e += blockDim.x) {
-    int lo = 0, hi = nr - 1;  // the last rule whose list starts at or before e
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (off[mid] <= e) lo = mid;
-      else hi = mid - 1;
+  // kRiUnroll events per thread per round, their loads issued together: a
+  // block whose rules fire thousands of times in the window (every-second
+  // rules) walks a long span, and one dependent load pair per round made it
+  // the kernel's latency tail
+  constexpr int kRiUnroll = 4;
+  for (int64_t e0 = off[0] + tid; e0 + 1 < e_end; e0 += int64_t(blockDim.x) * kRiUnroll) {
+    int64_t ta[kRiUnroll], tb[kRiUnroll];
+#pragma unroll
+    for (int u = 0; u < kRiUnroll; u++) {
+      const int64_t e = e0 + int64_t(u) * blockDim.x;
+      const int64_t ec = e + 1 < e_end ? e : e_end - 2;  // clamped: every load in range
+      ta[u] = times[ec];
+      tb[u] = times[ec + 1];
     }
-    if (e + 1 < off[lo + 1] && times[e + 1] - times[e] != step[lo]) ok[lo] = 0;
+#pragma unroll
+    for (int u = 0; u < kRiUnroll; u++) {
+      const int64_t e = e0 + int64_t(u) * blockDim.x;
+      if (e + 1 >= e_end) break;
+      int lo = 0, hi = nr - 1;  // the last rule whose list starts at or before e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      if (e + 1 < off[lo + 1] && tb[u] - ta[u] != step[lo]) ok[lo] = 0;
+    }
   }
   __syncthreads();
   if (tid < nr) {
