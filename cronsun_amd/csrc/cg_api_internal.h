@@ -71,8 +71,9 @@ struct RulesStore {
   DBuf<int32_t> nids, gids, ex, group_nodes, rule_job;
   // next_same[r]: the next rule of r's job with r's Cmd key (rule_key), or -1
   // (Job.Cmds keeps the last included rule per key, job.go:604-609); only
-  // uploaded when some job repeats a key (has_dup)
-  DBuf<int32_t> next_same;
+  // uploaded when some job repeats a key (has_dup); prev_same[r] the previous
+  // one (k_rule_nodes sweeps each key's chain from its last rule back)
+  DBuf<int32_t> next_same, prev_same;
   bool has_dup = false;
   DBuf<uint8_t> group_exists, job_pause;
   int32_t n_nodes = 0, n_groups = 0, n_rules = 0, n_jobs = 0;
@@ -80,7 +81,7 @@ struct RulesStore {
   void release() {
     nid_off.release(); gid_off.release(); ex_off.release(); group_off.release();
     nids.release(); gids.release(); ex.release(); group_nodes.release(); rule_job.release();
-    next_same.release();
+    next_same.release(); prev_same.release();
     group_exists.release(); job_pause.release();
   }
 };

@@ -51,6 +51,7 @@ struct RulesDev {
   const int32_t* group_nodes;
   const uint8_t* group_exists;
   const int32_t* next_same;  // next rule of the job with the same Cmd key, -1; null: none repeats
+  const int32_t* prev_same;  // the previous one, -1 (with next_same)
   int32_t R, G, N, words;
 };
 
@@ -97,12 +98,15 @@ __device__ void rule_bitmap(const RulesDev& d, int mode, int64_t q, uint32_t* bm
   wave_sync_lds();
 }
 
-// One wave per rule r: r's node set (rule_bitmap), minus the node sets of the
+// One wave per rule r: r's node set (rule_bitmap) minus the node sets of the
 // later rules of r's job with the same Cmd key -- Job.Cmds' map keeps the
 // last included rule per Job.ID+Rule.ID (job.go:604-609) -- then either the
 // count (WRITE false) or the ballot/prefix compaction of the set bits into the
-// rule-major pairs (WRITE true).  With repeated keys each wave has a second
-// bitmap (sh) for the later rules.
+// rule-major pairs (WRITE true).  With repeated keys the wave of a key's last
+// rule sweeps the key's rules from last to first, keeping the union of the
+// later ones' sets in a second bitmap (sh): every rule's set is built once
+// (a job with k rules of one key costs k bitmap builds, not k^2 / 2); the
+// other rules' waves have nothing to do.
 template <bool WRITE>
 __global__ __launch_bounds__(256) void k_rule_nodes(RulesDev d, int mode, int wpb,
                                                      int32_t* __restrict__ rn_cnt,
@@ -112,45 +116,50 @@ __global__ __launch_bounds__(256) void k_rule_nodes(RulesDev d, int mode, int wp
   extern __shared__ uint32_t bm_all[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   if (wave >= wpb) return;
-  const int per = d.next_same ? 2 : 1;
-  uint32_t* bm = bm_all + size_t(wave) * per * d.words;
-  uint32_t* sh = bm + d.words;
+  const bool dup = d.next_same != nullptr;
+  uint32_t* bm = bm_all + size_t(wave) * (dup ? 2 : 1) * d.words;
+  uint32_t* sh = bm + d.words;  // dup: union of the later same-key rules' sets
   for (int64_t r = int64_t(blockIdx.x) * wpb + wave; r < d.R; r += int64_t(gridDim.x) * wpb) {
-    rule_bitmap(d, mode, r, bm, lane);
-    if (d.next_same) {
-      for (int32_t q = d.next_same[r]; q >= 0; q = d.next_same[q]) {
-        rule_bitmap(d, mode, q, sh, lane);
-        for (int w = lane; w < d.words; w += 64) bm[w] &= ~sh[w];
-        wave_sync_lds();
-      }
+    if (dup) {
+      if (d.next_same[r] >= 0) continue;  // the key's last rule sweeps it
+      for (int w = lane; w < d.words; w += 64) sh[w] = 0;
     }
-    if (!WRITE) {
-      int32_t c = 0;
-      for (int w = lane; w < d.words; w += 64) c += __popc(bm[w]);
-      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-      if (lane == 0) rn_cnt[r] = c;
-    } else {
-      int64_t pos = rn_off[r];
-      for (int base = 0; base < d.words; base += 64) {
-        int w = base + lane;
-        uint32_t bits = w < d.words ? bm[w] : 0u;
-        int32_t c = __popc(bits);
-        int32_t inc = c;
-        for (int o = 1; o < 64; o <<= 1) {
-          int32_t y = __shfl_up(inc, o, 64);
-          if (lane >= o) inc += y;
+    int64_t q = r;
+    do {
+      rule_bitmap(d, mode, q, bm, lane);
+      if (!WRITE) {
+        int32_t c = 0;
+        for (int w = lane; w < d.words; w += 64) c += __popc(dup ? bm[w] & ~sh[w] : bm[w]);
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        if (lane == 0) rn_cnt[q] = c;
+      } else {
+        int64_t pos = rn_off[q];
+        for (int base = 0; base < d.words; base += 64) {
+          int w = base + lane;
+          uint32_t bits = w < d.words ? (dup ? bm[w] & ~sh[w] : bm[w]) : 0u;
+          int32_t c = __popc(bits);
+          int32_t inc = c;
+          for (int o = 1; o < 64; o <<= 1) {
+            int32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+          }
+          int64_t p = pos + inc - c;
+          while (bits) {
+            int b = __builtin_ctz(bits);
+            bits &= bits - 1;
+            rn_nodes[p] = w * 32 + b;
+            pair_rule[p] = int32_t(q);
+            p++;
+          }
+          pos += __shfl(inc, 63, 64);
         }
-        int64_t p = pos + inc - c;
-        while (bits) {
-          int b = __builtin_ctz(bits);
-          bits &= bits - 1;
-          rn_nodes[p] = w * 32 + b;
-          pair_rule[p] = int32_t(r);
-          p++;
-        }
-        pos += __shfl(inc, 63, 64);
       }
-    }
+      if (!dup) break;
+      q = d.prev_same[q];
+      if (q >= 0)
+        for (int w = lane; w < d.words; w += 64) sh[w] |= bm[w];
+      wave_sync_lds();
+    } while (q >= 0);
     wave_sync_lds();
   }
 }
@@ -1011,16 +1020,18 @@ int upload_rules(const cg_rules_in* in, RulesStore* st, hipStream_t s) {
   if ((rc = upload(st->group_exists, in->group_exists, G, s))) return rc;
   // Cmd keys: next_same[r] = the next rule of r's job with r's key (Job.Cmds'
   // later-rule-wins map, job.go:604-609), uploaded only when a key repeats
-  std::vector<int32_t> next_same;
+  std::vector<int32_t> next_same, prev_same;
   st->has_dup = false;
   if (in->rule_key && R) {
     next_same.assign(size_t(R), -1);
+    prev_same.assign(size_t(R), -1);
     std::unordered_map<int32_t, int32_t> last;  // key -> the job's latest rule seen (walking back)
     for (int32_t r = R - 1; r >= 0; r--) {
       if (r == R - 1 || in->rule_job[r] != in->rule_job[r + 1]) last.clear();
       auto it = last.find(in->rule_key[r]);
       if (it != last.end()) {
         next_same[size_t(r)] = it->second;
+        prev_same[size_t(it->second)] = r;
         it->second = r;
         st->has_dup = true;
       } else {
@@ -1028,7 +1039,9 @@ int upload_rules(const cg_rules_in* in, RulesStore* st, hipStream_t s) {
       }
     }
   }
-  if (st->has_dup && (rc = upload(st->next_same, next_same.data(), size_t(R), s))) return rc;
+  if (st->has_dup && ((rc = upload(st->next_same, next_same.data(), size_t(R), s)) ||
+                      (rc = upload(st->prev_same, prev_same.data(), size_t(R), s))))
+    return rc;
   st->n_nodes = in->n_nodes;
   st->n_groups = G;
   st->n_rules = R;
@@ -1053,7 +1066,8 @@ int rule_nodes_locked(cg_ctx* c, const RulesStore& st, int mode, int64_t* nnz_ou
   if ((rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(R))))) return rc;
   RulesDev d{st.nid_off.p, st.nids.p, st.gid_off.p, st.gids.p, st.ex_off.p, st.ex.p,
              st.rule_job.p, st.job_pause.p, st.group_off.p, st.group_nodes.p,
-             st.group_exists.p, st.has_dup ? st.next_same.p : nullptr, R, G, N, std::max(words, 1)};
+             st.group_exists.p, st.has_dup ? st.next_same.p : nullptr,
+             st.has_dup ? st.prev_same.p : nullptr, R, G, N, std::max(words, 1)};
   const size_t per = st.has_dup ? 2 : 1;  // a second bitmap per wave for repeated Cmd keys
   int wpb = int(std::min<size_t>(4, std::max<size_t>(1, (64 * 1024) / (per * size_t(d.words) * 4))));
   size_t lds = size_t(wpb) * per * d.words * 4;

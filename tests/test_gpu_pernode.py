@@ -33,13 +33,14 @@ def oracle_rule_nodes(rin, mode):
     return out
 
 
-@pytest.mark.parametrize("keys", [0, 2])
+@pytest.mark.parametrize("keys,per", [(0, (1, 4)), (2, (1, 4)), (1, (6, 12))])
 @pytest.mark.parametrize("mode", [_lib.EXCLUDE_NONE, _lib.EXCLUDE_RULE, _lib.EXCLUDE_CUMULATIVE])
-def test_rule_nodes_vs_oracle(eng, mode, keys):
+def test_rule_nodes_vs_oracle(eng, mode, keys, per):
     """keys 2: Rule.IDs drawn from two values, so a job's rules repeat Cmd keys
     and the join drops a rule on the nodes a later same-key rule takes
-    (job.go:604-609)."""
-    rin = synth.multi_rule_jobs(400, seed=11 + mode, key_choices=keys)
+    (job.go:604-609); keys 1 with 6-12 rules per job: chains of up to 12
+    rules of one key (k_rule_nodes sweeps each chain from its last rule)."""
+    rin = synth.multi_rule_jobs(400, rules_per_job=per, seed=11 + mode, key_choices=keys)
     off, nodes = eng.rule_nodes(rin, mode)
     exp = oracle_rule_nodes(rin, mode)
     for r in range(rin.n_rules):
