@@ -681,8 +681,8 @@ def main():
         workload = (f"config 2: 1M mixed cron rules x {H // 3600}h horizon, {args.zone}, per GPU "
                     f"(job-ID-range shards)" if wl == "config2" else
                     f"config 4: 10M rules x 7d horizon, light spec mix, {args.zone}, job-ID-range shards over N GPUs")
-        if wl == "config2" and args.zone == "UTC" and not args.tick:
-            traffic_src = pmc_traffic("", R, E, ["k_write_cf"], "k_write_cf")
+        if wl in ("config2", "config4") and args.zone == "UTC" and not args.tick:
+            traffic_src = pmc_traffic("" if wl == "config2" else "config4", R, E, ["k_write_cf"], "k_write_cf")
     traffic = traffic_src["bytes"] if traffic_src else None
     achieved = algo_bytes / ksec / 1e9 if ksec > 0 else 0.0
 
