@@ -382,10 +382,12 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[IT], int n, int32_t
 
 // Stable sort of n packed words (offset << 12 | index) held as items by
 // digits of rel = offset - lo: `passes` (1 or 2) passes of log2(D) bits from
-// bit sh of rel up; the sorted words end in pk[0..n).  Ends synchronised.
+// bit sh of rel up (the second from bit sh2 when given: overlapping digits
+// still sort by rel, the last pass deciding); the sorted words end in
+// pk[0..n).  Ends synchronised.
 template <int NW, int D, bool RUNS = false, int IB = kOtIdxBits, int IT = kOtItems>  // IB: bits below the offset; IT: items per thread
 __device__ __forceinline__ void ot_sort(uint32_t (&key)[IT], int n, uint32_t lo, int sh, int passes,
-                                        uint32_t* pk, OtRank<NW, D>& s) {
+                                        uint32_t* pk, OtRank<NW, D>& s, int sh2 = -1) {
   constexpr int B = D == 64 ? 6 : 8;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * IT);
@@ -403,7 +405,7 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[IT], int n, uint32_t lo,
   for (int j = 0; j < IT; j++) {
     const int e = ebase + j * 64 + lane;
     key[j] = e < n ? pk[e] : 0u;
-    dg[j] = (((key[j] >> IB) - lo) >> (sh + B)) & uint32_t(D - 1);
+    dg[j] = (((key[j] >> IB) - lo) >> (sh2 >= 0 ? sh2 : sh + B)) & uint32_t(D - 1);
   }
   ot_rank<NW, D, false, IT>(dg, n, pos, s);  // its first barrier orders the reloads before the stores below
 #pragma unroll
@@ -449,7 +451,7 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
                                                   const int64_t* __restrict__ node_off, int64_t t0,
                                                   uint16_t* __restrict__ toff_out, int32_t* __restrict__ rule_out,
                                                   int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles,
-                                                  int64_t* __restrict__ err) {
+                                                  int64_t* __restrict__ err, int sb) {
   constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
   constexpr uint32_t kLow = (1u << IB) - 1u;
   __shared__ OtRank<4, 64> s;
@@ -490,11 +492,12 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
       if (e < n) rl[e] = rv[j];
     }
   }
-  // by slab; a node's only tile by the whole offset (its last pass is the slab)
+  // by slab (offset >> sb); a node's only tile by the whole offset: bits 0..5,
+  // then its last pass by the slab (offset >> sb: the pre row's digits)
   const int32_t nd = tile_node[t];
   const bool one = tile_base[nd + 1] - tile_base[nd] == 1;
-  if (one) ot_sort<4, 64, false, IB>(key, n, 0u, 0, 2, pk, s);
-  else ot_sort<4, 64, true, IB>(key, n, 0u, kOtSlabBits, 1, pk, s);
+  if (one) ot_sort<4, 64, false, IB>(key, n, 0u, 0, 2, pk, s, sb);
+  else ot_sort<4, 64, true, IB>(key, n, 0u, sb, 1, pk, s);
   int32_t* __restrict__ pt = pre + t * kOtPre;
   if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];  // slabs = the last pass's digits
   auto rule_of = [&](uint32_t v) { return PACK ? int32_t(v & kLow) : rl[v & kLow]; };
@@ -515,7 +518,7 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
       const int32_t ru = rule_of(u), rv2 = rule_of(v);
       const uint32_t ou = u >> IB, ov = v >> IB;
       if (one) bad |= ou > ov || (ou == ov && ru >= rv2);
-      else if ((ou >> kOtSlabBits) == (ov >> kOtSlabBits)) bad |= ru > rv2 || (ru == rv2 && ou >= ov);  // rule-major
+      else if ((ou >> sb) == (ov >> sb)) bad |= ru > rv2 || (ru == rv2 && ou >= ov);  // rule-major
     }
   }
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
@@ -903,7 +906,7 @@ __device__ __forceinline__ void ot_merge_node_pipe(const uint16_t* __restrict__ 
                                                    const int32_t* __restrict__ pq, int M, const int64_t* slab_off,
                                                    int64_t t0, int64_t* __restrict__ tout_n,
                                                    int32_t* __restrict__ rout_n, OtRank<NW, 256>& s, uint32_t* pk,
-                                                   int32_t* ps, int32_t* psrc, int32_t* wsum, bool& bad) {
+                                                   int32_t* ps, int32_t* psrc, int32_t* wsum, bool& bad, int sb) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
   const uint32_t n_src = uint32_t(M) * kOtTile;
   // the first run of whole slabs at or after j0 that a chunk holds: empty and
@@ -928,7 +931,7 @@ __device__ __forceinline__ void ot_merge_node_pipe(const uint16_t* __restrict__ 
   uint32_t key[IT];
   int n_el = int(slab_off[jb] - slab_off[ja]);
   ot_gather_words<IT>(rin_n, ps, psrc, n_el, key, M, n_src);
-  ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
+  ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << sb, 0, ((jb - ja) << sb) > 256 ? 2 : 1, pk, s);
   for (;;) {
     // pk holds run [ja, jb) sorted; the next run's prefixes are in pa / pb
     const int64_t o = slab_off[ja];
@@ -956,7 +959,7 @@ __device__ __forceinline__ void ot_merge_node_pipe(const uint16_t* __restrict__ 
     }
     ot_sync<NW>();
     if (!more) break;
-    ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << kOtSlabBits, 0, jb - ja > 4 ? 2 : 1, pk, s);
+    ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << sb, 0, ((jb - ja) << sb) > 256 ? 2 : 1, pk, s);
   }
 }
 
@@ -984,7 +987,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
                                                        int64_t* __restrict__ mid, unsigned* __restrict__ mid_n,
                                                        int64_t* __restrict__ mid2, unsigned* __restrict__ mid2_n,
                                                        int64_t e_lo, int64_t e_hi, unsigned* __restrict__ ticket,
-                                                       int64_t* __restrict__ err) {
+                                                       int64_t* __restrict__ err, int sb) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
   constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems, kMid2Chunk = 64 * kOtMid2Waves * kOtItems;
   __shared__ OtRank<NW, 256> s;
@@ -1027,7 +1030,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
     const int32_t* __restrict__ pq = pre + (ta + (threadIdx.x < M ? threadIdx.x : 0)) * kOtPre;
     bool bad = false;
     ot_merge_node_pipe<NW, IT, PIN>(tin + lo_n, rin + lo_n, pq, int(M), slab_off, t0, tout + lo_n, rout + lo_n, s, pk,
-                                    ps, psrc, wsum, bad);
+                                    ps, psrc, wsum, bad, sb);
     if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
     continue;
   }
@@ -1065,8 +1068,8 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
       // pass for up to 4 slabs
       const int64_t o = lo_n + slab_off[ja];
       ot_merge_chunk<NW, PACK, IT, PIN>(
-          tin + lo_n, rin + lo_n, int(M), int(slab_off[jb] - slab_off[ja]), uint32_t(ja) << kOtSlabBits,
-          jb - ja > 4 ? 2 : 1,
+          tin + lo_n, rin + lo_n, int(M), int(slab_off[jb] - slab_off[ja]), uint32_t(ja) << sb,
+          ((jb - ja) << sb) > 256 ? 2 : 1,
           [&](int q, int32_t* src) {
             *src = q * kOtTile + pa;  // q == q_own
             return pb - pa;
@@ -1092,7 +1095,8 @@ __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_
                                                     const int64_t* __restrict__ slab_tab,
                                                     int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                     const int64_t* __restrict__ mid,
-                                                    const unsigned* __restrict__ mid_n, int64_t* __restrict__ err) {
+                                                    const unsigned* __restrict__ mid_n, int64_t* __restrict__ err,
+                                                    int sb) {
   constexpr int kChunk = 64 * NW * IT;
   __shared__ OtRank<NW, 256> s;
   __shared__ uint32_t pk[kChunk + kChunk / 32];
@@ -1114,7 +1118,7 @@ __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_
       continue;
     }
     ot_merge_chunk<NW, PACK, IT, PIN>(
-        tin + lo_n, rin + lo_n, int(M), int(n_el), uint32_t(j) << kOtSlabBits, 1,
+        tin + lo_n, rin + lo_n, int(M), int(n_el), uint32_t(j) << sb, 1,
         [&](int q, int32_t* src) {
           const int32_t* pt = pre + (ta + q) * kOtPre;
           *src = q * kOtTile + pt[j];
@@ -1134,7 +1138,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
                                                  const int32_t* __restrict__ pre, int64_t t0,
                                                  int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                  const int64_t* __restrict__ big, const unsigned* __restrict__ big_n,
-                                                 int64_t* __restrict__ err) {
+                                                 int64_t* __restrict__ err, int sb) {
   __shared__ OtRank<4, 64> s;
   __shared__ uint32_t pk[kOtTile + kOtTile / 32];
   __shared__ int32_t rl[kOtTile];
@@ -1146,7 +1150,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
   __shared__ int64_t red[4];
   int32_t* own = reinterpret_cast<int32_t*>(pk);
   const int lane = threadIdx.x & 63, ebase = (threadIdx.x >> 6) * (64 * kOtItems);
-  constexpr uint32_t kSec = (1u << kOtSlabBits) - 1u;
+  const uint32_t kSec = (1u << sb) - 1u;  // seconds of a slab
   const unsigned nb = *big_n;
   for (unsigned task = blockIdx.x; task < nb; task += gridDim.x) {
     const int32_t n = int32_t(big[task] >> 8);
@@ -1208,7 +1212,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
         ot_gather<true, 0, false, kOtItems, false, PIN>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc,
                                                         own, c0, n_el, key, rl);
-        ot_sort<4, 64, bool(CG_OT_MERGE_RUNS)>(key, n_el, uint32_t(j) << kOtSlabBits, 0, 1, pk, s);
+        ot_sort<4, 64, bool(CG_OT_MERGE_RUNS)>(key, n_el, uint32_t(j) << sb, 0, 1, pk, s);
         bool bad = false;
         for (int p = threadIdx.x; p < n_el; p += 256) {
           const uint32_t v = pk[p];
@@ -1463,6 +1467,15 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
   return CG_OK;
 }
 
+// Slab width 2^sb seconds for a window of H <= 4096 s: 64 s, or 32 s when the
+// window fits 64 of them (H <= 2048: a dense node's 30-min window then puts
+// half as many events in a slab, so they fit k_ot_mid's chunks instead of
+// k_ot_big's two reads).  The tile pre rows keep 64 slabs either way.
+#ifndef CG_OT_SLAB32
+#define CG_OT_SLAB32 1
+#endif
+int ot_slab_bits(int64_t H) { return CG_OT_SLAB32 && H <= 2048 ? kOtSlabBits - 1 : kOtSlabBits; }
+
 #ifndef CG_OT_DENSE_BPC
 #define CG_OT_DENSE_BPC 2  // blocks per CU of the dense merge's persistent grid
 #endif
@@ -1471,7 +1484,7 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
 #endif
 // pin: the tiles were stored as packed words offset << 20 | rule (in node_rule2)
 int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st, int64_t* err,
-               int64_t R, bool pin) {
+               int64_t R, bool pin, int sb) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
   // [0] big, [1] mid, [2] the dense merge's node ticket, [3] mid2
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
@@ -1512,25 +1525,25 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
     hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtDenseWaves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
-                       dense_min, INT64_MAX, big_n + 2, err);
+                       dense_min, INT64_MAX, big_n + 2, err, sb);
     if (early)  // k_ot_mid's 16-wave form behind the dense merge, beside the sparse one
       hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, c->st_ot, toff, c->node_rule2.p,
                          c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
-                         big_n + 3, err);
+                         big_n + 3, err, sb);
     hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
-                       mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err);
+                       mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err, sb);
     // k_ot_mid's queue is filled by the 4-wave merge only (the 8-wave merge's
     // chunk holds any slab of <= 8192 events): it runs beside the dense merge
     hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, st, toff, c->node_rule2.p,
                        c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid,
-                       big_n + 1, err);
+                       big_n + 1, err, sb);
     (void)hipEventRecord(c->ot_join, c->st_ot);
     (void)hipStreamWaitEvent(st, c->ot_join, 0);
     if (!early)
       hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
                          c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
-                         big_n + 3, err);
+                         big_n + 3, err, sb);
   };
   if (pack && pin)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,
@@ -1545,7 +1558,7 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   auto big = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff, c->node_rule2.p,
                        c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
-                       err);
+                       err, sb);
   };
   pin ? big(k_ot_big<true>) : big(k_ot_big<false>);
   return cg_hip_check(hipGetLastError(), "time-order kernels");
@@ -1565,9 +1578,10 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
   // the tiles stored as packed words when every rule index is below 2^20
   const bool pack = CG_OT_TILE_PACK && CG_OT_PACK && c->pn_R <= (int64_t(1) << kOtRuleBits);
+  const int sb = ot_slab_bits(H);
   auto tile = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p, c->ts_tile_node.p,
-                       c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p, c->ts_base.p + N, err);
+                       c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p, c->ts_base.p + N, err, sb);
   };
   if (in_mode == kInPacked) {
     if (!pack) return cg_fail(CG_EINVAL, "time order: packed lists need rule indices below 2^20");
@@ -1577,7 +1591,7 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   } else {
     pack ? tile(k_ot_tile<0, true>) : tile(k_ot_tile<0, false>);
   }
-  return order_tail(c, node_off, N, t0, H, st, err, c->pn_R, pack);
+  return order_tail(c, node_off, N, t0, H, st, err, c->pn_R, pack, sb);
 }
 
 // The per-node writer and tile sort in one (k_node_tile), then the merge: the
@@ -1594,7 +1608,7 @@ int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int6
   hipLaunchKernelGGL(k_node_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec, a.recs,
                      a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
                      reinterpret_cast<uint16_t*>(c->node_time2.p), c->node_rule2.p, c->ts_hist.p, n_tiles, err);
-  return order_tail(c, a.node_off, a.N, a.t0, 4096, st, err, c->pn_R, false);  // windows <= 4096 s; 16-bit tiles
+  return order_tail(c, a.node_off, a.N, a.t0, 4096, st, err, c->pn_R, false, kOtSlabBits);  // 16-bit tiles, 64-s slabs
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {

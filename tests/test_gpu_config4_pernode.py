@@ -6,8 +6,8 @@ One rank's share at N = 8: 1.25M rules of config 4's 10M-rule set (the
 over 10k nodes / 500 groups (synth.rules_for_nodes of the whole 10M-job set,
 sliced to the rank's job-ID range, as bench.py --per-node does).  The local
 rule indices pass 2^20, so the time-ordered lists take the unpacked path
-(16-bit offsets + int32 rules).  One-hour windows spread over the 7 days, in
-rule order and in (time, rule) order: every window's node-event total equals
+(16-bit offsets + int32 rules).  One-hour windows spread over the 7 days and
+one 30-min window (the bench's), in rule order and in (time, rule) order: every window's node-event total equals
 sum_r fires(r) x |nodes(r)| (oracle fire counts, the GPU join's degrees) and
 48 seeded nodes' lists are bit-exact against each node's own filter over the
 rank's jobs (node/node.go:121-158 -> Job.Cmds, job.go:591-614) composed with
@@ -49,7 +49,8 @@ def share():
 def _windows():
     t0 = synth.T0_2026
     hours = [0, 29, 58, 87, 116, 145, 167]  # spread over the 7 days, the last hour included
-    return [(t0 + 3600 * h, t0 + 3600 * (h + 1)) for h in hours]
+    # and one 30-min window as bench.py --per-node runs them (32-s time-order slabs)
+    return [(t0 + 3600 * h, t0 + 3600 * (h + 1)) for h in hours] + [(t0 + 3600 * 100 + 1800, t0 + 3600 * 101)]
 
 
 def test_config4_per_node_rank_share(share):

@@ -298,7 +298,8 @@ def progression_rules(R, n_nodes):
 
 @pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("R,N,secs,star_every", [(1200, 3, 3600, 13), (2600, 2, 4096, 2), (64, 1, 61, 3),
-                                                 (12000, 1, 120, 1), (40, 1, 4096, 10**9), (200, 1, 3600, 2)])
+                                                 (12000, 1, 120, 1), (40, 1, 4096, 10**9), (200, 1, 3600, 2),
+                                                 (1200, 1, 1800, 1), (2600, 2, 2048, 2)])
 def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
     """The one-pass time order on nodes far larger than one LDS chunk:
     every-second rules put > 4096 events into one 64-s slab (the slab is
@@ -310,7 +311,9 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
     on one node over 4096 s: ~7 k events in two tiles, merge runs of dozens of
     slabs (sorted in two 8-bit passes).  200 rules on one node, every other one
     every second, over 1 h: ~6.5 k events per slab, each merged by k_ot_mid's
-    8192-event chunk.
+    8192-event chunk.  Windows <= 2048 s (32-s slabs): 1200 every-second
+    rules on one node over 30 min (38 k events per slab -> k_ot_big), 2600
+    rules on 2 nodes over 2048 s (> 1024 tiles per node).
     Against the oracle's lists sorted by (time, rule)."""
     specs = [PROGRESSION_MIX[0] if i % star_every == 0 else PROGRESSION_MIX[1 + i % (len(PROGRESSION_MIX) - 1)]
              for i in range(R)]
@@ -334,7 +337,7 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
         assert b - a == len(exp_t), n
         assert np.array_equal(time2[a:b], exp_t[order]), n
         assert np.array_equal(rule2[a:b], exp_r[order]), n
-    if R == 2600:
+    if R == 2600 and secs == 4096:
         assert (np.diff(node_off) > 1024 * 4096).all()
     if R == 200:  # every slab between a merge chunk and a k_ot_mid chunk
         per_slab = node_off[1] / (secs / 64)
@@ -345,26 +348,30 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
 
 @pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("case", ["mid", "dense", "mid2"])
-def test_per_node_time_ordered_slab_classes(eng, writer, case):
-    """Each path of the merge by slab size, on one node over 1 h, against the
-    oracle's (time, rule) lists:
-    mid    a sparse node (<= 2048 events per 64-s slab on average, 4-wave
-           merge) with one heavy slab: 100 rules every second of minute 5
-           put 6 k events into slab 0 -> k_ot_mid (8-wave, 8192 events);
-    dense  100 every-second rules among 200: ~6.5 k events per slab on
-           average (> 2048) -> the 8-wave merge (persistent grid, own stream);
-    mid2   200 every-second rules among 400: ~13 k per slab -> k_ot_mid's
+@pytest.mark.parametrize("secs", [3600, 1800])
+def test_per_node_time_ordered_slab_classes(eng, writer, case, secs):
+    """Each path of the merge by slab size, on one node over 1 h (64-s slabs)
+    and over 30 min (windows <= 2048 s: 32-s slabs, ot_slab_bits), against
+    the oracle's (time, rule) lists; k = 64 / slab width rules per unit:
+    mid    a sparse node (<= 2048 events per 64 s on average, 4-wave merge)
+           with one heavy slab: 100 k rules every second of minute 5 put
+           > 4096 events into one slab -> k_ot_mid (8-wave, 8192 events);
+    dense  100 k every-second rules among 200 k: > 2048 events per 64 s on
+           average -> the 8-wave merge (persistent grid, own stream);
+    mid2   200 k every-second rules among 400 k: ~13 k per slab -> k_ot_mid's
            16-wave form (16384 events)."""
+    w = 64 if secs > 2048 else 32
+    k = 64 // w
     mix = PROGRESSION_MIX[1:]
     if case == "mid":
-        specs = ["* 5 * * * *" if i % 2 == 0 else mix[i % len(mix)] for i in range(200)]
+        specs = ["* 5 * * * *" if i % 2 == 0 else mix[i % len(mix)] for i in range(200 * k)]
     else:
-        R = 200 if case == "dense" else 400
+        R = (200 if case == "dense" else 400) * k
         specs = [PROGRESSION_MIX[0] if i % 2 == 0 else mix[i % len(mix)] for i in range(R)]
     rin = progression_rules(len(specs), 1)
     scheds = [cron.Parse(x) for x in specs]
-    t0 = synth.T0_2026 + 11 * DAY + 297  # minute 5 of the hour at offsets 2..61: all in slab 0
-    t1 = t0 + 3600
+    t0 = synth.T0_2026 + 11 * DAY + 297  # minute 5 of the hour at offsets 2..61
+    t1 = t0 + secs
     node_off, off2, time2, rule2 = _ordered_per_node(eng, writer, scheds, product_zone("UTC"), t0, t1, rin)
     assert np.array_equal(off2, node_off)
     arr = O.sched_array(oracle_parse_all(specs))
@@ -374,8 +381,8 @@ def test_per_node_time_ordered_slab_classes(eng, writer, case):
     assert node_off[1] == len(exp_t)
     assert np.array_equal(time2, exp_t[order])
     assert np.array_equal(rule2, exp_r[order])
-    per_slab = np.bincount((exp_t - t0 - 1) // 64)
-    avg = len(exp_t) / np.ceil(3600 / 64)
+    per_slab = np.bincount((exp_t - t0 - 1) // w)
+    avg = len(exp_t) / np.ceil(secs / 64)  # the dense split's events per 64 s
     if case == "mid":
         assert avg <= 2048 and 4096 < per_slab.max() <= 8192
     elif case == "dense":
