@@ -105,6 +105,7 @@ struct AsyncSet {
   uint64_t plan_zone = 0;
   int64_t plan_t0 = 0, plan_t1 = 0;
   hipEvent_t written = nullptr, w0 = nullptr, w1 = nullptr;  // writer done; writer start/end
+  bool written_w1 = false;  // the set's writer-done event is w1 (no walk kernel)
   bool pending = false;  // a call on this set whose record has not been checked
   bool armed = false;    // stuck flag holds ~0 (set once; every scan re-arms it)
   int64_t R = 0, cap = 0;

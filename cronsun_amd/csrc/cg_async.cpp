@@ -25,6 +25,13 @@
 
 using namespace cg;
 
+#ifndef CG_ASYNC_ONE_EVENT
+#define CG_ASYNC_ONE_EVENT 1
+#endif
+#ifndef CG_ASYNC_NO_TIMING
+#define CG_ASYNC_NO_TIMING 0  // diagnostic: no writer timing events (kernel_ms then meaningless)
+#endif
+
 namespace {
 
 // the record of a finished call on set a: fold its errors and writer time in
@@ -32,7 +39,7 @@ void check_set(cg_ctx* c, AsyncSet& a) {
   if (!a.pending) return;
   a.pending = false;
   float ms = 0.f;
-  if (hipEventElapsedTime(&ms, a.w0, a.w1) == hipSuccess) {
+  if (!CG_ASYNC_NO_TIMING && hipEventElapsedTime(&ms, a.w0, a.w1) == hipSuccess) {
     c->wr_ms_sum += ms;
     c->wr_n++;
   }
@@ -156,7 +163,7 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   AsyncSet& a = c->as[k];
   // the set was last used kAsyncSets calls ago: its writer must be done
   // before the host restages its plan or the count stream rewrites its runs
-  HIPCHK(hipEventSynchronize(a.written));
+  HIPCHK(hipEventSynchronize(a.written_w1 ? a.w1 : a.written));
   check_set(c, a);
   const int64_t R = int64_t(s->n);
   bool empty = false;
@@ -178,14 +185,17 @@ int cg_expand_device_async(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64
   // the writer after the previous call's writer, once this call's scan is done
   HIPCHK(hipStreamWaitEvent(c->st, c->cs_done[k], 0));
   const bool has_walk = (a.plan.flags & (kPlanT0Walk | kPlanWalkSegs)) != 0;
-  (void)hipEventRecord(a.w0, c->st);
+  if (!CG_ASYNC_NO_TIMING) (void)hipEventRecord(a.w0, c->st);
   launch_write_cf(s->d, pa, a.run_anchor.p, a.run_count.p, a.run_dmask.p, a.run_off.p, nruns, a.block_run.p, cap,
                   c->times.p, c->write_blocks, c->st);
-  (void)hipEventRecord(a.w1, c->st);
+  if (!CG_ASYNC_NO_TIMING) (void)hipEventRecord(a.w1, c->st);
   if (has_walk)
     launch_write_walk(s->d, R, pa, a.run_anchor.p, a.run_count.p, a.run_dmask.p, a.run_off.p, cap, c->times.p,
                       c->st);
-  HIPCHK(hipEventRecord(a.written, c->st));
+  // the set is free again once its writer is done: without a walk that is w1
+  // (one event packet fewer between back-to-back writers)
+  a.written_w1 = CG_ASYNC_ONE_EVENT && !has_walk && !CG_ASYNC_NO_TIMING;
+  if (!a.written_w1) HIPCHK(hipEventRecord(a.written, c->st));
   HIPCHK(hipGetLastError());
   a.R = R;
   a.cap = cap;
