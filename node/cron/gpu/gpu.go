@@ -579,10 +579,13 @@ func (cm *Comm) NodeOffsets(nNodes int) (start, base []int64, err error) {
 	return start[:nNodes], base, nil
 }
 
-// GatherNodeCSR gathers every rank's last per-node result (rule order) on
-// root into device buffers (root only; pass 0 elsewhere), in chunks whose peer
-// bytes stay within budget; ruleBase is this rank's first global rule.
-// Returns the global node-event total.
+// GatherNodeCSR gathers every rank's last per-node result on root into device
+// buffers (root only; pass 0 elsewhere), in chunks whose peer bytes stay within
+// budget; ruleBase is this rank's first global rule.  Rule-ordered results are
+// concatenated in rank (job-ID) order; when every rank's result is in (time,
+// rule) order (SetNodeOrder(NodeOrderTime)) root merges each node's slices
+// into one byTime list (cron.go:64-79,220).  Returns the global node-event
+// total.
 func (cm *Comm) GatherNodeCSR(root int, ruleBase, budget int64, dOff, dTime, dRule uintptr, cap int64) (int64, error) {
 	defer runtime.KeepAlive(cm)
 	var n C.int64_t
@@ -593,4 +596,65 @@ func (cm *Comm) GatherNodeCSR(root int, ruleBase, budget int64, dOff, dTime, dRu
 		return int64(n), lastErr(rc)
 	}
 	return int64(n), nil
+}
+
+// MergeRanks merges, in place, the time-ordered rank slices of every node of a
+// per-node CSR already placed in device buffers (cg_node_csr_merge_ranks):
+// runBounds holds nNodes*(world+1) ascending positions, run g of node n being
+// [runBounds[n*(world+1)+g], runBounds[n*(world+1)+g+1]).  Equal times end in
+// rank (= global rule) order.  budget bounds the scratch copy (bytes).
+func (e *Engine) MergeRanks(nNodes, world int, runBounds []int64, dTime, dRule uintptr, budget int64) error {
+	e.mu.Lock()
+	defer e.mu.Unlock()
+	if nNodes == 0 || world <= 1 {
+		return nil
+	}
+	if len(runBounds) < nNodes*(world+1) {
+		return fmt.Errorf("cronsun gpu: run bounds: %d positions for %d nodes x %d ranks", len(runBounds), nNodes, world)
+	}
+	rb := (*C.int64_t)(C.malloc(C.size_t(8 * nNodes * (world + 1))))
+	defer C.free(unsafe.Pointer(rb))
+	copy(unsafe.Slice((*int64)(unsafe.Pointer(rb)), nNodes*(world+1)), runBounds)
+	rc := C.cg_node_csr_merge_ranks(e.ctx, C.int32_t(nNodes), C.int32_t(world), rb,
+		(*C.int64_t)(unsafe.Pointer(dTime)), (*C.int32_t)(unsafe.Pointer(dRule)), C.int64_t(budget))
+	runtime.KeepAlive(e)
+	if rc != 0 {
+		return lastErr(rc)
+	}
+	return nil
+}
+
+// GatherPlan is the gather's chunk plan for per-node counts counts[g*nNodes+n]
+// (host only): chunk i = {first node, end node, part, parts}; a node with more
+// peer events than the budget is split into parts.
+func GatherPlan(counts []int64, world, nNodes, root int, budget int64) ([][4]int64, error) {
+	if len(counts) < world*nNodes {
+		return nil, fmt.Errorf("cronsun gpu: gather plan: %d counts for %d ranks x %d nodes", len(counts), world, nNodes)
+	}
+	var n C.int64_t
+	words := world * nNodes
+	if words < 1 {
+		words = 1
+	}
+	cc := (*C.int64_t)(C.malloc(C.size_t(8 * words)))
+	defer C.free(unsafe.Pointer(cc))
+	copy(unsafe.Slice((*int64)(unsafe.Pointer(cc)), world*nNodes), counts)
+	// sizing call: *n_chunks is set, CG_ECAPACITY when there are any chunks
+	if rc := C.cg_comm_gather_plan(cc, C.int32_t(world), C.int32_t(nNodes), C.int32_t(root), C.int64_t(budget), nil, 0, &n); rc != 0 && rc != C.CG_ECAPACITY {
+		return nil, lastErr(rc)
+	}
+	out := make([][4]int64, int(n))
+	if n == 0 {
+		return out, nil
+	}
+	buf := (*C.int64_t)(C.malloc(C.size_t(8 * 4 * int(n))))
+	defer C.free(unsafe.Pointer(buf))
+	if rc := C.cg_comm_gather_plan(cc, C.int32_t(world), C.int32_t(nNodes), C.int32_t(root), C.int64_t(budget), buf, n, &n); rc != 0 {
+		return nil, lastErr(rc)
+	}
+	flat := unsafe.Slice((*int64)(unsafe.Pointer(buf)), 4*int(n))
+	for i := range out {
+		copy(out[i][:], flat[4*i:4*i+4])
+	}
+	return out, nil
 }
