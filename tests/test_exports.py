@@ -53,3 +53,12 @@ def test_library_does_not_link_oracle():
     assert "or_spec_next" not in out and "or_expand" not in out
     deps = subprocess.run(["readelf", "-d", LIB], capture_output=True, text=True, check=True).stdout
     assert "oracle" not in deps
+
+
+def test_go_binding_calls_only_declared_symbols():
+    """The cgo package (node/cron/gpu/gpu.go, uncompiled here: no Go
+    toolchain) calls only entry points the header declares."""
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "node", "cron", "gpu", "gpu.go")).read()
+    called = set(re.findall(r"\bC\.(cg_[a-z0-9_]+)\s*\(", src))
+    assert called and not (called - set(declared())), sorted(called - set(declared()))
