@@ -218,7 +218,11 @@ constexpr int kOtMid2Waves = 16;  // its 16-wave form (slabs of <= 16384 events;
 #define CG_OT_DENSE_WAVES 8
 #endif
 constexpr int kOtDenseWaves = CG_OT_DENSE_WAVES;  // the dense nodes' merge: waves per block (8 or 16)
-static_assert(64 * kOtMid2Waves * kOtItems <= (1 << kOtIdxBits) && 64 * kOtDenseWaves * kOtItems <= (1 << kOtIdxBits),
+#ifndef CG_OT_DENSE_ITEMS
+#define CG_OT_DENSE_ITEMS 16
+#endif
+constexpr int kOtDenseItems = CG_OT_DENSE_ITEMS;  // its events per thread of a chunk
+static_assert(64 * kOtMid2Waves * kOtItems <= (1 << kOtIdxBits) && 64 * kOtDenseWaves * kOtDenseItems <= (1 << kOtIdxBits),
               "every chunk's element index fits the packed words' index bits");
 static_assert(kOtMergeWaves <= 8 && 12 + kOtIdxBits <= 32, "packed words");
 constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
@@ -1500,7 +1504,7 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   const bool pack = CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
   OtQueues oq{c->ts_off.p, slab_tab + int64_t(N) * kOtPre, slab_tab + int64_t(N) * kOtPre + int64_t(N) * kOtSlabs,
               big_n, big_n + 1, big_n + 3, node_off, dense_min, 64 * kOtMergeWaves * kOtMergeItems,
-              64 * kOtDenseWaves * kOtItems, (CG_OT_EARLY_QUEUE || (pack && pin && CG_OT_PIPE)) ? 1 : 0};
+              64 * kOtDenseWaves * kOtDenseItems, (CG_OT_EARLY_QUEUE || (pack && pin && CG_OT_PIPE)) ? 1 : 0};
   const bool early = oq.on != 0;
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab, oq);
   if (!c->st_ot) {  // created together: the ctx holds all three or none
@@ -1547,13 +1551,13 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   };
   if (pack && pin)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,
-           k_ot_merge<kOtDenseWaves, true, kOtItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,
+           k_ot_merge<kOtDenseWaves, true, kOtDenseItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,
            k_ot_mid<kOtMid2Waves, true, kOtItems, true>);
   else if (pack)
-    merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems>, k_ot_merge<kOtDenseWaves, true, kOtItems, true>,
+    merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems>, k_ot_merge<kOtDenseWaves, true, kOtDenseItems, true>,
            k_ot_mid<kOtMidWaves, true>, k_ot_mid<kOtMid2Waves, true>);
   else
-    merges(k_ot_merge<kOtMergeWaves, false, kOtMergeItems>, k_ot_merge<kOtDenseWaves, false, kOtItems, true>,
+    merges(k_ot_merge<kOtMergeWaves, false, kOtMergeItems>, k_ot_merge<kOtDenseWaves, false, kOtDenseItems, true>,
            k_ot_mid<kOtMidWaves, false>, k_ot_mid<kOtMid2Waves, false>);
   auto big = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff, c->node_rule2.p,
