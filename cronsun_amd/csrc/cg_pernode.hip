@@ -591,7 +591,21 @@ __device__ __forceinline__ void out_store(T* p, T v) {
   *p = v;
 #endif
 }
-constexpr int kNodeMajorDefault = 0;  // writer task order: 0 band-major, 1 node-major
+// Writer task order: 0 band-major (every node's segment of band 0, then band
+// 1, ...: a band's fire lists stay in L2 for the gathers), 1 node-major (the
+// segments of one node in turn: the concurrent write fronts stay in a few
+// nodes' lists).  Rule-ordered lists are written node-major (same-box A/B,
+// profiles/r05_ab_writer_order.txt: config 3 150.4 -> 146.9 ms, pernode
+// -3 %); the time-order writer's packed words band-major (node-major: config
+// 3 in time order +1 %, pernode equal).
+#ifndef CG_NODE_MAJOR
+#define CG_NODE_MAJOR 1
+#endif
+#ifndef CG_NODE_MAJOR_ORDERED
+#define CG_NODE_MAJOR_ORDERED 0
+#endif
+constexpr int kNodeMajorDefault = CG_NODE_MAJOR;
+constexpr int kNodeMajorOrdered = CG_NODE_MAJOR_ORDERED;  // the time-order writer (packed words / 16-bit offsets)
 
 // OUT (windows <= 4096 s whose lists the time-order tile sort reads next):
 // kInTimes int64 times + int32 rules; kIn16 the times as 16-bit offsets
@@ -1274,11 +1288,11 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
       if (in_mode == kInPacked)
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
                            dim3(256), 0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,
-                           c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
+                           c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorOrdered);
       else
         hipLaunchKernelGGL((k_node_write<0, kIn16>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
                            dim3(256), 0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,
-                           c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, node_major);
+                           c->times.p, N, K, B, cap, c->pn_tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorOrdered);
     } else if (NK > 0 && cap > 0) {
 #define CG_NW(V)                                                                                    \
   hipLaunchKernelGGL((k_node_write<V, kInTimes>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256), \
@@ -1542,12 +1556,12 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
                            dim3(256), 0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p,
                            a.times.p, N, K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p,
-                           kNodeMajorDefault);
+                           kNodeMajorOrdered);
       else
         hipLaunchKernelGGL((k_node_write<0, kIn16>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
                            dim3(256), 0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p,
                            a.times.p, N, K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p,
-                           kNodeMajorDefault);
+                           kNodeMajorOrdered);
       if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, t1 - t0, st, in_mode, a.res_dev + 2)))
         return rc;
     } else {
