@@ -596,8 +596,8 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 // segments of one node in turn: the concurrent write fronts stay in a few
 // nodes' lists).  Rule-ordered lists are written node-major (same-box A/B,
 // profiles/r05_ab_writer_order.txt: config 3 150.4 -> 146.9 ms, pernode
-// -3 %); the time-order writer's packed words band-major (node-major: config
-// 3 in time order +1 %, pernode equal).
+// -3 %, config 4 per node -2 %); the time-order writer's packed words
+// band-major (node-major: config 3 in time order +1 %, pernode equal).
 #ifndef CG_NODE_MAJOR
 #define CG_NODE_MAJOR 1
 #endif
