@@ -292,6 +292,21 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
   seg_pair[t] = lo;
 }
 
+// Periodic rules (RuleInfo / PairRec st < 0): a window's fires that step by s
+// with a wrap every m fires, fire p = A + (v / m) * P + (v % m) * s with
+// v = p + ph -- e.g. `0 */13 * * * *` over (t0, t0 + 1 h]: minutes 13, 26,
+// 39, 52, then 60 (the next hour's minute 0).  P is 60 or 3600; st packs
+// s (bits 0-11), m (12-17), ph (18-23) and P (bit 24: 3600) under bit 31.
+__device__ __forceinline__ int64_t periodic_fire(int32_t st, int64_t A, int32_t p) {
+  const uint32_t s = uint32_t(st) & 0xFFFu, m = (uint32_t(st) >> 12) & 63u, ph = (uint32_t(st) >> 18) & 63u;
+  const uint32_t P = (uint32_t(st) >> 24) & 1u ? 3600u : 60u;
+  const uint32_t v = uint32_t(p) + ph;  // < 2^24: fires of one rule in one window
+  uint32_t k = uint32_t(float(v) * (1.0f / float(m)));
+  const int32_t r = int32_t(v) - int32_t(k * m);
+  k = r < 0 ? k - 1u : (r >= int32_t(m) ? k + 1u : k);
+  return A + int64_t(k) * P + int64_t(v - k * m) * s;
+}
+
 // Per rule of the window's rule-major CSR, one 16-byte RuleInfo: its fire
 // count, the band-relative index of its first fire, and whether its fires
 // form an arithmetic progression {first fire - t0, stride} (stride 0: they do
@@ -306,6 +321,12 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
 #ifndef CG_NODE_AP
 #define CG_NODE_AP 1
 #endif
+#ifndef CG_NODE_TILE_FUSED
+#define CG_NODE_TILE_FUSED 0  // the per-node writer fused with the time-order tile sort (k_node_tile; A/B only)
+#endif
+#ifndef CG_NODE_PERIODIC
+#define CG_NODE_PERIODIC 0  // 1: periodic records (A/B: slower, profiles/r05_ab_periodic.txt; the fused tile writer reads progressions only)
+#endif
 constexpr int kApRules = 256;
 __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ rule_off,
                                                     const int64_t* __restrict__ times, int64_t R, int64_t t0,
@@ -314,6 +335,8 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
   __shared__ int64_t off[kApRules + 1];
   __shared__ int64_t step[kApRules];
   __shared__ int32_t ok[kApRules];
+  __shared__ int32_t pst[kApRules];  // a periodic candidate's packed st (0: none)
+  __shared__ int64_t pA[kApRules];   // and its A
   const int64_t r0 = int64_t(blockIdx.x) * kApRules;
   const int nr = int(R - r0 < kApRules ? R - r0 : kApRules);
   const int tid = threadIdx.x;
@@ -334,6 +357,7 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
     off[tid] = a;
     step[tid] = cnt > 1 ? times[a + 1] - first : 1;
     ok[tid] = CG_NODE_AP;
+    pst[tid] = 0;
   }
   if (tid == 0) off[nr] = rule_off[r0 + nr];
   __syncthreads();
@@ -366,13 +390,70 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
     }
   }
   __syncthreads();
+  // Not a progression: a periodic candidate from the first steps (one thread
+  // per rule: steps of s with a wrap g every m fires), then every fire of the
+  // candidates checked against the formula, lanes over the block's events.
+  constexpr bool kPeriodic = CG_NODE_PERIODIC && !CG_NODE_TILE_FUSED;
+  bool any = false;
+  if (kPeriodic && tid < nr && cnt >= 3 && !ok[tid]) {
+    const int64_t* __restrict__ t = times + off[tid];
+    const int lim = cnt - 1 < 130 ? int(cnt - 1) : 130;  // steps looked at
+    const int64_t d0 = t[1] - t[0];
+    int i = 1;
+    while (i < lim && t[i + 1] - t[i] == d0) i++;
+    if (i < lim) {
+      const int64_t b = t[i + 1] - t[i];
+      int64_t sv, g;
+      int m, ph;
+      const bool h2 = i == 1 && cnt >= 4 && t[3] - t[2] == b;  // the first step is the wrap
+      int j = h2 ? 2 : i + 1;
+      const int64_t sj = h2 ? b : d0;
+      while (j < lim && t[j + 1] - t[j] == sj) j++;
+      if (h2) {  // fire 0 is the last phase; the next wrap after step j
+        sv = b;
+        g = d0;
+        m = j < lim ? j : int(cnt - 1 > 1 ? cnt - 1 : 1);
+        ph = m - 1;
+      } else {  // fires 0..i in one period (fire i the last phase)
+        sv = d0;
+        g = b;
+        m = j < lim ? j - i : int(i + 1 > cnt - 1 - i ? i + 1 : cnt - 1 - i);
+        ph = m - 1 - i;
+      }
+      const int64_t P = int64_t(m - 1) * sv + g;
+      if (sv > 0 && sv < 4096 && g > 0 && m >= 2 && m <= 63 && ph >= 0 && ph < m && (P == 60 || P == 3600)) {
+        const int64_t A = t[0] - int64_t(ph) * sv;
+        if (A - t0 >= INT32_MIN && A - t0 <= INT32_MAX) {
+          pst[tid] = int32_t(0x80000000u | uint32_t(sv) | (uint32_t(m) << 12) | (uint32_t(ph) << 18) |
+                             (P == 3600 ? (1u << 24) : 0u));
+          pA[tid] = A;
+          any = true;
+        }
+      }
+    }
+  }
+  if (kPeriodic && __syncthreads_or(any)) {
+    for (int64_t e = off[0] + tid; e < e_end; e += blockDim.x) {
+      int lo = 0, hi = nr - 1;  // the last rule whose list starts at or before e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= e) lo = mid;
+        else hi = mid - 1;
+      }
+      const int32_t ps = pst[lo];
+      if (ps != 0 && times[e] != periodic_fire(ps, pA[lo], int32_t(e - off[lo]))) pst[lo] = 0;
+    }
+    __syncthreads();
+  }
   if (tid < nr) {
     const int64_t rel = first - t0, s = step[tid];
     const bool prog = cnt > 0 && ok[tid] && rel >= 0 && rel <= INT32_MAX && s > 0 && s <= INT32_MAX;
+    const int32_t ps = prog || !kPeriodic ? 0 : pst[tid];
     // counts and band-relative indices are < 2^30 (k_seg_records checks the
     // band span and fails the call otherwise)
-    info[r0 + tid] = RuleInfo{int32_t(cnt), int32_t(off[tid] - band_lo), prog ? int32_t(rel) : 0,
-                              prog ? int32_t(s) : 0};
+    info[r0 + tid] = RuleInfo{int32_t(cnt), int32_t(off[tid] - band_lo),
+                              prog ? int32_t(rel) : (ps != 0 ? int32_t(pA[tid] - t0) : 0),
+                              prog ? int32_t(s) : ps};
   }
 }
 
@@ -503,8 +584,10 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
         if (g[u].cnt > 0) {
           const int64_t at = cur.p0 + nrec + __popc(ne & below);
           const int64_t x = int64_t(g[u].first) - d * g[u].st;
-          const bool prog = g[u].st != 0 && x >= INT32_MIN && x <= INT32_MAX;
-          recs[at] = PairRec{r[u], int32_t(d), int32_t(prog ? x : int64_t(g[u].off) - d), prog ? g[u].st : 0};
+          const bool prog = (CG_NODE_PERIODIC ? g[u].st > 0 : g[u].st != 0) && x >= INT32_MIN && x <= INT32_MAX;
+          const bool per = CG_NODE_PERIODIC && g[u].st < 0;  // periodic: x = A - t0, the writer counts from d
+          recs[at] = PairRec{r[u], int32_t(d), int32_t(per ? int64_t(g[u].first) : (prog ? x : int64_t(g[u].off) - d)),
+                             per || prog ? g[u].st : 0};
         }
         run += half_total(incl);
         nrec += __popc(ne);
@@ -713,7 +796,11 @@ __global__ __launch_bounds__(256) void k_node_write(
         const int32_t sv = __builtin_amdgcn_ds_bpermute(own << 2, sst);
         int32_t rv = __builtin_amdgcn_ds_bpermute(own << 2, rr);
         const bool in = q >= qw && q < we;
-        int64_t val = in && sv != 0 ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
+        int64_t val = in && (CG_NODE_PERIODIC ? sv > 0 : sv != 0) ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
+        if (CG_NODE_PERIODIC && __ballot(in && sv < 0)) {  // periodic records: fire q - (their first position)
+          const int32_t d0 = __builtin_amdgcn_ds_bpermute(own << 2, dst);
+          if (in && sv < 0) val = periodic_fire(sv, t0 + int64_t(dl), q - d0);
+        }
         const int32_t gi = in && sv == 0 ? q + dl - q_lo : -1;
         if (__ballot(gi >= 0)) {  // waited for here, not after the branch
           if (gi >= 0) val = (V & 1) ? int64_t(gi) : tb[gi];
@@ -747,7 +834,10 @@ __global__ __launch_bounds__(256) void k_node_write(
         const int32_t bend = (e & ~63) < bl ? (e & ~63) : bl;  // blocks [b, bend) all o's
         const int32_t dl = __builtin_amdgcn_readlane(dlt, o), sv = __builtin_amdgcn_readlane(sst, o);
         const int32_t rv = __builtin_amdgcn_readlane(rr, o);
-        if (sv != 0) {
+        if (CG_NODE_PERIODIC && sv < 0) {  // periodic
+          const int32_t d0 = __builtin_amdgcn_readlane(dst, o);
+          for (; b < bend; b += 64) put(b + lane, periodic_fire(sv, t0 + int64_t(dl), b + lane - d0), rv);
+        } else if (sv != 0) {
           int64_t val = t0 + int64_t(dl) + int64_t(b + lane - q_lo) * sv;
           const int64_t step = int64_t(64) * sv;
           for (; b < bend; b += 64, val += step) {
@@ -946,9 +1036,7 @@ __global__ __launch_bounds__(256) void k_node_checksums(const int64_t* __restric
 // fused vs 9.4 separate -- k_node_tile (5.9 ms) waits on its dependent loads
 // per tile (segment window, records, gathers) where the writer (1.5 ms) and
 // k_ot_tile (2.65 ms) stream.
-#ifndef CG_NODE_TILE_FUSED
-#define CG_NODE_TILE_FUSED 0
-#endif
+// (CG_NODE_TILE_FUSED is defined beside CG_NODE_PERIODIC, above)
 
 // persistent k_node_write grid: as many 4-wave blocks per CU as its register
 // and LDS use let run at once (no block of the grid waits for a slot)
