@@ -284,7 +284,9 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[IT], int n, int32_t
     const bool valid = ebase + j * 64 + lane < n;
     if constexpr (RUNS) {
       const uint32_t d = valid ? dg[j] : uint32_t(D);  // invalid lanes (the tail) add nothing
-      const uint32_t left = __shfl_up(d, 1, 64);
+      // the left neighbour's digit by DPP wave_shr:1 (no LDS round trip;
+      // lane 0 is a head whatever it reads)
+      const uint32_t left = uint32_t(__builtin_amdgcn_update_dpp(0, int(d), 0x138, 0xf, 0xf, false));
       const bool head = lane == 0 || left != d;
       const uint64_t hm = __ballot(head);
       const int h = 63 - __builtin_clzll(hm & upto);  // this lane's run starts at lane h
