@@ -423,7 +423,11 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[IT], int n, uint32_t lo,
 // pk[p - 1] for the element p this lane holds, where a wave's lanes hold
 // consecutive elements: the left lane's v by DPP (wave_shr:1, no LDS access),
 // lane 0 reads LDS (p > 0)
+#ifndef CG_OT_PREV_LDS
+#define CG_OT_PREV_LDS 0  // 1: every lane reads pk[p - 1] (no branch; A/B equal, profiles/r05_ab_prev_read.txt); 0: DPP + lane 0's read
+#endif
 __device__ __forceinline__ uint32_t ot_prev(const uint32_t* pk, int p, uint32_t v) {
+  if (CG_OT_PREV_LDS) return pk[p > 0 ? p - 1 : 0];
   uint32_t u = uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x138, 0xf, 0xf, false));  // wave_shr:1
   if ((threadIdx.x & 63) == 0 && p > 0) u = pk[p - 1];
   return u;
