@@ -1486,6 +1486,9 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
 #endif
 int ot_slab_bits(int64_t H) { return CG_OT_SLAB32 && H <= 2048 ? kOtSlabBits - 1 : kOtSlabBits; }
 
+#ifndef CG_OT_MID_AFTER_DENSE
+#define CG_OT_MID_AFTER_DENSE 1
+#endif
 #ifndef CG_OT_DENSE_BPC
 #define CG_OT_DENSE_BPC 2  // blocks per CU of the dense merge's persistent grid
 #endif
@@ -1544,10 +1547,18 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
                        mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err, sb);
     // k_ot_mid's queue is filled by the 4-wave merge only (the 8-wave merge's
-    // chunk holds any slab of <= 8192 events): it runs beside the dense merge
-    hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, st, toff, c->node_rule2.p,
-                       c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid,
-                       big_n + 1, err, sb);
+    // chunk holds any slab of <= 8192 events).  Its blocks find no room
+    // beside the dense merge (whose persistent grid holds every CU's VGPRs),
+    // so it is queued behind both merges on the dense merge's stream: it
+    // starts when it can run, and an empty queue costs one short launch
+    // instead of a launch that spans the dense merge.
+    if (CG_OT_MID_AFTER_DENSE) {
+      (void)hipEventRecord(c->ot_fork, st);  // the 4-wave merge's queue entries are in
+      (void)hipStreamWaitEvent(c->st_ot, c->ot_fork, 0);
+    }
+    hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, CG_OT_MID_AFTER_DENSE ? c->st_ot : st,
+                       toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p,
+                       c->node_rule.p, mid, big_n + 1, err, sb);
     (void)hipEventRecord(c->ot_join, c->st_ot);
     (void)hipStreamWaitEvent(st, c->ot_join, 0);
     if (!early)
