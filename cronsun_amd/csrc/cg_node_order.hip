@@ -242,9 +242,13 @@ __device__ __forceinline__ void ot_sync() {
   }
 }
 
+#ifndef CG_OT_RUN_SLOTS
+#define CG_OT_RUN_SLOTS 1  // RUNS ranks: a run's position handed to its lanes through LDS by run ordinal (mbcnt), not ds_bpermute from the head lane
+#endif
 template <int NW, int D>  // D digits: 64 or 256
 struct OtRank {
   int32_t run[NW][D];  // per wave: its events of each digit, then their first position
+  int32_t head[CG_OT_RUN_SLOTS ? NW : 1][64];  // RUNS, CG_OT_RUN_SLOTS: per wave, run k's first position - its head lane
   int32_t dbase[65];   // D == 64: exclusive prefix of the digit totals; [64] = events
   int32_t wtot[4];     // CG_OT_SCAN_ALL: the digit-scan waves' totals
 };
@@ -289,13 +293,27 @@ __device__ __forceinline__ void ot_rank(const uint32_t (&dg)[IT], int n, int32_t
       const uint32_t left = uint32_t(__builtin_amdgcn_update_dpp(0, int(d), 0x138, 0xf, 0xf, false));
       const bool head = lane == 0 || left != d;
       const uint64_t hm = __ballot(head);
-      const int h = 63 - __builtin_clzll(hm & upto);  // this lane's run starts at lane h
       const uint64_t after = hm & ~upto;
       const int end = after ? __builtin_ctzll(after) : 64;
-      uint32_t r = 0;
-      if (head && valid) r = atomicAdd(run + d, uint32_t(end - lane));
-      r = __shfl(r, h, 64);
-      pos[j] = valid ? int32_t(r) + (lane - h) : 0;
+      if constexpr (CG_OT_RUN_SLOTS) {
+        // run ordinal k = heads before this lane (mbcnt), minus one off a head;
+        // the head leaves its run's first position - its lane in slot k (a
+        // wave's LDS operations complete in order)
+        const int before = int(__builtin_amdgcn_mbcnt_hi(uint32_t(hm >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(hm), 0u)));
+        const int k = head ? before : before - 1;
+        int32_t* slot = s.head[w];
+        if (head && valid) slot[k] = int32_t(atomicAdd(run + d, uint32_t(end - lane))) - lane;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        pos[j] = valid ? slot[k] + lane : 0;
+      } else {
+        const int h = 63 - __builtin_clzll(hm & upto);  // this lane's run starts at lane h
+        uint32_t r = 0;
+        if (head && valid) r = atomicAdd(run + d, uint32_t(end - lane));
+        r = __shfl(r, h, 64);
+        pos[j] = valid ? int32_t(r) + (lane - h) : 0;
+      }
     } else {
       pos[j] = valid ? int32_t(atomicAdd(run + dg[j], 1u)) : 0;
     }
