@@ -328,6 +328,15 @@ __device__ __forceinline__ int64_t periodic_fire(int32_t st, int64_t A, int32_t 
 #define CG_NODE_PERIODIC 0  // 1: periodic records (A/B: slower, profiles/r05_ab_periodic.txt; the fused tile writer reads progressions only)
 #endif
 constexpr int kApRules = 256;
+#ifndef CG_SEG_NEMASK
+#define CG_SEG_NEMASK 0  // 1: k_seg_records reads a per-window bit per rule (fires in the window) before gathering its RuleInfo (A/B: no gain, profiles/r05_ab_nonempty_mask.txt)
+#endif
+// the rule-info buffer: R RuleInfos, then (CG_SEG_NEMASK) the window's
+// non-empty-rule bitmask, one bit per rule (a 16-B slot holds 128 bits)
+inline int64_t rule_info_slots(int64_t R) { return std::max<int64_t>(R, 1) + (CG_SEG_NEMASK ? (R + 255) / 128 : 0); }
+__device__ __forceinline__ const uint64_t* ne_mask_of(const RuleInfo* info, int64_t R) {
+  return reinterpret_cast<const uint64_t*>(info + (R > 0 ? R : 1));
+}
 __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ rule_off,
                                                     const int64_t* __restrict__ times, int64_t R, int64_t t0,
                                                     int32_t B, int64_t cap, RuleInfo* __restrict__ info,
@@ -340,8 +349,10 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
   const int64_t r0 = int64_t(blockIdx.x) * kApRules;
   const int nr = int(R - r0 < kApRules ? R - r0 : kApRules);
   const int tid = threadIdx.x;
+  uint64_t* ne = const_cast<uint64_t*>(ne_mask_of(info, R)) + (r0 >> 6);
   if (rule_off[R] > cap) {  // a pipelined window past the fire-time capacity: no fires read, none written
     if (tid < nr) info[r0 + tid] = RuleInfo{0, 0, 0, 0};
+    if (CG_SEG_NEMASK && (tid & 63) == 0 && r0 + tid < R) ne[tid >> 6] = 0;
     return;
   }
   const int64_t band_lo = rule_off[(r0 / B) * B];  // B is a multiple of kApRules
@@ -454,6 +465,10 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
     info[r0 + tid] = RuleInfo{int32_t(cnt), int32_t(off[tid] - band_lo),
                               prog ? int32_t(rel) : (ps != 0 ? int32_t(pA[tid] - t0) : 0),
                               prog ? int32_t(s) : ps};
+  }
+  if (CG_SEG_NEMASK) {  // bit r of the window's non-empty-rule mask
+    const uint64_t b = __ballot(tid < nr && cnt > 0);
+    if ((tid & 63) == 0 && r0 + tid < R) ne[tid >> 6] = b;
   }
 }
 
@@ -570,9 +585,20 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
     for (int32_t pc = 0; pc < rounds_len; pc += L * P) {
       if (pc > 0) rules(cur, pc, r);  // segments of more than L*P pairs
       RuleInfo g[P];
+      if (CG_SEG_NEMASK && !CG_SEG_NOINFO) {
+        // about half of a 1-h window's rules do not fire: their pairs need
+        // no RuleInfo (cnt 0), so only the rules whose bit is set are gathered
+        const uint64_t* __restrict__ ne = ne_mask_of(info, R);
+        uint32_t mb[P];
 #pragma unroll
-      for (int u = 0; u < P; u++)
-        g[u] = r[u] >= 0 ? (CG_SEG_NOINFO ? RuleInfo{1, 0, 0, 1} : info[r[u]]) : RuleInfo{0, 0, 0, 0};
+        for (int u = 0; u < P; u++) mb[u] = r[u] >= 0 ? uint32_t(ne[r[u] >> 6] >> (r[u] & 63)) & 1u : 0u;
+#pragma unroll
+        for (int u = 0; u < P; u++) g[u] = mb[u] ? info[r[u]] : RuleInfo{0, 0, 0, 0};
+      } else {
+#pragma unroll
+        for (int u = 0; u < P; u++)
+          g[u] = r[u] >= 0 ? (CG_SEG_NOINFO ? RuleInfo{1, 0, 0, 1} : info[r[u]]) : RuleInfo{0, 0, 0, 0};
+      }
 #pragma unroll
       for (int u = 0; u < P; u++) {
         // events before this pair: half-wave inclusive scan of the counts
@@ -1321,7 +1347,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   if ((rc = pn_ensure_res(c))) return rc;
   if ((rc = c->seg_nrec.ensure(std::max<int64_t>(NK, 1))) ||
       (rc = c->recs.ensure(std::max<int64_t>(nnz, 1))) ||
-      (rc = c->rule_info.ensure(std::max<int64_t>(R, 1))))
+      (rc = c->rule_info.ensure(rule_info_slots(R))))
     return rc;
   c->pn_res_host[1] = 0;  // error flag (nothing of this ctx is in flight here)
   if (R > 0)
@@ -1582,7 +1608,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     return cg_fail(CG_EINVAL, "pipelined per-node windows in time order: windows of at most 4096 s");
   bool empty = false;
   if ((rc = async_count_scan(c, a.rm, s, z, t0, t1, rm_cap, &empty))) return rc;
-  if ((rc = a.times.ensure(std::max<int64_t>(rm_cap, 1))) || (rc = a.rule_info.ensure(std::max<int64_t>(R, 1))) ||
+  if ((rc = a.times.ensure(std::max<int64_t>(rm_cap, 1))) || (rc = a.rule_info.ensure(rule_info_slots(R))) ||
       (rc = a.seg_cnt.ensure(std::max<int64_t>(NK, 1))) || (rc = a.seg_pos.ensure(NK + 1)) ||
       (rc = a.seg_nrec.ensure(std::max<int64_t>(NK, 1))) || (rc = a.recs.ensure(std::max<int64_t>(nnz, 1))) ||
       (rc = a.tickets.ensure(kTicketGroups * kTicketStride)) || (rc = a.node_off.ensure(int64_t(N) + 1)) ||
@@ -1595,7 +1621,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     a.rm.res_host[0] = 0;
     a.rm.res_host[1] = -1;
     HIPCHK(hipMemsetAsync(a.seg_pos.p, 0, (NK + 1) * 8, sc));
-    HIPCHK(hipMemsetAsync(a.rule_info.p, 0, std::max<int64_t>(R, 1) * sizeof(RuleInfo), sc));
+    HIPCHK(hipMemsetAsync(a.rule_info.p, 0, rule_info_slots(R) * sizeof(RuleInfo), sc));
   } else {
     const PlanArgs& pa = a.rm.pa;
     const int64_t nruns = R * int64_t(pa.G);
