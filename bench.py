@@ -3,7 +3,22 @@
 job-ID-range shards at N > 1.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--workload W]
-  (N > 1: launched by torch.distributed.run, one rank per GPU, RCCL)
+  (N > 1: one rank per GPU over RCCL.  Run under torch.distributed.run, or
+  alone: `--gpus N` then starts torch.distributed.run with N ranks of the same
+  command as a child process, before this process touches the GPU, and
+  forwards rank 0's JSON line and the child's exit status.  A WORLD_SIZE that
+  differs from --gpus is refused.)
+
+At N > 1 every workload ends, after its timed region, with one verified
+time-ordered per-node gather (`verify.gather`): a small pernode-shaped window
+gathered on rank 0 in many chunks under a small byte budget (split nodes
+included) -- through the library's RCCL communicator
+(cg_comm_gather_node_csr: send/recv, placement, the merge of the ranks' runs)
+with the nccl backend, through shard.gather_node_csr with gloo -- and 24 nodes
+checked against the oracle.  With nccl the per-step exchanges (config-2
+totals, per-node counts) also go through the library's communicator
+(cg_comm_allgather_i64 / cg_comm_node_offsets; `--torch-comm`: through
+torch.distributed instead).
 
 Workloads (`--workload`, default config2 -- the headline line):
   config2  a step = one full expansion of the rank's 1M-rule shard over 24 h:
@@ -145,8 +160,15 @@ def main():
                          "rank 0 (shard.gather_node_csr; timed)")
     ap.add_argument("--lib-comm", action="store_true",
                     help="N > 1: the exchanges through the library's RCCL communicator behind the C-ABI "
-                         "(cg_comm_*: totals all-gather, per-node offsets, chunked per-node CSR gather) "
-                         "instead of torch.distributed")
+                         "(cg_comm_*: totals all-gather, per-node offsets, chunked per-node CSR gather); "
+                         "the default with the nccl backend")
+    ap.add_argument("--torch-comm", action="store_true",
+                    help="N > 1 with nccl: the per-step exchanges through torch.distributed instead of "
+                         "the library's communicator")
+    ap.add_argument("--no-gather-check", action="store_true",
+                    help="N > 1: skip the verified time-ordered per-node gather after the timed region")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check: every rank reports its rank / world and exits before any GPU use")
     ap.add_argument("--gather-budget", type=int, default=1 << 31,
                     help="bytes of peer events rank 0 stages per chunk of the per-node CSR gather")
     ap.add_argument("--sync", action="store_true",
@@ -172,9 +194,24 @@ def main():
     if args.workload == "parse":  # host-only: no GPU, no ranks
         print(json.dumps(parse_line(args)), flush=True)
         return
+    rc = launch_ranks(args)  # before anything touches torch.cuda, HIP or the library
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and os.environ.get("CG_RCCL_ONE_GPU_REHEARSAL"):
+        # rehearsal of the N-GPU RCCL path with N ranks on fewer GPUs: RCCL
+        # refuses two ranks on one device of one host, so every rank claims a
+        # host of its own and RCCL moves the data over sockets on loopback
+        # (tools/comm_world2.py does the same for the library's gather)
+        os.environ["NCCL_HOSTID"] = f"cg-bench-rank-{rank}"
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+        os.environ["NCCL_IB_DISABLE"] = "1"
+    if args.dry_run:
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "rank": rank, "world": world, "gpus": args.gpus}), flush=True)
+        return
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -329,7 +366,7 @@ def main():
     dev = torch.device("cuda", local)
     cdev = dev if backend == "nccl" else torch.device("cpu")  # collective tensors
     lcomm = None
-    if args.lib_comm and world > 1:
+    if world > 1 and (args.lib_comm or (backend == "nccl" and not args.torch_comm)):
         # the library's own RCCL communicator (cg_comm_init): rank 0's unique id
         # handed to every rank over torch.distributed
         from cronsun_amd.engine import Comm
@@ -573,6 +610,17 @@ def main():
         verify["verified_all_ranks"] = bool(ok.item())
         log(f"[rank {rank}] verify: {verify}")
 
+    if world > 1 and not args.no_gather_check:
+        # the multi-rank exchange itself, verified (outside the timed region)
+        g = gather_check(eng, dist, world, rank, backend, utc, args.zone, t0, dev, cdev,
+                         restore_order=_cg.NODE_ORDER_TIME if (pn and args.time_order) else _cg.NODE_ORDER_RULE)
+        if rank == 0:
+            log(f"[rank 0] gather check: {g}")
+            if verify is None:
+                verify = {"verified": True, "verified_all_ranks": True}
+            verify["gather"] = g
+            verify["verified_all_ranks"] = verify["verified_all_ranks"] and g["verified"]
+
     if lean:
         # per-phase breakdown of a few untimed steps (events between phases)
         eng.set_phase_timing(2)
@@ -749,6 +797,10 @@ def main():
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBPS,
+            # the whole step (every kernel, every window) against the same
+            # algorithmic bytes: what a caller of the step gets
+            "step_achieved": algo_bytes / (elapsed / args.steps) / 1e9,
+            "step_frac": algo_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS,
             "traffic": traffic,
             "traffic_source": traffic_src,
             "timed_interval_s": ksec,
@@ -789,6 +841,150 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def rank_launch_cmd(gpus, argv, port):
+    """The child that runs N ranks of this same command (one per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) with no launcher around this process: one child,
+    torch.distributed.run with N ranks of this command (node.go:121-141: the
+    ranks shard the jobs), started before this process imports torch.cuda,
+    loads the library or makes any HIP call (a process that has touched the
+    GPU must not start ranks by exec).  Rank 0's JSON line is forwarded to
+    stdout, everything else the ranks print to stderr; returns the child's
+    exit status.  Inside a launcher (WORLD_SIZE set) returns None, or 2 when
+    WORLD_SIZE differs from --gpus."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != args.gpus:
+            log(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}: refusing (one rank per GPU)")
+            return 2
+        return None
+    if args.gpus <= 1:
+        return None
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = rank_launch_cmd(args.gpus, sys.argv[1:], port)
+    log(f"bench.py: launching {args.gpus} ranks: {' '.join(cmd)}")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    for line in p.stdout:
+        if line.lstrip().startswith("{"):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return p.wait()
+
+
+def gather_check(eng, dist, world, rank, backend, loc, zone, t0, dev, cdev, restore_order=0, rules_per_rank=50_000,
+                 n_nodes=200, window=600, n_check=24, seed=0x5EED + 91):
+    """N > 1, after the timed region: the multi-rank exchange of the per-node
+    view, run and verified.  A pernode-shaped job set (`rules_per_rank` jobs
+    per rank in job-ID ranges, `n_nodes` nodes, the light spec mix), one
+    `window`-second window per rank in (time, rule) order
+    (cg_set_node_order(TIME)), gathered on rank 0 with a byte budget of a
+    third of the largest node's peer events, so the plan has hundreds of
+    chunks and splits nodes: nccl -> the library's communicator
+    (cg_comm_gather_node_csr: grouped ncclSend/ncclRecv per chunk,
+    k_node_place / k_span_place from the staging buffer, k_merge_ranks over
+    the ranks' runs); gloo -> shard.gather_node_csr (the same plan over
+    torch.distributed, merged by the library's kernel or numpy).  Rank 0
+    checks the offsets and `n_check` seeded nodes' whole lists against the
+    oracle (each node filtering every job, node.go:121-141, in its Cron's
+    byTime order, cron.go:64-79,220; ties by rule).  Returns the record on
+    rank 0 (None elsewhere); every rank returns only after the check."""
+    import numpy as np
+    import torch
+    from cronsun_amd import _lib as cg
+    from cronsun_amd import cron, shard, synth
+    from cronsun_amd.engine import Comm
+    tg = time.perf_counter()
+    glob = rules_per_rank * world
+    specs = synth.spec_mix(glob, seed=seed, mix=synth.MIX_LIGHT)
+    rin = synth.rules_for_nodes(glob, n_nodes=n_nodes, n_groups=20, seed=seed + 1, group_size=(4, 64))
+    lo, hi = shard.shard_range(glob, world, rank)
+    arr, st = cron.parse_batch(specs[lo:hi], threads=16)
+    assert (st == 0).all()
+    sp = eng.upload_c(arr, hi - lo)
+    drules = eng.upload_rules(rin.slice_rules(lo, hi))
+    eng.set_node_order(cg.NODE_ORDER_TIME)
+    try:
+        En, _ = eng.expand_per_node_rules_device(sp, loc, t0, t0 + window, drules, cg.EXCLUDE_NONE)
+    finally:
+        eng.set_node_order(restore_order)
+    n_off, n_time, n_rule = eng.node_result_tensors(n_nodes)
+    cnt = (n_off[1:] - n_off[:-1]).to(cdev)
+    allc = torch.zeros(world * n_nodes, dtype=torch.int64, device=cdev)
+    dist.all_gather_into_tensor(allc, cnt.contiguous())
+    allc = allc.view(world, n_nodes).cpu().numpy()
+    peer = allc.sum(axis=0) - allc[0]
+    budget = 12 * max(2 * world, int(peer.max()) // 3)
+    plan = shard.node_gather_plan(allc, 0, budget)
+    total = int(allc.sum())
+    tx = time.perf_counter()
+    out = None
+    if backend == "nccl":
+        uid = [Comm.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        comm = Comm(eng, world, rank, uid[0])
+        try:
+            if rank == 0:
+                o = torch.empty(n_nodes + 1, dtype=torch.int64, device=dev)
+                t = torch.full((total,), -1, dtype=torch.int64, device=dev)
+                r = torch.full((total,), -1, dtype=torch.int32, device=dev)
+                torch.cuda.synchronize(dev)
+                n = comm.gather_node_csr(0, lo, budget, o.data_ptr(), t.data_ptr(), r.data_ptr(), total)
+                out = (o.cpu().numpy(), t.cpu().numpy(), r.cpu().numpy(), n)
+            else:
+                comm.gather_node_csr(0, lo, budget)
+        finally:
+            comm.free()
+        how = "cg_comm_gather_node_csr (the library's RCCL communicator)"
+    else:
+        g = shard.gather_node_csr(n_off.to(cdev), n_time.to(cdev), n_rule.to(cdev), lo, dist, engine=eng,
+                                  budget_bytes=budget, order="time")
+        if rank == 0:
+            out = (g[0].cpu().numpy(), g[1].cpu().numpy(), g[2].cpu().numpy(), int(g[1].numel()))
+        how = "shard.gather_node_csr over torch.distributed (gloo)"
+    t_gather = time.perf_counter() - tx
+    sp.free()
+    drules.free()
+    res = None
+    if rank == 0:
+        O = _oracle()
+        off, gt, gr, n = out
+        nodes = np.sort(np.random.default_rng(seed + 2).choice(n_nodes, n_check, replace=False))
+        roff, rules = O.node_rules(rin, 0, nodes, threads=host_cpus()[0])
+        union = np.unique(rules)
+        eo, et = O.expand_batch(_oracle_scheds(O, [specs[int(i)] for i in union]), t0, t0 + window,
+                                O.Loc(zone), threads=host_cpus()[0])
+        bad, ev = 0, 0
+        for k, nd in enumerate(nodes):
+            pos = np.searchsorted(union, rules[roff[k]:roff[k + 1]])
+            exp_t, exp_p = O.node_list(eo, et, pos)
+            o = np.lexsort((exp_p, exp_t))  # (time, rule): pos ascends with the global rule
+            exp_t, exp_r = exp_t[o], union[exp_p[o]]
+            a, b = int(off[nd]), int(off[nd + 1])
+            ev += len(exp_t)
+            bad += not (np.array_equal(gt[a:b], exp_t) and np.array_equal(gr[a:b], exp_r))
+        exp_off = np.concatenate([[0], np.cumsum(allc.sum(axis=0))])
+        offs_ok = bool(np.array_equal(off, exp_off) and n == total)
+        split = sum(1 for c in plan if c[3] > 1)
+        res = {"verified": bad == 0 and offs_ok, "via": how,
+               "shape": f"{glob} jobs ({rules_per_rank} per rank) x {n_nodes} nodes, light mix, {window}-s window, "
+                        f"(time, rule) order per node",
+               "events": total, "budget_bytes": budget, "chunks": len(plan), "split_node_chunks": split,
+               "nodes_checked": int(len(nodes)), "events_checked": int(ev), "mismatched_nodes": int(bad),
+               "offsets_consistent": offs_ok, "gather_s": t_gather, "seconds": time.perf_counter() - tg}
+    dist.barrier()
+    return res
 
 
 def dispatch_line(args, R, world, elapsed, wake, nkt, build_info, cpu):

@@ -232,7 +232,6 @@ struct cg_ctx {
   // histograms/offsets, and the second buffers of the ping-pong
   DBuf<int32_t> ts_cnt, ts_tile_node, ts_hist, node_rule2;
   DBuf<int64_t> ts_base, ts_off, node_time2, ts_node_off;
-  DBuf<int64_t> ts_rec;  // per tile: the segment and record holding its first event (k_node_tile)
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
@@ -286,7 +285,7 @@ struct cg_ctx {
     seg_nrec.release(); recs.release();
     rule_info.release();
     ts_cnt.release(); ts_tile_node.release(); ts_hist.release(); node_rule2.release();
-    ts_base.release(); ts_off.release(); node_time2.release(); ts_node_off.release(); ts_rec.release();
+    ts_base.release(); ts_off.release(); node_time2.release(); ts_node_off.release();
     mr_rb.release(); mr_tp.release(); mr_t.release(); mr_r.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);
     pn_res_host = nullptr;
@@ -345,22 +344,6 @@ bool pn_async_pending(const cg_ctx* c);  // an asynchronous expansion not yet wa
 constexpr int kInTimes = 0, kIn16 = 1, kInPacked = 2;
 // the time-order writer may emit kInPacked for R rules (indices < 2^20)
 bool pn_pack_ok(int64_t R);
-// The per-node lists of a window <= 4096 s in (time, rule) order straight
-// from the segment records (cg_node_order.hip: k_node_tile writes the tiles,
-// then the merge), enqueued on st without a host sync
-struct FusedOrderArgs {
-  const int64_t* seg_pos;   // [N*K+1] output position of each (node, band) segment
-  const int64_t* seg_pair;  // [N*K+1] first record (pair index) of each segment
-  const int32_t* seg_nrec;  // [N*K] records of each segment
-  const PairRec* recs;
-  const int64_t* rule_off;  // the window's rule-major offsets and fire times (gathers)
-  const int64_t* times;
-  int64_t times_cap;
-  const int64_t* node_off;  // [N+1]
-  int32_t N, K, B;
-  int64_t cap, t0;
-};
-int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int64_t* err);
 // err: a device word the kernels set when a sorted chunk is out of (time,
 // rule) order (the sorts' ranks rest on lane-ordered LDS atomics; checked)
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,

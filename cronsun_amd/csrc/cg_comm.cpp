@@ -423,6 +423,22 @@ int cg_comm_gather_node_csr(cg_comm* m, int root, int64_t rule_base, int64_t bud
     total += mq[1];
   }
   const bool timed = meta[6] != 0;
+  if (timed && W > kMergeMaxRanks)  // refused here, on every rank, before any transfer
+    return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: time-ordered results of more than " +
+                                  std::to_string(kMergeMaxRanks) + " ranks");
+  if (timed) {
+    // the merge breaks (time) ties by rank: that is (time, global rule) order
+    // only when the ranks' job-ID ranges ascend with the rank
+    int64_t prev = -1;
+    for (int q = 0; q < W; q++) {
+      const int64_t* mq = &meta[size_t(kMeta * q)];
+      if (mq[1] == 0) continue;  // no events: no ties to order
+      if (mq[3] <= prev)
+        return cg_fail(CG_EINVAL, "cg_comm_gather_node_csr: rule_base of rank " + std::to_string(q) +
+                                      " does not ascend with the rank (time-ordered results merge by rank)");
+      prev = mq[3];
+    }
+  }
   if (n_events) *n_events = total;
   const int64_t root_cap = meta[size_t(kMeta * root + 4)];
   if (total > root_cap)

@@ -441,11 +441,7 @@ __device__ __forceinline__ void ot_sort(uint32_t (&key)[IT], int n, uint32_t lo,
 // pk[p - 1] for the element p this lane holds, where a wave's lanes hold
 // consecutive elements: the left lane's v by DPP (wave_shr:1, no LDS access),
 // lane 0 reads LDS (p > 0)
-#ifndef CG_OT_PREV_LDS
-#define CG_OT_PREV_LDS 0  // 1: every lane reads pk[p - 1] (no branch; A/B equal, profiles/r05_ab_prev_read.txt); 0: DPP + lane 0's read
-#endif
 __device__ __forceinline__ uint32_t ot_prev(const uint32_t* pk, int p, uint32_t v) {
-  if (CG_OT_PREV_LDS) return pk[p > 0 ? p - 1 : 0];
   uint32_t u = uint32_t(__builtin_amdgcn_update_dpp(0, int(v), 0x138, 0xf, 0xf, false));  // wave_shr:1
   if ((threadIdx.x & 63) == 0 && p > 0) u = pk[p - 1];
   return u;
@@ -459,9 +455,6 @@ __device__ __forceinline__ bool ot_out_of_order(uint32_t u, uint32_t v, const in
   return a > b || (a == b && rl[u & kOtIdxMask] >= rl[v & kOtIdxMask]);
 }
 
-#ifndef CG_OT_TILE_PACK
-#define CG_OT_TILE_PACK 1  // 0: the tile sort keeps an LDS rule array (A/B)
-#endif
 #ifndef CG_OT_TILE_WPE
 #define CG_OT_TILE_WPE 6  // min waves per SIMD of the packed tile sort (its LDS allows 9 blocks per CU)
 #endif
@@ -664,9 +657,6 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 // BUF: the loads as raw buffer loads (32-bit offsets against a descriptor
 // over n_src elements; an index past it reads 0): one VGPR per address
 // instead of two, and no 64-bit address arithmetic per item
-#ifndef CG_OT_BUF
-#define CG_OT_BUF 1
-#endif
 // PIN: the source is one array of packed words offset << 20 | rule (rin; tin
 // unused), 4 B per event instead of 2 + 4
 template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems, bool BUF = false, bool PIN = false>
@@ -738,73 +728,12 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
   }
 }
 
-#ifndef CG_OT_MID2
-#define CG_OT_MID2 1  // 0: slabs of 8193..16384 events to k_ot_big, not k_ot_mid's 16-wave form (A/B)
-#endif
-#ifndef CG_OT_MID
-#define CG_OT_MID 1  // 0: every slab of more than a merge chunk to k_ot_big (A/B)
-#endif
-#ifndef CG_OT_PIPE
-// 1: the packed merge pipelined -- the next chunk's gathers issued before the
-// current chunk's stores, every store instruction unconditional (a fixed
-// count), so waiting for the gathers does not drain the stores (gfx9: one
-// in-order vmcnt for loads and stores); big slabs queued by k_ot_slabs
-#define CG_OT_PIPE 0
-#endif
-#ifndef CG_OT_EARLY_QUEUE
-// 1: k_ot_slabs queues the slabs no merge chunk holds (also without
-// CG_OT_PIPE), so k_ot_mid's two forms run beside the merges instead of after
-// them: the 16-wave form behind the dense merge on its stream, the 8-wave form
-// behind the sparse merge
-#define CG_OT_EARLY_QUEUE 0
-#endif
-// The packed words (offset << 20 | rule) of elements 0 .. n_el of the
-// portion list as keys, for the pipelined merge: no use of the loaded values
-// here (the waits for them come at the sort, after the previous chunk's
-// stores), lanes past n_el read out of the buffer's range (0).  Portions by
-// search + walk (ot_gather SEARCH 2), raw buffer loads.
-template <int IT>
-__device__ __forceinline__ void ot_gather_words(const int32_t* __restrict__ rin, const int32_t* ps, const int32_t* psrc,
-                                                int n_el, uint32_t (&key)[IT], int Q, uint32_t n_src) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ebase = w * (64 * IT);
-  constexpr int kRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<int32_t*>(rin), 0, int(n_src * 4u), kRsrcWord3);
-  const int e0 = ebase + lane < n_el ? ebase + lane : n_el - 1;
-  int qw = ot_find(ps, Q, e0), qa = ps[qw], qb = ps[qw + 1], qs = psrc[qw];
-#pragma unroll
-  for (int j = 0; j < IT; j++) {
-    const int e = ebase + j * 64 + lane;
-    const int ec = e < n_el ? e : n_el - 1;
-    while (qb <= ec && qw + 1 < Q) {
-      qw++;
-      qa = qb;
-      qb = ps[qw + 1];
-      qs = psrc[qw];
-    }
-    const uint32_t off = e < n_el ? uint32_t(qs + (ec - qa)) * 4u : 0xFFFFFFF0u;
-    key[j] = uint32_t(__builtin_amdgcn_raw_buffer_load_b32(rb, int(off), 0, 0));
-  }
-}
-
 // Per node: the first node-relative position of each slab (events of the
 // earlier slabs over all its tiles), slab_off[n][0..kOtSlabs].  One wave per
-// node, kOtSlabs / 64 slabs per lane.  With q.on (the pipelined merge), the
-// slabs no merge chunk of their node can hold are queued here, so the merge
-// loop issues no atomics: to k_ot_mid / its 16-wave form when they fit those
-// chunks, else to k_ot_big; every non-empty slab of a node of more than
-// kOtMaxTiles tiles to k_ot_big.  Entries (node << 8 | slab).
-struct OtQueues {
-  int64_t *big, *mid, *mid2;
-  unsigned *big_n, *mid_n, *mid2_n;
-  const int64_t* node_off;
-  int64_t dense_min;            // events from which a node takes the dense merge
-  int32_t chunk, dense_chunk;   // the two merges' chunks
-  int32_t on;
-};
+// node, kOtSlabs / 64 slabs per lane.
 __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ tile_base,
                                                   const int32_t* __restrict__ pre, int32_t N,
-                                                  int64_t* __restrict__ slab_off, OtQueues q) {
+                                                  int64_t* __restrict__ slab_off) {
   constexpr int kSpl = kOtSlabs / 64;
   const int lane = threadIdx.x;
   const int32_t n = blockIdx.x;
@@ -838,35 +767,8 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
     run += c[i];
   }
   if (lane == 63) so[kOtSlabs] = run;
-  if (!q.on || M <= 1) return;  // one tile: sorted by k_ot_tile
-  constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems, kMid2Chunk = 64 * kOtMid2Waves * kOtItems;
-  const int64_t e_n = q.node_off[n + 1] - q.node_off[n];
-  const int64_t chunk = e_n >= q.dense_min ? q.dense_chunk : q.chunk;
-#pragma unroll
-  for (int i = 0; i < kSpl; i++) {
-    const int64_t e = (int64_t(n) << 8) | (kSpl * lane + i);
-    if (M > kOtMaxTiles) {
-      if (c[i] > 0) q.big[atomicAdd(q.big_n, 1u)] = e;
-    } else if (c[i] > chunk) {
-      if (CG_OT_MID && c[i] <= kMidChunk) q.mid[atomicAdd(q.mid_n, 1u)] = e;
-      else if (CG_OT_MID2 && c[i] <= kMid2Chunk) q.mid2[atomicAdd(q.mid2_n, 1u)] = e;
-      else q.big[atomicAdd(q.big_n, 1u)] = e;
-    }
-  }
 }
 
-#ifndef CG_OT_OWN_SEARCH
-#define CG_OT_OWN_SEARCH 2  // the merge's portion per element: 0 owner map, 1 binary search, 2 search + walk
-#endif
-#ifndef CG_OT_MERGE_RUNS
-// 1: the merge / k_ot_big ranks add once per run of equal digits in
-// neighbouring lanes (ot_rank RUNS): events of a rule-major portion often
-// share a second with their neighbours (minutely rules all at :00)
-#define CG_OT_MERGE_RUNS 0
-#endif
-#ifndef CG_OT_RUN_SLABS
-#define CG_OT_RUN_SLABS 0  // > 0: a merge run holds at most this many slabs (4: always one 8-bit pass)
-#endif
 #ifndef CG_OT_MID_WPE
 #define CG_OT_MID_WPE 4  // min waves per SIMD of k_ot_mid (8-wave blocks: 2 per SIMD each)
 #endif
@@ -893,14 +795,10 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   uint32_t key[IT];
   ot_portions<NW>(M, portion, ps, psrc, wsum);
   const uint32_t n_src = uint32_t(M) * kOtTile;  // the node's tiles (M <= kOtMaxTiles)
-#if CG_OT_OWN_SEARCH
-  ot_gather<true, CG_OT_OWN_SEARCH, PACK, IT, CG_OT_BUF, PIN>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M, n_src);
-#else
-  ot_owners<NW, IT>(ps, M, 0, n_el, own, wsum);
-  ot_gather<true, 0, PACK, IT, CG_OT_BUF, PIN>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, 0, n_src);
-#endif
+  // each element's portion by search + walk, raw buffer loads
+  ot_gather<true, 2, PACK, IT, true, PIN>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M, n_src);
   constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
-  ot_sort<NW, 256, bool(CG_OT_MERGE_RUNS), IB, IT>(key, n_el, lo, 0, passes, pk, s);
+  ot_sort<NW, 256, false, IB, IT>(key, n_el, lo, 0, passes, pk, s);
   bool bad = false;
   for (int p = threadIdx.x; p < n_el; p += 64 * NW) {
     const uint32_t v = pk[p];
@@ -917,78 +815,6 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
   }
   if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
   ot_sync<NW>();
-}
-
-// One node's merge, pipelined (CG_OT_PIPE; packed words, rule indices <
-// 2^20): its slabs in runs of whole slabs that fit one chunk (the slabs no
-// chunk holds were queued by k_ot_slabs), run after run -- the next run's
-// portions and gathers are issued between this run's sort and its stores,
-// and the run after next's tile prefixes right after them, so the wait for a
-// chunk's gathers covers only loads issued before the previous chunk's
-// stores.  Every store instruction is unconditional (lanes past the chunk
-// store its last element again), so the compiler's vmcnt waits count a fixed
-// number of stores instead of draining them.  pq: this thread's tile's slab
-// prefix row (thread q owns tile q); bad collects order-check failures.
-template <int NW, int IT, bool PIN>
-__device__ __forceinline__ void ot_merge_node_pipe(const uint16_t* __restrict__ tin_n, const int32_t* __restrict__ rin_n,
-                                                   const int32_t* __restrict__ pq, int M, const int64_t* slab_off,
-                                                   int64_t t0, int64_t* __restrict__ tout_n,
-                                                   int32_t* __restrict__ rout_n, OtRank<NW, 256>& s, uint32_t* pk,
-                                                   int32_t* ps, int32_t* psrc, int32_t* wsum, bool& bad, int sb) {
-  constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
-  const uint32_t n_src = uint32_t(M) * kOtTile;
-  // the first run of whole slabs at or after j0 that a chunk holds: empty and
-  // queued slabs skipped, then every slab that still fits
-  auto next_run = [&](int j0, int& ja, int& jb) {
-    ja = j0;
-    while (ja < kOtSlabs && (slab_off[ja + 1] == slab_off[ja] || slab_off[ja + 1] - slab_off[ja] > kChunk)) ja++;
-    jb = ja;
-    while (jb < kOtSlabs && slab_off[jb + 1] - slab_off[ja] <= kChunk) jb++;
-  };
-  int ja, jb, ja2, jb2;
-  next_run(0, ja, jb);
-  if (ja >= kOtSlabs) return;
-  next_run(jb, ja2, jb2);
-  const int q = threadIdx.x;
-  int32_t pa = pq[ja], pb = pq[jb];
-  ot_portions<NW>(M, [&](int, int32_t* src) { *src = q * kOtTile + pa; return pb - pa; }, ps, psrc, wsum);
-  // the next run's tile prefixes are loaded before this run's gathers: the
-  // wait for the gathers (at the sort) covers them
-  pa = pq[ja2 < kOtSlabs ? ja2 : kOtSlabs];
-  pb = pq[jb2 < kOtSlabs ? jb2 : kOtSlabs];
-  uint32_t key[IT];
-  int n_el = int(slab_off[jb] - slab_off[ja]);
-  ot_gather_words<IT>(rin_n, ps, psrc, n_el, key, M, n_src);
-  ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << sb, 0, ((jb - ja) << sb) > 256 ? 2 : 1, pk, s);
-  for (;;) {
-    // pk holds run [ja, jb) sorted; the next run's prefixes are in pa / pb
-    const int64_t o = slab_off[ja];
-    const int n_cur = n_el;
-    const bool more = ja2 < kOtSlabs;  // block-uniform
-    if (more) {
-      ot_portions<NW>(M, [&](int, int32_t* src) { *src = q * kOtTile + pa; return pb - pa; }, ps, psrc, wsum);
-      ja = ja2;
-      jb = jb2;
-      next_run(jb, ja2, jb2);
-      pa = pq[ja2 < kOtSlabs ? ja2 : kOtSlabs];
-      pb = pq[jb2 < kOtSlabs ? jb2 : kOtSlabs];
-      n_el = int(slab_off[jb] - slab_off[ja]);
-      ot_gather_words<IT>(rin_n, ps, psrc, n_el, key, M, n_src);
-    }
-#pragma unroll
-    for (int j = 0; j < IT; j++) {
-      const int p = threadIdx.x + j * kThreads;
-      const int pc = p < n_cur ? p : n_cur - 1;
-      const uint32_t v = pk[pc];
-      __builtin_nontemporal_store(t0 + 1 + int64_t(v >> kOtRuleBits), tout_n + o + pc);
-      __builtin_nontemporal_store(int32_t(v & ((1u << kOtRuleBits) - 1u)), rout_n + o + pc);
-      const uint32_t u = ot_prev(pk, p, v);
-      if (p > 0 && p < n_cur) bad |= u >= v;  // (time, rule) order of the chunk: the words ascend
-    }
-    ot_sync<NW>();
-    if (!more) break;
-    ot_sort<NW, 256, false, kOtRuleBits, IT>(key, n_el, uint32_t(ja) << sb, 0, ((jb - ja) << sb) > 256 ? 2 : 1, pk, s);
-  }
 }
 
 // Per node with e_lo <= events < e_hi: its slabs in runs that fit one chunk,
@@ -1047,27 +873,17 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
     }
     continue;
   }
-  if (M > kOtMaxTiles) {  // every slab to k_ot_big (queued by k_ot_slabs in the pipelined form)
-    if (!(CG_OT_EARLY_QUEUE || (PACK && PIN && CG_OT_PIPE)))
-      for (int j = threadIdx.x; j < kOtSlabs; j += kThreads) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | j;
+  if (M > kOtMaxTiles) {  // every slab to k_ot_big
+    for (int j = threadIdx.x; j < kOtSlabs; j += kThreads) big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | j;
     continue;
   }
   for (int j = threadIdx.x; j <= kOtSlabs; j += kThreads) slab_off[j] = slab_tab[int64_t(n) * kOtPre + j];
   ot_sync<NW>();
-  if constexpr (PACK && PIN && CG_OT_PIPE) {
-    const int32_t* __restrict__ pq = pre + (ta + (threadIdx.x < M ? threadIdx.x : 0)) * kOtPre;
-    bool bad = false;
-    ot_merge_node_pipe<NW, IT, PIN>(tin + lo_n, rin + lo_n, pq, int(M), slab_off, t0, tout + lo_n, rout + lo_n, s, pk,
-                                    ps, psrc, wsum, bad, sb);
-    if (__ballot(bad) && (threadIdx.x & 63) == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
-    continue;
-  }
   // the longest run of whole slabs [j0, j1) that fits one chunk (j1 == j0: a
   // slab of more than a chunk)
   auto run_end = [&](int j0) {
     int j1 = j0;
-    while (j1 < kOtSlabs && (CG_OT_RUN_SLABS == 0 || j1 - j0 < CG_OT_RUN_SLABS) &&
-           slab_off[j1 + 1] - slab_off[j0] <= kChunk)
+    while (j1 < kOtSlabs && slab_off[j1 + 1] - slab_off[j0] <= kChunk)
       j1++;
     return j1;
   };
@@ -1083,11 +899,11 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
     const int jb2 = ja2 < kOtSlabs ? run_end(ja2) : ja2;
     const int32_t pa2 = jb == ja ? pq[ja2 <= kOtSlabs ? ja2 : kOtSlabs] : pb;
     const int32_t pb2 = pq[jb2 <= kOtSlabs ? jb2 : kOtSlabs];  // in flight while this run is merged
-    if (jb == ja) {  // one slab of more than a chunk (queued by k_ot_slabs with CG_OT_EARLY_QUEUE)
-      if (!CG_OT_EARLY_QUEUE && threadIdx.x == 0) {
+    if (jb == ja) {  // one slab of more than a chunk
+      if (threadIdx.x == 0) {
         const int64_t sz = slab_off[ja + 1] - slab_off[ja];
-        if (CG_OT_MID && sz <= kMidChunk) mid[atomicAdd(mid_n, 1u)] = (int64_t(n) << 8) | ja;
-        else if (CG_OT_MID2 && sz <= kMid2Chunk) mid2[atomicAdd(mid2_n, 1u)] = (int64_t(n) << 8) | ja;
+        if (sz <= kMidChunk) mid[atomicAdd(mid_n, 1u)] = (int64_t(n) << 8) | ja;
+        else if (sz <= kMid2Chunk) mid2[atomicAdd(mid2_n, 1u)] = (int64_t(n) << 8) | ja;
         else big[atomicAdd(big_n, 1u)] = (int64_t(n) << 8) | ja;
       }
     } else if (slab_off[jb] > slab_off[ja]) {
@@ -1240,7 +1056,7 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
         ot_gather<true, 0, false, kOtItems, false, PIN>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc,
                                                         own, c0, n_el, key, rl);
-        ot_sort<4, 64, bool(CG_OT_MERGE_RUNS)>(key, n_el, uint32_t(j) << sb, 0, 1, pk, s);
+        ot_sort<4, 64, false>(key, n_el, uint32_t(j) << sb, 0, 1, pk, s);
         bool bad = false;
         for (int p = threadIdx.x; p < n_el; p += 256) {
           const uint32_t v = pk[p];
@@ -1259,216 +1075,15 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
   }
 }
 
-// ---- the per-node writer fused with the tile sort (time order, windows <= 4096 s) ----
-//
-// k_node_write<.., OFF16> followed by k_ot_tile wrote every event's 16-bit
-// offset and rule rule-major (6 B), then read them back to partition each
-// node-aligned 4096-event tile by slab.  k_node_tile builds a tile's events in
-// LDS straight from the segment records (k_seg_records: {rule, first
-// position, x, stride}; a progression's fire at segment position p is
-// t0 + x + p * stride, another rule's the band's rule-major fire list at
-// x + p) and partitions them there: 12 B per event less, one launch less.
-//
-// k_tile_rec_start: per tile, the segment holding its first position and the
-// record covering it (binary searches, one thread per tile).
-__global__ void k_tile_rec_start(const int64_t* __restrict__ seg_pos, const int64_t* __restrict__ seg_pair,
-                                 const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, int32_t K,
-                                 const int32_t* __restrict__ tile_node, const int64_t* __restrict__ tile_base,
-                                 const int64_t* __restrict__ node_off, const int64_t* __restrict__ n_tiles,
-                                 int64_t* __restrict__ tile_start) {
-  const int64_t t = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (t >= *n_tiles) return;
-  const int32_t n = tile_node[t];
-  const int64_t X = node_off[n] + (t - tile_base[n]) * kOtTile;  // the tile's first position
-  int64_t lo = int64_t(n) * K, hi = lo + K - 1;  // last segment starting at or before X
-  while (lo < hi) {
-    const int64_t mid = (lo + hi + 1) >> 1;
-    if (seg_pos[mid] <= X) lo = mid;
-    else hi = mid - 1;
-  }
-  const int64_t p0 = seg_pair[lo];
-  const int32_t rel = int32_t(X - seg_pos[lo]);
-  int32_t a = 0, b = seg_nrec[lo] - 1;  // last record whose first position is <= rel
-  while (a < b) {
-    const int32_t mid = (a + b + 1) >> 1;
-    if (recs[p0 + mid].dst <= rel) a = mid;
-    else b = mid - 1;
-  }
-  tile_start[2 * t] = lo;
-  tile_start[2 * t + 1] = a;
-}
-
-constexpr int kNtRecs = 512;  // records staged per pass
-constexpr int kNtSegs = 256;  // segments per window
-
-__global__ __launch_bounds__(256) void k_node_tile(
-    const int64_t* __restrict__ seg_pos, const int64_t* __restrict__ seg_pair, const int32_t* __restrict__ seg_nrec,
-    const PairRec* __restrict__ recs, const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times,
-    int64_t times_cap, int32_t K, int32_t B, int64_t t0, const int32_t* __restrict__ tile_node, const int64_t* __restrict__ tile_base,
-    const int64_t* __restrict__ node_off, const int64_t* __restrict__ tile_start, uint16_t* __restrict__ toff_out,
-    int32_t* __restrict__ rule_out, int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles,
-    int64_t* __restrict__ err) {
-  __shared__ OtRank<4, 64> s;
-  __shared__ uint32_t pk[kOtTile + kOtTile / 32];  // the pass's owner map (padded), then the sorted words
-  __shared__ int32_t rl[kOtTile];
-  __shared__ int4 tab[kNtRecs];            // per staged record {x, stride, window segment, rule}
-  __shared__ int32_t ps[kNtRecs + 1];      // its first position relative to the pass
-  __shared__ int32_t sg_cnt[kNtSegs + 1];  // records of the window's segments before segment j
-  __shared__ int64_t sg_rec[kNtSegs];      // global index of segment j's first record in the window
-  __shared__ int64_t sg_band[kNtSegs];     // band_lo of segment j (fire-list base of its gathers)
-  __shared__ int32_t sg_S[kNtSegs + 1];    // node-relative first position of segment j
-  __shared__ int32_t wsum[4];
-  int32_t* own = reinterpret_cast<int32_t*>(pk);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t t = blockIdx.x;
-  if (t >= *n_tiles) return;  // the grid is an upper bound (pipelined windows)
-  const int32_t n = tile_node[t];
-  const int64_t lo_n = node_off[n], E_n = node_off[n + 1] - lo_n;
-  const int32_t P = int32_t((t - tile_base[n]) * kOtTile);  // node-relative (a node holds < 2^30 events per band)
-  const int n_el = int(E_n - P < kOtTile ? E_n - P : kOtTile);
-  const int32_t hi_t = P + n_el;
-  const int ebase = w * (64 * kOtItems);
-  const int64_t s_end = int64_t(n) * K + K;
-  int64_t s_cur = tile_start[2 * t];
-  int32_t i_cur = int32_t(tile_start[2 * t + 1]);
-  uint32_t key[kOtItems];
-  int32_t done = P;  // positions below are computed
-  bool bad = false;
-  while (done < hi_t && s_cur < s_end) {
-    // a window of up to kNtSegs segments from s_cur (the first from record i_cur)
-    {
-      const int j = threadIdx.x;
-      const int64_t sj = s_cur + j;
-      int32_t cnt = 0;
-      if (sj < s_end) {
-        const int32_t S = int32_t(seg_pos[sj] - lo_n);
-        if (S < hi_t) {
-          const int32_t first = j == 0 ? i_cur : 0;
-          cnt = seg_nrec[sj] - first;
-          sg_rec[j] = seg_pair[sj] + first;
-          sg_band[j] = rule_off[int64_t(sj - int64_t(n) * K) * B];
-        }
-        sg_S[j] = S;
-      }
-      // exclusive block scan of cnt
-      int32_t inc = cnt;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int32_t y = __shfl_up(inc, o, 64);
-        if (lane >= o) inc += y;
-      }
-      if (lane == 63) wsum[w] = inc;
-      __syncthreads();
-      int32_t before = 0;
-      for (int ww = 0; ww < w; ww++) before += wsum[ww];
-      sg_cnt[j] = before + inc - cnt;
-      if (j == 255) sg_cnt[kNtSegs] = before + inc;
-      __syncthreads();
-    }
-    const int32_t Wn = sg_cnt[kNtSegs];
-    // segment j's end: the next segment's start, or the node's end
-    auto seg_end = [&](int j) -> int32_t {
-      const int64_t sj = s_cur + j + 1;
-      return sj < s_end ? (j + 1 < kNtSegs ? sg_S[j + 1] : int32_t(seg_pos[sj] - lo_n)) : int32_t(E_n);
-    };
-    for (int32_t fb = 0; fb < Wn && done < hi_t; fb += kNtRecs) {
-      const int nr = Wn - fb < kNtRecs ? int(Wn - fb) : kNtRecs;
-      int32_t pass_end = 0;
-      // stage the pass's records: first positions, and {x, stride, segment, rule}
-      for (int f = threadIdx.x; f < nr; f += 256) {
-        const int32_t fg = fb + f;
-        int a = 0, b = kNtSegs - 1;  // the segment holding flattened record fg
-        while (a < b) {
-          const int mid = (a + b + 1) >> 1;
-          if (sg_cnt[mid] <= fg) a = mid;
-          else b = mid - 1;
-        }
-        const int64_t g = sg_rec[a] + (fg - sg_cnt[a]);
-        const PairRec r = recs[g];
-        ps[f] = sg_S[a] + r.dst;
-        tab[f] = make_int4(r.x, r.st, a, r.rule);
-        if (f == nr - 1) {  // where the pass's last record ends
-          const bool last_of_seg = fg + 1 >= sg_cnt[a + 1];
-          pass_end = last_of_seg ? seg_end(a) : sg_S[a] + recs[g + 1].dst;
-          wsum[0] = pass_end;  // read after the barrier below
-        }
-      }
-      __syncthreads();
-      pass_end = wsum[0];
-      const int32_t plo = done, phi = pass_end < hi_t ? pass_end : hi_t;
-      __syncthreads();  // wsum reused by ot_owners
-      if (phi > plo) {
-        // first positions relative to the pass (the first record may start before it)
-        for (int f = threadIdx.x; f < nr; f += 256) ps[f] = max(ps[f] - plo, 0);
-        if (threadIdx.x == 0) ps[nr] = phi - plo;
-        __syncthreads();
-        ot_owners<4>(ps, nr, 0, phi - plo, own, wsum);
-#pragma unroll
-        for (int j = 0; j < kOtItems; j++) {
-          const int e = ebase + j * 64 + lane;
-          const int32_t q = P + e;
-          if (e < n_el && q >= plo && q < phi) {
-            const int4 r = tab[own[ot_pad(q - plo)]];
-            const int32_t p = q - sg_S[r.z];  // segment-relative position
-            int64_t off;
-            if (r.y != 0) {
-              off = int64_t(r.x) + int64_t(p) * r.y - 1;
-            } else {
-              const int64_t gi = sg_band[r.z] + int64_t(r.x) + p;  // the band's fire list
-              off = gi >= 0 && gi < times_cap ? times[gi] - t0 - 1 : -1;
-            }
-            bad |= off < 0 || off >= 4096;
-            key[j] = (uint32_t(off) << kOtIdxBits) | uint32_t(e);
-            rl[e] = r.w;
-          }
-        }
-        __syncthreads();  // own (pk) is rewritten by the next pass
-        done = phi;
-      }
-    }
-    // the next window: the segment after this one's last
-    s_cur += kNtSegs;
-    i_cur = 0;
-  }
-#pragma unroll
-  for (int j = 0; j < kOtItems; j++)
-    if (ebase + j * 64 + lane >= n_el) key[j] = 0u;
-  // by slab; a node's only tile by the whole offset (its last pass is the slab)
-  const bool one = tile_base[n + 1] - tile_base[n] == 1;
-  if (one) ot_sort<4, 64>(key, n_el, 0u, 0, 2, pk, s);
-  else ot_sort<4, 64, true>(key, n_el, 0u, kOtSlabBits, 1, pk, s);
-  int32_t* __restrict__ pt = pre + t * kOtPre;
-  if (threadIdx.x <= 64) pt[threadIdx.x] = s.dbase[threadIdx.x];
-  const int64_t base = lo_n + P;
-  for (int p = threadIdx.x; p < n_el; p += 256) {
-    const uint32_t v = pk[p];
-    toff_out[base + p] = uint16_t(v >> kOtIdxBits);
-    __builtin_nontemporal_store(rl[v & kOtIdxMask], rule_out + base + p);
-    if (p > 0) {
-      const uint32_t u = pk[p - 1];
-      if (one) bad |= ot_out_of_order(u, v, rl);
-      else if ((u >> (kOtIdxBits + kOtSlabBits)) == (v >> (kOtIdxBits + kOtSlabBits))) {
-        const int32_t ru = rl[u & kOtIdxMask], rv = rl[v & kOtIdxMask];
-        bad |= ru > rv || (ru == rv && (u >> kOtIdxBits) >= (v >> kOtIdxBits));
-      }
-    }
-  }
-  if (__ballot(bad) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
-}
-
 int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads - 1) / threads)); }
 
-#ifndef CG_OT_PACK
-#define CG_OT_PACK 1
-#endif
 
 }  // namespace
 
 // Windows <= 4096 s, in three steps enqueued on st with no host sync (buffers
 // sized from the output capacity cap, grids upper bounds trimmed on the
 // device): order_setup (node-aligned tiles from the node offsets), the tiles
-// (k_ot_tile over a written rule-major result, or k_node_tile straight from
-// the segment records), order_tail (slab offsets, k_ot_merge, k_ot_big).
+// (k_ot_tile over the writer's lists), order_tail (slab offsets, k_ot_merge, k_ot_big).
 namespace {
 
 int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipStream_t st, int64_t* Tmax) {
@@ -1480,13 +1095,12 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
   // growing a buffer frees the old one: earlier windows' kernels finish first
   if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(*Tmax) ||
       c->ts_hist.cap < size_t(*Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
-      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->scan_tmp.cap < scan_temp_bytes(N) ||
-      c->ts_rec.cap < size_t(2 * *Tmax))
+      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->scan_tmp.cap < scan_temp_bytes(N))
     HIPCHK(hipStreamSynchronize(st));
   int rc;
   if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1)) || (rc = c->ts_tile_node.ensure(*Tmax)) ||
       (rc = c->ts_hist.ensure(*Tmax * kOtPre)) || (rc = c->node_time2.ensure(toff_words)) ||
-      (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) || (rc = c->ts_rec.ensure(2 * *Tmax)) ||
+      (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) ||
       (rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N)))))
     return rc;
   hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, node_off, N, kOtTile, cap, c->ts_cnt.p);
@@ -1499,14 +1113,8 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
 // window fits 64 of them (H <= 2048: a dense node's 30-min window then puts
 // half as many events in a slab, so they fit k_ot_mid's chunks instead of
 // k_ot_big's two reads).  The tile pre rows keep 64 slabs either way.
-#ifndef CG_OT_SLAB32
-#define CG_OT_SLAB32 1
-#endif
-int ot_slab_bits(int64_t H) { return CG_OT_SLAB32 && H <= 2048 ? kOtSlabBits - 1 : kOtSlabBits; }
+int ot_slab_bits(int64_t H) { return H <= 2048 ? kOtSlabBits - 1 : kOtSlabBits; }
 
-#ifndef CG_OT_MID_AFTER_DENSE
-#define CG_OT_MID_AFTER_DENSE 1
-#endif
 #ifndef CG_OT_DENSE_BPC
 #define CG_OT_DENSE_BPC 2  // blocks per CU of the dense merge's persistent grid
 #endif
@@ -1528,12 +1136,8 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   // nodes' merge runs on its own stream beside the sparse one (few dense
   // nodes after all the sparse ones would run as a tail at low occupancy)
   const int64_t dense_min = int64_t(CG_OT_DENSE_PER_SLAB) * std::max<int64_t>(1, (H + 63) / 64);
-  const bool pack = CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
-  OtQueues oq{c->ts_off.p, slab_tab + int64_t(N) * kOtPre, slab_tab + int64_t(N) * kOtPre + int64_t(N) * kOtSlabs,
-              big_n, big_n + 1, big_n + 3, node_off, dense_min, 64 * kOtMergeWaves * kOtMergeItems,
-              64 * kOtDenseWaves * kOtDenseItems, (CG_OT_EARLY_QUEUE || (pack && pin && CG_OT_PIPE)) ? 1 : 0};
-  const bool early = oq.on != 0;
-  hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab, oq);
+  const bool pack = R <= (int64_t(1) << kOtRuleBits);
+  hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
   if (!c->st_ot) {  // created together: the ctx holds all three or none
     hipStream_t so = nullptr;
     hipEvent_t ef = nullptr, ej = nullptr;
@@ -1550,17 +1154,13 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   }
   HIPCHK(hipEventRecord(c->ot_fork, st));
   HIPCHK(hipStreamWaitEvent(c->st_ot, c->ot_fork, 0));
-  // rule indices below 2^20: (offset, rule) packed in one word (CG_OT_PACK)
+  // rule indices below 2^20: (offset, rule) packed in one word
   auto merges = [&](auto m4, auto m8, auto mid_k, auto mid2_k) {
     // the dense merge: a persistent grid (2 blocks per CU) taking nodes by ticket
     hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtDenseWaves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
                        dense_min, INT64_MAX, big_n + 2, err, sb);
-    if (early)  // k_ot_mid's 16-wave form behind the dense merge, beside the sparse one
-      hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, c->st_ot, toff, c->node_rule2.p,
-                         c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
-                         big_n + 3, err, sb);
     hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
                        mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err, sb);
@@ -1570,17 +1170,14 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
     // so it is queued behind both merges on the dense merge's stream: it
     // starts when it can run, and an empty queue costs one short launch
     // instead of a launch that spans the dense merge.
-    if (CG_OT_MID_AFTER_DENSE) {
-      (void)hipEventRecord(c->ot_fork, st);  // the 4-wave merge's queue entries are in
-      (void)hipStreamWaitEvent(c->st_ot, c->ot_fork, 0);
-    }
-    hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, CG_OT_MID_AFTER_DENSE ? c->st_ot : st,
+    (void)hipEventRecord(c->ot_fork, st);  // the 4-wave merge's queue entries are in
+    (void)hipStreamWaitEvent(c->st_ot, c->ot_fork, 0);
+    hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, c->st_ot,
                        toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p,
                        c->node_rule.p, mid, big_n + 1, err, sb);
     (void)hipEventRecord(c->ot_join, c->st_ot);
     (void)hipStreamWaitEvent(st, c->ot_join, 0);
-    if (!early)
-      hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
+    hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
                          c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
                          big_n + 3, err, sb);
   };
@@ -1616,7 +1213,7 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   if (rc) return rc;
   uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
   // the tiles stored as packed words when every rule index is below 2^20
-  const bool pack = CG_OT_TILE_PACK && CG_OT_PACK && c->pn_R <= (int64_t(1) << kOtRuleBits);
+  const bool pack = c->pn_R <= (int64_t(1) << kOtRuleBits);
   const int sb = ot_slab_bits(H);
   auto tile = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p, c->ts_tile_node.p,
@@ -1631,23 +1228,6 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
     pack ? tile(k_ot_tile<0, true>) : tile(k_ot_tile<0, false>);
   }
   return order_tail(c, node_off, N, t0, H, st, err, c->pn_R, pack, sb);
-}
-
-// The per-node writer and tile sort in one (k_node_tile), then the merge: the
-// lists of a window <= 4096 s in (time, rule) order straight from the segment
-// records, into c->node_time / c->node_rule.
-int order_fused_enqueue(cg_ctx* c, const FusedOrderArgs& a, hipStream_t st, int64_t* err) {
-  if (a.N == 0 || a.cap == 0) return CG_OK;
-  int64_t Tmax = 0;
-  int rc = order_setup(c, a.node_off, a.N, a.cap, st, &Tmax);
-  if (rc) return rc;
-  const int64_t* n_tiles = c->ts_base.p + a.N;
-  hipLaunchKernelGGL(k_tile_rec_start, dim3(gridn(Tmax, 256)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec,
-                     a.recs, a.K, c->ts_tile_node.p, c->ts_base.p, a.node_off, n_tiles, c->ts_rec.p);
-  hipLaunchKernelGGL(k_node_tile, dim3(unsigned(Tmax)), dim3(256), 0, st, a.seg_pos, a.seg_pair, a.seg_nrec, a.recs,
-                     a.rule_off, a.times, a.times_cap, a.K, a.B, a.t0, c->ts_tile_node.p, c->ts_base.p, a.node_off, c->ts_rec.p,
-                     reinterpret_cast<uint16_t*>(c->node_time2.p), c->node_rule2.p, c->ts_hist.p, n_tiles, err);
-  return order_tail(c, a.node_off, a.N, a.t0, 4096, st, err, c->pn_R, false, kOtSlabBits);  // 16-bit tiles, 64-s slabs
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
@@ -1669,12 +1249,7 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   return rc;
 }
 
-#ifndef CG_OT_PIN
-#define CG_OT_PIN 1  // 0: the time-order writer emits 16-bit offsets + rules, not packed words (A/B)
-#endif
-bool pn_pack_ok(int64_t R) {
-  return CG_OT_PIN && CG_OT_TILE_PACK && CG_OT_PACK && R <= (int64_t(1) << kOtRuleBits);
-}
+bool pn_pack_ok(int64_t R) { return R <= (int64_t(1) << kOtRuleBits); }
 
 bool order_lsd_only() {
   static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;

@@ -292,21 +292,6 @@ __global__ void k_seg_bounds(const int64_t* __restrict__ nt_off, const int32_t* 
   seg_pair[t] = lo;
 }
 
-// Periodic rules (RuleInfo / PairRec st < 0): a window's fires that step by s
-// with a wrap every m fires, fire p = A + (v / m) * P + (v % m) * s with
-// v = p + ph -- e.g. `0 */13 * * * *` over (t0, t0 + 1 h]: minutes 13, 26,
-// 39, 52, then 60 (the next hour's minute 0).  P is 60 or 3600; st packs
-// s (bits 0-11), m (12-17), ph (18-23) and P (bit 24: 3600) under bit 31.
-__device__ __forceinline__ int64_t periodic_fire(int32_t st, int64_t A, int32_t p) {
-  const uint32_t s = uint32_t(st) & 0xFFFu, m = (uint32_t(st) >> 12) & 63u, ph = (uint32_t(st) >> 18) & 63u;
-  const uint32_t P = (uint32_t(st) >> 24) & 1u ? 3600u : 60u;
-  const uint32_t v = uint32_t(p) + ph;  // < 2^24: fires of one rule in one window
-  uint32_t k = uint32_t(float(v) * (1.0f / float(m)));
-  const int32_t r = int32_t(v) - int32_t(k * m);
-  k = r < 0 ? k - 1u : (r >= int32_t(m) ? k + 1u : k);
-  return A + int64_t(k) * P + int64_t(v - k * m) * s;
-}
-
 // Per rule of the window's rule-major CSR, one 16-byte RuleInfo: its fire
 // count, the band-relative index of its first fire, and whether its fires
 // form an arithmetic progression {first fire - t0, stride} (stride 0: they do
@@ -321,22 +306,8 @@ __device__ __forceinline__ int64_t periodic_fire(int32_t st, int64_t A, int32_t 
 #ifndef CG_NODE_AP
 #define CG_NODE_AP 1
 #endif
-#ifndef CG_NODE_TILE_FUSED
-#define CG_NODE_TILE_FUSED 0  // the per-node writer fused with the time-order tile sort (k_node_tile; A/B only)
-#endif
-#ifndef CG_NODE_PERIODIC
-#define CG_NODE_PERIODIC 0  // 1: periodic records (A/B: slower, profiles/r05_ab_periodic.txt; the fused tile writer reads progressions only)
-#endif
 constexpr int kApRules = 256;
-#ifndef CG_SEG_NEMASK
-#define CG_SEG_NEMASK 0  // 1: k_seg_records reads a per-window bit per rule (fires in the window) before gathering its RuleInfo (A/B: no gain, profiles/r05_ab_nonempty_mask.txt)
-#endif
-// the rule-info buffer: R RuleInfos, then (CG_SEG_NEMASK) the window's
-// non-empty-rule bitmask, one bit per rule (a 16-B slot holds 128 bits)
-inline int64_t rule_info_slots(int64_t R) { return std::max<int64_t>(R, 1) + (CG_SEG_NEMASK ? (R + 255) / 128 : 0); }
-__device__ __forceinline__ const uint64_t* ne_mask_of(const RuleInfo* info, int64_t R) {
-  return reinterpret_cast<const uint64_t*>(info + (R > 0 ? R : 1));
-}
+inline int64_t rule_info_slots(int64_t R) { return std::max<int64_t>(R, 1); }
 __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ rule_off,
                                                     const int64_t* __restrict__ times, int64_t R, int64_t t0,
                                                     int32_t B, int64_t cap, RuleInfo* __restrict__ info,
@@ -344,15 +315,11 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
   __shared__ int64_t off[kApRules + 1];
   __shared__ int64_t step[kApRules];
   __shared__ int32_t ok[kApRules];
-  __shared__ int32_t pst[kApRules];  // a periodic candidate's packed st (0: none)
-  __shared__ int64_t pA[kApRules];   // and its A
   const int64_t r0 = int64_t(blockIdx.x) * kApRules;
   const int nr = int(R - r0 < kApRules ? R - r0 : kApRules);
   const int tid = threadIdx.x;
-  uint64_t* ne = const_cast<uint64_t*>(ne_mask_of(info, R)) + (r0 >> 6);
   if (rule_off[R] > cap) {  // a pipelined window past the fire-time capacity: no fires read, none written
     if (tid < nr) info[r0 + tid] = RuleInfo{0, 0, 0, 0};
-    if (CG_SEG_NEMASK && (tid & 63) == 0 && r0 + tid < R) ne[tid >> 6] = 0;
     return;
   }
   const int64_t band_lo = rule_off[(r0 / B) * B];  // B is a multiple of kApRules
@@ -368,7 +335,6 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
     off[tid] = a;
     step[tid] = cnt > 1 ? times[a + 1] - first : 1;
     ok[tid] = CG_NODE_AP;
-    pst[tid] = 0;
   }
   if (tid == 0) off[nr] = rule_off[r0 + nr];
   __syncthreads();
@@ -401,74 +367,13 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
     }
   }
   __syncthreads();
-  // Not a progression: a periodic candidate from the first steps (one thread
-  // per rule: steps of s with a wrap g every m fires), then every fire of the
-  // candidates checked against the formula, lanes over the block's events.
-  constexpr bool kPeriodic = CG_NODE_PERIODIC && !CG_NODE_TILE_FUSED;
-  bool any = false;
-  if (kPeriodic && tid < nr && cnt >= 3 && !ok[tid]) {
-    const int64_t* __restrict__ t = times + off[tid];
-    const int lim = cnt - 1 < 130 ? int(cnt - 1) : 130;  // steps looked at
-    const int64_t d0 = t[1] - t[0];
-    int i = 1;
-    while (i < lim && t[i + 1] - t[i] == d0) i++;
-    if (i < lim) {
-      const int64_t b = t[i + 1] - t[i];
-      int64_t sv, g;
-      int m, ph;
-      const bool h2 = i == 1 && cnt >= 4 && t[3] - t[2] == b;  // the first step is the wrap
-      int j = h2 ? 2 : i + 1;
-      const int64_t sj = h2 ? b : d0;
-      while (j < lim && t[j + 1] - t[j] == sj) j++;
-      if (h2) {  // fire 0 is the last phase; the next wrap after step j
-        sv = b;
-        g = d0;
-        m = j < lim ? j : int(cnt - 1 > 1 ? cnt - 1 : 1);
-        ph = m - 1;
-      } else {  // fires 0..i in one period (fire i the last phase)
-        sv = d0;
-        g = b;
-        m = j < lim ? j - i : int(i + 1 > cnt - 1 - i ? i + 1 : cnt - 1 - i);
-        ph = m - 1 - i;
-      }
-      const int64_t P = int64_t(m - 1) * sv + g;
-      if (sv > 0 && sv < 4096 && g > 0 && m >= 2 && m <= 63 && ph >= 0 && ph < m && (P == 60 || P == 3600)) {
-        const int64_t A = t[0] - int64_t(ph) * sv;
-        if (A - t0 >= INT32_MIN && A - t0 <= INT32_MAX) {
-          pst[tid] = int32_t(0x80000000u | uint32_t(sv) | (uint32_t(m) << 12) | (uint32_t(ph) << 18) |
-                             (P == 3600 ? (1u << 24) : 0u));
-          pA[tid] = A;
-          any = true;
-        }
-      }
-    }
-  }
-  if (kPeriodic && __syncthreads_or(any)) {
-    for (int64_t e = off[0] + tid; e < e_end; e += blockDim.x) {
-      int lo = 0, hi = nr - 1;  // the last rule whose list starts at or before e
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (off[mid] <= e) lo = mid;
-        else hi = mid - 1;
-      }
-      const int32_t ps = pst[lo];
-      if (ps != 0 && times[e] != periodic_fire(ps, pA[lo], int32_t(e - off[lo]))) pst[lo] = 0;
-    }
-    __syncthreads();
-  }
   if (tid < nr) {
     const int64_t rel = first - t0, s = step[tid];
     const bool prog = cnt > 0 && ok[tid] && rel >= 0 && rel <= INT32_MAX && s > 0 && s <= INT32_MAX;
-    const int32_t ps = prog || !kPeriodic ? 0 : pst[tid];
     // counts and band-relative indices are < 2^30 (k_seg_records checks the
     // band span and fails the call otherwise)
     info[r0 + tid] = RuleInfo{int32_t(cnt), int32_t(off[tid] - band_lo),
-                              prog ? int32_t(rel) : (ps != 0 ? int32_t(pA[tid] - t0) : 0),
-                              prog ? int32_t(s) : ps};
-  }
-  if (CG_SEG_NEMASK) {  // bit r of the window's non-empty-rule mask
-    const uint64_t b = __ballot(tid < nr && cnt > 0);
-    if ((tid & 63) == 0 && r0 + tid < R) ne[tid >> 6] = b;
+                              prog ? int32_t(rel) : 0, prog ? int32_t(s) : 0};
   }
 }
 
@@ -585,20 +490,9 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
     for (int32_t pc = 0; pc < rounds_len; pc += L * P) {
       if (pc > 0) rules(cur, pc, r);  // segments of more than L*P pairs
       RuleInfo g[P];
-      if (CG_SEG_NEMASK && !CG_SEG_NOINFO) {
-        // about half of a 1-h window's rules do not fire: their pairs need
-        // no RuleInfo (cnt 0), so only the rules whose bit is set are gathered
-        const uint64_t* __restrict__ ne = ne_mask_of(info, R);
-        uint32_t mb[P];
 #pragma unroll
-        for (int u = 0; u < P; u++) mb[u] = r[u] >= 0 ? uint32_t(ne[r[u] >> 6] >> (r[u] & 63)) & 1u : 0u;
-#pragma unroll
-        for (int u = 0; u < P; u++) g[u] = mb[u] ? info[r[u]] : RuleInfo{0, 0, 0, 0};
-      } else {
-#pragma unroll
-        for (int u = 0; u < P; u++)
-          g[u] = r[u] >= 0 ? (CG_SEG_NOINFO ? RuleInfo{1, 0, 0, 1} : info[r[u]]) : RuleInfo{0, 0, 0, 0};
-      }
+      for (int u = 0; u < P; u++)
+        g[u] = r[u] >= 0 ? (CG_SEG_NOINFO ? RuleInfo{1, 0, 0, 1} : info[r[u]]) : RuleInfo{0, 0, 0, 0};
 #pragma unroll
       for (int u = 0; u < P; u++) {
         // events before this pair: half-wave inclusive scan of the counts
@@ -610,10 +504,8 @@ __global__ __launch_bounds__(256, CG_SEG_WPE) void k_seg_records(const int64_t* 
         if (g[u].cnt > 0) {
           const int64_t at = cur.p0 + nrec + __popc(ne & below);
           const int64_t x = int64_t(g[u].first) - d * g[u].st;
-          const bool prog = (CG_NODE_PERIODIC ? g[u].st > 0 : g[u].st != 0) && x >= INT32_MIN && x <= INT32_MAX;
-          const bool per = CG_NODE_PERIODIC && g[u].st < 0;  // periodic: x = A - t0, the writer counts from d
-          recs[at] = PairRec{r[u], int32_t(d), int32_t(per ? int64_t(g[u].first) : (prog ? x : int64_t(g[u].off) - d)),
-                             per || prog ? g[u].st : 0};
+          const bool prog = g[u].st != 0 && x >= INT32_MIN && x <= INT32_MAX;
+          recs[at] = PairRec{r[u], int32_t(d), int32_t(prog ? x : int64_t(g[u].off) - d), prog ? g[u].st : 0};
         }
         run += half_total(incl);
         nrec += __popc(ne);
@@ -822,11 +714,7 @@ __global__ __launch_bounds__(256) void k_node_write(
         const int32_t sv = __builtin_amdgcn_ds_bpermute(own << 2, sst);
         int32_t rv = __builtin_amdgcn_ds_bpermute(own << 2, rr);
         const bool in = q >= qw && q < we;
-        int64_t val = in && (CG_NODE_PERIODIC ? sv > 0 : sv != 0) ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
-        if (CG_NODE_PERIODIC && __ballot(in && sv < 0)) {  // periodic records: fire q - (their first position)
-          const int32_t d0 = __builtin_amdgcn_ds_bpermute(own << 2, dst);
-          if (in && sv < 0) val = periodic_fire(sv, t0 + int64_t(dl), q - d0);
-        }
+        int64_t val = in && sv != 0 ? t0 + int64_t(dl) + int64_t(q - q_lo) * sv : 0;
         const int32_t gi = in && sv == 0 ? q + dl - q_lo : -1;
         if (__ballot(gi >= 0)) {  // waited for here, not after the branch
           if (gi >= 0) val = (V & 1) ? int64_t(gi) : tb[gi];
@@ -860,10 +748,7 @@ __global__ __launch_bounds__(256) void k_node_write(
         const int32_t bend = (e & ~63) < bl ? (e & ~63) : bl;  // blocks [b, bend) all o's
         const int32_t dl = __builtin_amdgcn_readlane(dlt, o), sv = __builtin_amdgcn_readlane(sst, o);
         const int32_t rv = __builtin_amdgcn_readlane(rr, o);
-        if (CG_NODE_PERIODIC && sv < 0) {  // periodic
-          const int32_t d0 = __builtin_amdgcn_readlane(dst, o);
-          for (; b < bend; b += 64) put(b + lane, periodic_fire(sv, t0 + int64_t(dl), b + lane - d0), rv);
-        } else if (sv != 0) {
+        if (sv != 0) {
           int64_t val = t0 + int64_t(dl) + int64_t(b + lane - q_lo) * sv;
           const int64_t step = int64_t(64) * sv;
           for (; b < bend; b += 64, val += step) {
@@ -1054,15 +939,6 @@ __global__ __launch_bounds__(256) void k_node_checksums(const int64_t* __restric
     out[2 * blockIdx.x + 1] = s[1][0] + s[1][1] + s[1][2] + s[1][3];
   }
 }
-
-// Time order of windows <= 4096 s: 1 = k_node_tile builds the tiles straight
-// from the segment records (no 16-bit list written and read back); 0 = the
-// writer's 16-bit lists, then k_ot_tile.  Same-box A/B
-// (profiles/r04_ab_pernode_builds.txt): pernode --time-order 10.9 ms per step
-// fused vs 9.4 separate -- k_node_tile (5.9 ms) waits on its dependent loads
-// per tile (segment window, records, gathers) where the writer (1.5 ms) and
-// k_ot_tile (2.65 ms) stream.
-// (CG_NODE_TILE_FUSED is defined beside CG_NODE_PERIODIC, above)
 
 // persistent k_node_write grid: as many 4-wave blocks per CU as its register
 // and LDS use let run at once (no block of the grid waits for a slot)
@@ -1384,21 +1260,15 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
   // (time, rule) order of a window <= 4096 s (the predicate of
   // order_by_time_locked's tile sort: bits <= 12, not LSD): the writer emits
-  // 16-bit offsets t - t0 - 1 for the tile sort; or (CG_NODE_TILE_FUSED) the
-  // writer fused with the tile sort, k_node_tile, then the merge
+  // 16-bit offsets t - t0 - 1 (or packed words) for the tile sort
   const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
-  const bool fused = off16 && CG_NODE_TILE_FUSED;
   // packed words (offset << 20 | rule) when every rule index fits 20 bits
   const int in_mode = !off16 ? kInTimes : (pn_pack_ok(R) ? kInPacked : kIn16);
   c->pn_res_host[2] = 0;
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
-    if (fused) {
-      const FusedOrderArgs fa{c->seg_pos.p, c->seg_pair.p, c->seg_nrec.p, c->recs.p, c->offsets.p, c->times.p,
-                              int64_t(c->times.cap), c->node_off.p, N, K, B, cap, t0};
-      if (NK > 0 && cap > 0 && (rc = order_fused_enqueue(c, fa, st, c->pn_res_dev + 2))) return rc;
-    } else if (NK > 0 && cap > 0 && off16) {
+    if (NK > 0 && cap > 0 && off16) {
       if (in_mode == kInPacked)
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
                            dim3(256), 0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,
@@ -1448,17 +1318,6 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_cache_mode = mode;
   *n_events = En;
   *nnz_out = nnz;
-  if (fused) {  // written in (time, rule) order
-    if (c->pn_res_host[2]) {
-      c->pn_E = 0;
-      c->pn_valid = false;
-      *n_events = 0;
-      return cg_fail(CG_EHIP, kOrderCheckMsg);
-    }
-    c->pn_time_ordered = true;
-    c->kt[12] = 0.f;  // inside the writer's time (kt[8])
-    return CG_OK;
-  }
   // (time, rule) order: the tile sort + merge (or, past 4096 s, the LSD
   // passes) after the writer; if it fails nothing is readable (the lists may
   // hold the writer's 16-bit offsets)
@@ -1660,11 +1519,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     // wave slots beside this writer instead of waiting for it to retire
     static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-    if (timed && CG_NODE_TILE_FUSED) {  // the writer fused with the tile sort, then the merge
-      const FusedOrderArgs fa{a.seg_pos.p, c->seg_pair.p, a.seg_nrec.p, a.recs.p, a.rm.offsets.p, a.times.p,
-                              rm_cap, a.node_off.p, N, K, B, node_cap, t0};
-      if ((rc = order_fused_enqueue(c, fa, st, a.res_dev + 2))) return rc;
-    } else if (timed) {  // packed words (or 16-bit offsets), then the tile sort + merge on the same stream
+    if (timed) {  // packed words (or 16-bit offsets), then the tile sort + merge on the same stream
       const int in_mode = pn_pack_ok(R) ? kInPacked : kIn16;
       if (in_mode == kInPacked)
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
@@ -1970,7 +1825,10 @@ int merge_ranks_locked(cg_ctx* c, hipStream_t st, int32_t N, int32_t W, const in
     if (nonempty >= 2) big = std::max(big, nb[W] - nb[0]);
   }
   if (tp[size_t(NW)] == 0) return CG_OK;
-  scratch_ev = std::max(scratch_ev, big);
+  // the scratch never exceeds the events of the lists being merged (a small
+  // CSR with the default 2-GiB budget needs only its own size), nor falls
+  // below the largest merging node
+  scratch_ev = std::max(std::min(scratch_ev, h_rb[NW + N - 1] - h_rb[0]), big);
   int rc;
   if ((rc = c->mr_rb.ensure(size_t(N) * (W + 1))) || (rc = c->mr_tp.ensure(size_t(NW + 1))) ||
       (rc = scr_t.ensure(size_t(scratch_ev))) || (rc = scr_r.ensure(size_t(scratch_ev))))

@@ -197,93 +197,6 @@ __device__ __forceinline__ void drive(Val&& value, Step&& step, int64_t p0, int6
   }
 }
 
-// 16-byte stores (CG_WRITE_PAIRS): a long piece is written in aligned
-// 128-fire blocks where lane l holds fires 2l and 2l + 1 of the block -- one
-// 1 KB store instruction per block instead of two 512 B ones.  The generator
-// g is re-seeded per phase (g.init(x): this lane's fire x of the piece) and
-// stepped by +1 / +127 between a lane's two fires and on to the next block.
-// The head block and the last full and partial blocks keep the 64-fire lane
-// mapping and the Pending protocol of drive().  All lanes call every g
-// member (the table generator reads across lanes).
-#ifndef CG_WRITE_PAIRS
-#define CG_WRITE_PAIRS 0
-#endif
-#ifndef CG_WRITE_PAIR_MIN
-#define CG_WRITE_PAIR_MIN 512  // pieces shorter than this keep drive() (the re-seeds cost a few divisions)
-#endif
-#ifndef CG_WRITE_PAIR_BATCH
-#define CG_WRITE_PAIR_BATCH 4
-#endif
-typedef long long cg_v2i64 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void put2(int64_t* p, int64_t a, int64_t b) {
-  cg_v2i64 v = {a, b};
-  if (CG_WRITE_NT) __builtin_nontemporal_store(v, reinterpret_cast<cg_v2i64*>(p));
-  else *reinterpret_cast<cg_v2i64*>(p) = v;
-}
-template <class Gen>
-__device__ __forceinline__ void drive2(Gen& g, int64_t p0, int64_t p1, Pending& pd, int64_t* __restrict__ times) {
-  const int lane = threadIdx.x & 63;
-  const int64_t b0 = p0 & ~int64_t(63);
-  const bool mine0 = b0 + lane >= p0;
-  g.init(mine0 ? b0 + lane - p0 : 0);
-  int64_t v = g.value();
-  if (!mine0) v = pd.val;
-  if (b0 + 64 > p1) {
-    pd.blk = b0;
-    pd.val = v;
-    return;
-  }
-  put(times + b0 + lane, v);
-  pd.blk = -1;
-  int64_t b = b0 + 64;
-  if (b & 127) {  // one 64-fire block to reach a 128-aligned start
-    g.init(b + lane - p0);
-    const int64_t u = g.value();
-    if (b + 64 > p1) {
-      pd.blk = b;
-      pd.val = u;
-      return;
-    }
-    put(times + b + lane, u);
-    b += 64;
-  }
-  if (b + 128 <= p1) {
-    g.init(b + 2 * lane - p0);
-    constexpr int kB = CG_WRITE_PAIR_BATCH;
-    for (; b + kB * 128 <= p1; b += kB * 128) {
-      int64_t va[kB], vb[kB];
-#pragma unroll
-      for (int u = 0; u < kB; u++) {
-        va[u] = g.value();
-        g.step(1);
-        vb[u] = g.value();
-        g.step(127);
-      }
-#pragma unroll
-      for (int u = 0; u < kB; u++) asm volatile("" : "+v"(va[u]), "+v"(vb[u]));
-#pragma unroll
-      for (int u = 0; u < kB; u++) put2(times + b + 128 * u + 2 * lane, va[u], vb[u]);
-    }
-    for (; b + 128 <= p1; b += 128) {
-      const int64_t x = g.value();
-      g.step(1);
-      const int64_t y = g.value();
-      g.step(127);
-      put2(times + b + 2 * lane, x, y);
-    }
-  }
-  if (b + 64 <= p1) {
-    g.init(b + lane - p0);
-    put(times + b + lane, g.value());
-    b += 64;
-  }
-  if (b < p1) {
-    g.init(b + lane - p0);
-    pd.blk = b;
-    pd.val = g.value();
-  }
-}
-
 // Fires [p0, p1) of closed-form run w (run start roff), wave-cooperatively.
 // A fire's index g = rank(anchor) - 1 + (p - roff) counts (day, hour, minute,
 // second) combinations from the anchor's local day, so it is carried as
@@ -346,93 +259,6 @@ __device__ void coop_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_
   const uint32_t nD = uint32_t(__builtin_popcount(dmask));
   const bool apS = ap_level(c.S, nS, &s0, &ss), apM = ap_level(c.M, nM, &m0, &ms);
   const bool apH = ap_level(c.H, nH, &h0, &hs), apD = ap_level(dmask, nD, &d0, &ds);
-  if (CG_WRITE_PAIRS && p1 - p0 >= CG_WRITE_PAIR_MIN) {
-    // the generator of drive2: digits of g0 + x, stepped by constant digit
-    // vectors (+1: (1, 0, 0, 0) with carries; +127: its own digits)
-    struct Dig {
-      uint32_t d, h, m, s;
-    };
-    const uint32_t g0 = cf_rank(c, int32_t(tf)) - 1u + uint32_t(p0 - roff);
-    const float iC = 1.0f / float(c.C), iMS = 1.0f / float(c.nMS);
-    auto digits = [&](uint32_t n) -> Dig {  // n < 2^24
-      Dig r;
-      r.d = fdiv(n, c.C, iC);
-      n -= r.d * c.C;
-      r.h = fdiv(n, c.nMS, iMS);
-      n -= r.h * c.nMS;
-      r.m = fdiv(n, nS, iS);
-      r.s = n - r.m * nS;
-      return r;
-    };
-    const Dig k127 = digits(127u);
-    struct Gen {
-      Dig x;
-      Dig k127;
-      uint32_t nS, nM, nH;
-      uint32_t g0, C, nMS;
-      float iC, iMS, iS;
-      int mode;  // 0 affine, 1 tables
-      int64_t C0, base;
-      uint32_t ws, wm, wh, wd;
-      int32_t ts, tm, th, td;
-      __device__ void init(int64_t xi) {
-        uint32_t n = g0 + uint32_t(xi);
-        x.d = fdiv(n, C, iC);
-        n -= x.d * C;
-        x.h = fdiv(n, nMS, iMS);
-        n -= x.h * nMS;
-        x.m = fdiv(n, nS, iS);
-        x.s = n - x.m * nS;
-      }
-      __device__ void step(int k) {
-        const uint32_t a0 = k == 1 ? 1u : k127.s, a1 = k == 1 ? 0u : k127.m, a2 = k == 1 ? 0u : k127.h,
-                       a3 = k == 1 ? 0u : k127.d;
-        x.s += a0;
-        const uint32_t cs = x.s >= nS;
-        x.s -= cs ? nS : 0u;
-        x.m += a1 + cs;
-        const uint32_t cm = x.m >= nM;
-        x.m -= cm ? nM : 0u;
-        x.h += a2 + cm;
-        const uint32_t ch = x.h >= nH;
-        x.h -= ch ? nH : 0u;
-        x.d += a3 + ch;
-      }
-      __device__ int64_t value() const {
-        if (mode == 0)
-          return C0 + int64_t(__umul24(x.s, ws) + __umul24(x.m, wm) + __umul24(x.h, wh) + __umul24(x.d, wd));
-        return base + int64_t(rank_at(td, x.d) + rank_at(th, x.h) + rank_at(tm, x.m) + rank_at(ts, x.s));
-      }
-    };
-    Gen gen;
-    gen.k127 = k127;
-    gen.nS = nS;
-    gen.nM = nM;
-    gen.nH = nH;
-    gen.g0 = g0;
-    gen.C = c.C;
-    gen.nMS = c.nMS;
-    gen.iC = iC;
-    gen.iMS = iMS;
-    gen.iS = iS;
-    if (apS && apM && apH && apD) {
-      gen.mode = 0;
-      gen.C0 = sg.base + s0 + 60 * m0 + 3600 * h0 + 86400 * int32_t(jf);
-      gen.ws = uint32_t(ss);
-      gen.wm = 60u * uint32_t(ms);
-      gen.wh = 3600u * uint32_t(hs);
-      gen.wd = 86400u * uint32_t(ds);
-    } else {
-      gen.mode = 1;
-      gen.base = sg.base;
-      gen.ts = rank_table(c.S, 1);
-      gen.tm = rank_table(c.M, 60);
-      gen.th = rank_table(c.H, 3600);
-      gen.td = rank_table(uint64_t(dmask), 86400) + int32_t(jf) * 86400;
-    }
-    drive2(gen, p0, p1, pd, times);
-    return;
-  }
   if (apS && apM && apH && apD) {
     const int64_t C0 = sg.base + s0 + 60 * m0 + 3600 * h0 + 86400 * int32_t(jf);  // d0 == 0
     const uint32_t ws = uint32_t(ss), wm = 60u * uint32_t(ms), wh = 3600u * uint32_t(hs),
@@ -497,17 +323,6 @@ __device__ void tiny_cf(const WinRun& w, int64_t roff, const Segment& sg, int64_
 __device__ void coop_every(const WinRun& w, int64_t roff, int64_t p0, int64_t p1, Pending& pd,
                            int64_t* __restrict__ times) {
   const int64_t D = int64_t(w.sp.sec);
-  if (CG_WRITE_PAIRS && p1 - p0 >= CG_WRITE_PAIR_MIN) {
-    struct Gen {
-      int64_t t, a, D;
-      __device__ void init(int64_t x) { t = a + (x + 1) * D; }
-      __device__ void step(int k) { t += int64_t(k) * D; }
-      __device__ int64_t value() const { return t; }
-    };
-    Gen gen{0, w.anchor + (p0 - roff) * D, D};
-    drive2(gen, p0, p1, pd, times);
-    return;
-  }
   int64_t t = w.anchor + (p0 - roff + int64_t(lane_offset(p0)) + 1) * D;
   const int64_t st = 64 * D;
   drive<false>([&]() { return t; }, [&]() { t += st; }, p0, p1, pd, times);

@@ -193,6 +193,8 @@ def place_node_slice(node_off, time, rule, rule_add, starts, out_time, out_rule,
                 raise ValueError("place_node_slice: pass the Engine of the tensors' device")
             from .engine import default_engine
             engine = default_engine()
+        elif engine.device != (time.device.index or 0):
+            raise ValueError(f"place_node_slice: engine on device {engine.device}, tensors on {time.device}")
         torch.cuda.synchronize(time.device)  # the library runs on its own stream
         engine.node_csr_place(N, node_off.data_ptr(), time.data_ptr(), rule.data_ptr(), int(rule_add),
                               starts.contiguous().data_ptr(), out_time.data_ptr(), out_rule.data_ptr())
@@ -271,6 +273,8 @@ def merge_rank_runs(run_bounds, out_time, out_rule, engine=None, budget_bytes=DE
                 raise ValueError("merge_rank_runs: pass the Engine of the tensors' device")
             from .engine import default_engine
             engine = default_engine()
+        elif engine.device != (out_time.device.index or 0):
+            raise ValueError(f"merge_rank_runs: engine on device {engine.device}, tensors on {out_time.device}")
         torch.cuda.synchronize(out_time.device)  # the library runs on its own stream
         engine.node_csr_merge_ranks(N, w1 - 1, rb, out_time.data_ptr(), out_rule.data_ptr(), budget_bytes)
         return
@@ -322,6 +326,14 @@ def gather_node_csr(local_node_off, local_time, local_rule, rule_base, dist, dst
     bases = torch.zeros(world, dtype=torch.int64, device=dev)
     dist.all_gather_into_tensor(bases, base_t)
     bases = bases.cpu().numpy()
+    if order == "time":
+        # the merge breaks time ties by rank: (time, global rule) order only
+        # when the job-ID ranges of the ranks holding events ascend with the
+        # rank (every rank sees the same bases and totals, so all raise)
+        held = bases[allc_h.sum(axis=1) > 0]
+        if len(held) > 1 and not (np.diff(held) > 0).all():
+            raise ValueError("gather_node_csr: rule_base does not ascend with the rank "
+                             "(time-ordered slices merge by rank)")
     offs = np.zeros((world, N + 1), dtype=np.int64)
     offs[:, 1:] = np.cumsum(allc_h, axis=1)
     plan = node_gather_plan(allc_h, dst, budget_bytes)

@@ -13,7 +13,9 @@
 // cgo rules kept: Go memory passed to C never holds Go pointers (structs that
 // point at buffers, and those buffers, are C.malloc'ed), and every wrapper that
 // passes a handle keeps its owner alive across the call (runtime.KeepAlive;
-// Specs and Dispatcher hold their Engine).  Needs Go >= 1.17 (unsafe.Slice).
+// Specs and Dispatcher hold their Engine).  C memory is viewed as Go slices
+// through array-pointer conversions (int64sAt / bytesAt), not unsafe.Slice, so
+// the package builds with the Go releases the reference's CI pins (1.7 / 1.8).
 //
 // Go is not installed in the image this package was written in, so it is not
 // compiled there; tests/native/abi_c.c runs the same call sequence against the
@@ -41,6 +43,11 @@ import (
 )
 
 const zeroUnix = -62135596800 // time.Time{}.Unix()
+
+// int64sAt / bytesAt view n elements of C memory at p as a Go slice (the
+// array-pointer form works on every Go release; unsafe.Slice needs 1.17)
+func int64sAt(p unsafe.Pointer, n int) []int64 { return (*[1 << 28]int64)(p)[:n:n] }
+func bytesAt(p unsafe.Pointer, n int) []byte   { return (*[1 << 30]byte)(p)[:n:n] }
 
 // Exclude modes of the rule -> node resolution.
 const (
@@ -212,7 +219,7 @@ func (e *Engine) Expand(sp *Specs, z *Zone, t0, t1 time.Time) (offsets, times []
 		return nil, nil, lastErr(rc)
 	}
 	offsets = make([]int64, sp.n+1)
-	copy(offsets, unsafe.Slice((*int64)(unsafe.Pointer(coff)), sp.n+1))
+	copy(offsets, int64sAt(unsafe.Pointer(coff), int(sp.n+1)))
 	times = make([]int64, int64(csr.n_events))
 	if len(times) > 0 {
 		if rc := C.cg_result_copy_times(e.ctx, 0, csr.n_events, (*C.int64_t)(unsafe.Pointer(&times[0]))); rc != 0 {
@@ -381,7 +388,7 @@ func (e *Engine) ExpandPerNode(sp *Specs, z *Zone, t0, t1 time.Time, j *Jobset, 
 		return nil, lastErr(rc)
 	}
 	nodeOff := make([]int64, nn+1)
-	copy(nodeOff, unsafe.Slice((*int64)(unsafe.Pointer(coff)), nn+1))
+	copy(nodeOff, int64sAt(unsafe.Pointer(coff), int(nn+1)))
 	tm, rl := make([]int64, int64(out.n_events)), make([]int32, int64(out.n_events))
 	if len(tm) > 0 {
 		if rc := C.cg_node_result_copy(e.ctx, nil, (*C.int64_t)(unsafe.Pointer(&tm[0])),
@@ -531,7 +538,7 @@ func CommUniqueID() ([C.CG_COMM_ID_BYTES]byte, error) {
 	if rc := C.cg_comm_unique_id(cid); rc != 0 {
 		return id, lastErr(rc)
 	}
-	copy(id[:], unsafe.Slice((*byte)(unsafe.Pointer(cid)), C.CG_COMM_ID_BYTES))
+	copy(id[:], bytesAt(unsafe.Pointer(cid), int(C.CG_COMM_ID_BYTES)))
 	return id, nil
 }
 
@@ -540,7 +547,7 @@ func CommUniqueID() ([C.CG_COMM_ID_BYTES]byte, error) {
 func NewComm(e *Engine, world, rank int, id [C.CG_COMM_ID_BYTES]byte) (*Comm, error) {
 	cid := (*C.uint8_t)(C.malloc(C.CG_COMM_ID_BYTES))
 	defer C.free(unsafe.Pointer(cid))
-	copy(unsafe.Slice((*byte)(unsafe.Pointer(cid)), C.CG_COMM_ID_BYTES), id[:])
+	copy(bytesAt(unsafe.Pointer(cid), int(C.CG_COMM_ID_BYTES)), id[:])
 	var c *C.cg_comm
 	if rc := C.cg_comm_init(e.ctx, C.int(world), C.int(rank), cid, &c); rc != 0 {
 		return nil, lastErr(rc)
@@ -614,7 +621,7 @@ func (e *Engine) MergeRanks(nNodes, world int, runBounds []int64, dTime, dRule u
 	}
 	rb := (*C.int64_t)(C.malloc(C.size_t(8 * nNodes * (world + 1))))
 	defer C.free(unsafe.Pointer(rb))
-	copy(unsafe.Slice((*int64)(unsafe.Pointer(rb)), nNodes*(world+1)), runBounds)
+	copy(int64sAt(unsafe.Pointer(rb), int(nNodes*(world+1))), runBounds)
 	rc := C.cg_node_csr_merge_ranks(e.ctx, C.int32_t(nNodes), C.int32_t(world), rb,
 		(*C.int64_t)(unsafe.Pointer(dTime)), (*C.int32_t)(unsafe.Pointer(dRule)), C.int64_t(budget))
 	runtime.KeepAlive(e)
@@ -638,7 +645,7 @@ func GatherPlan(counts []int64, world, nNodes, root int, budget int64) ([][4]int
 	}
 	cc := (*C.int64_t)(C.malloc(C.size_t(8 * words)))
 	defer C.free(unsafe.Pointer(cc))
-	copy(unsafe.Slice((*int64)(unsafe.Pointer(cc)), world*nNodes), counts)
+	copy(int64sAt(unsafe.Pointer(cc), int(world*nNodes)), counts)
 	// sizing call: *n_chunks is set, CG_ECAPACITY when there are any chunks
 	if rc := C.cg_comm_gather_plan(cc, C.int32_t(world), C.int32_t(nNodes), C.int32_t(root), C.int64_t(budget), nil, 0, &n); rc != 0 && rc != C.CG_ECAPACITY {
 		return nil, lastErr(rc)
@@ -652,7 +659,7 @@ func GatherPlan(counts []int64, world, nNodes, root int, budget int64) ([][4]int
 	if rc := C.cg_comm_gather_plan(cc, C.int32_t(world), C.int32_t(nNodes), C.int32_t(root), C.int64_t(budget), buf, n, &n); rc != 0 {
 		return nil, lastErr(rc)
 	}
-	flat := unsafe.Slice((*int64)(unsafe.Pointer(buf)), 4*int(n))
+	flat := int64sAt(unsafe.Pointer(buf), 4*int(n))
 	for i := range out {
 		copy(out[i][:], flat[4*i:4*i+4])
 	}

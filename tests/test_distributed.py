@@ -275,6 +275,39 @@ def test_gather_node_csr_time_ordered_gloo(tmp_path, world, budget):
     assert np.array_equal(got["rule"], exp_r)
 
 
+def _bases_worker(rank, world, port, outdir):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off = torch.tensor([0, 2, 3], dtype=torch.int64)
+    t = torch.tensor([T0 + 1, T0 + 2, T0 + 1], dtype=torch.int64)
+    r = torch.tensor([0, 1, 0], dtype=torch.int32)
+    for order in ("time", "rule"):
+        # rank 1's range before rank 0's: ties merged by rank would be out of
+        # (time, global rule) order, so the time-ordered gather refuses on every
+        # rank; the rule-ordered gather needs no rank order and runs
+        try:
+            shard.gather_node_csr(off, t, r, 1000 * (world - rank), dist, order=order)
+            res = "ok"
+        except ValueError as e:
+            res = str(e)
+        with open(os.path.join(outdir, f"{order}{rank}.txt"), "w") as f:
+            f.write(res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_time_ordered_gather_refuses_descending_rule_bases(tmp_path):
+    import torch.multiprocessing as mp
+    world = 2
+    mp.spawn(_bases_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for g in range(world):
+        assert "does not ascend" in (tmp_path / f"time{g}.txt").read_text()
+        assert (tmp_path / f"rule{g}.txt").read_text() == "ok"
+
+
 def test_gather_node_csr_requires_order():
     """The Python gather cannot tell the lists' order: the caller states it."""
     with pytest.raises(TypeError):

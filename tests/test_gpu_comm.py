@@ -158,3 +158,97 @@ def test_merge_ranks_random(world, budget):
         eng.close()
     assert np.array_equal(dt.cpu().numpy(), exp_t)
     assert np.array_equal(dr.cpu().numpy(), exp_r)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_comm_world2_one_gpu(tmp_path, world):
+    """The library's multi-rank exchange for real at world 2 and 3 on one GPU
+    (tools/comm_world2.py: each rank claims its own NCCL_HOSTID, so RCCL
+    accepts two ranks on one device and moves the data over its socket
+    transport): all-gather, node offsets, and cg_comm_gather_node_csr of
+    job-ID-range shards in time order (ranks' runs merged on the root by
+    k_merge_ranks) and rule order, roots 0 and world - 1, budgets of 24 B per
+    rank (every chunk split), a third of the largest node and 1 GiB -- equal
+    to the unsharded per-node lists; and time-ordered results whose rule
+    bases descend with the rank refused with CG_EINVAL on every rank."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "tools", "comm_world2.py"), str(tmp_path), str(world)],
+                       capture_output=True, text=True, timeout=400)
+    assert p.returncode == 0, (p.stdout[-3000:], p.stderr[-5000:])
+    recs = {g: [json.loads(x) for x in open(tmp_path / f"rank{g}.jsonl")] for g in range(world)}
+    for g in range(world):
+        cases = {}
+        for x in recs[g]:
+            cases.setdefault(x["case"], []).append(x)
+        assert cases["done"]
+        assert cases["allgather"][0]["got"] == [[q * 10 + 1, -q] for q in range(world)]
+        assert cases["allgather_after"][0]["got"] == [[q] for q in range(world)]
+        assert cases["descending_bases"][0]["code"] == cases["descending_bases"][0]["expect"]
+        for x in cases.get("node_offsets", []):
+            assert x["ok"], x
+        for x in cases.get("gather", []):
+            assert x["ok"], x
+    n_gathers = sum(1 for g in range(world) for x in recs[g] if x["case"] == "gather")
+    assert n_gathers == 2 * 3 * len({0, world - 1})
+
+
+def test_merge_scratch_capped_at_the_merged_events():
+    """A small merge with the default 2-GiB budget allocates scratch for its
+    own events, not the budget's 179 M (2.1 GB of HBM held until
+    close)."""
+    import torch
+    from cronsun_amd.engine import Engine
+    dev = torch.device("cuda", 0)
+    N, world = 50, 4
+    rng = np.random.default_rng(3)
+    cnt = rng.integers(0, 30, (N, world))
+    rb = np.zeros((N, world + 1), dtype=np.int64)
+    rb[:, 1:] = np.cumsum(cnt, axis=1)
+    rb += np.concatenate([[0], np.cumsum(rb[:, -1])[:-1]])[:, None]
+    E = int(rb[-1, -1])
+    t = np.empty(E, dtype=np.int64)
+    r = np.empty(E, dtype=np.int32)
+    for n in range(N):
+        for g in range(world):
+            a, b = rb[n, g], rb[n, g + 1]
+            t[a:b] = np.sort(rng.integers(0, 20, b - a)) + 1767571200
+            r[a:b] = np.arange(b - a) + 1000 * g
+    dt, dr = torch.from_numpy(t).to(dev), torch.from_numpy(r).to(dev)
+    torch.cuda.synchronize(dev)
+    eng = Engine(0)
+    try:
+        free0 = torch.cuda.mem_get_info(dev)[0]
+        eng.node_csr_merge_ranks(N, world, rb, dt.data_ptr(), dr.data_ptr())  # default 2-GiB budget
+        used = free0 - torch.cuda.mem_get_info(dev)[0]
+    finally:
+        eng.close()
+    assert used < (64 << 20), used
+    exp_t = t.copy()
+    for n in range(N):
+        a, b = rb[n, 0], rb[n, -1]
+        exp_t[a:b] = np.sort(t[a:b], kind="stable")
+    assert np.array_equal(dt.cpu().numpy(), exp_t)
+
+
+def test_shard_helpers_refuse_an_engine_of_another_device():
+    """merge_rank_runs / place_node_slice with an engine whose device is not
+    the tensors' raise ValueError before the library sees a foreign pointer."""
+    import torch
+    from cronsun_amd import shard
+
+    class OtherDevice:
+        device = 1
+    dev = torch.device("cuda", 0)
+    t = torch.zeros(8, dtype=torch.int64, device=dev)
+    r = torch.zeros(8, dtype=torch.int32, device=dev)
+    rb = np.array([[0, 4, 8]], dtype=np.int64)
+    with pytest.raises(ValueError, match="engine on device 1"):
+        shard.merge_rank_runs(rb, t, r, engine=OtherDevice())
+    off = torch.tensor([0, 8], dtype=torch.int64, device=dev)
+    with pytest.raises(ValueError, match="engine on device 1"):
+        shard.place_node_slice(off, t, r, 0, torch.zeros(1, dtype=torch.int64, device=dev), t, r,
+                               engine=OtherDevice())
