@@ -576,6 +576,26 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 #ifndef CG_WRITE_WPE
 #define CG_WRITE_WPE 6
 #endif
+// Ticket groups across the XCDs (1) or one XCD per group (0: blocks go
+// round-robin over the XCDs, so group blockIdx % 32 lived on XCD
+// blockIdx % 8).  With one XCD per group the groups ran dry up to 120 us
+// apart on config 2 (the XCDs' rates differ), and a dry group's waves idled:
+// 5-9 % of the wave-time (per-wave stamps, profiles/r06_writer_tail_*.json).
+// Across the XCDs: dry within 40 us, idle 3.3 %, k_write_cf 0.980 -> 0.946 ms
+// (same box, profiles/r06_ab_writer_groups.txt; moving on to other groups
+// when dry, CG_WRITE_STEAL_SMALL, gains nothing on top).
+#ifndef CG_WRITE_GRP_XCD
+#define CG_WRITE_GRP_XCD 1
+#endif
+#ifndef CG_WRITE_STEAL_SMALL
+#define CG_WRITE_STEAL_SMALL 0
+#endif
+#ifdef CG_DIAG
+// diagnostic build only (CG_WRITE_STAMPS=1): per wave of the last k_write_cf
+// launch {start, end, slices written, the wall clock when its ticket group
+// ran dry}, wall_clock64() units (100 MHz) -- the launch's ramp and tail
+__device__ int64_t* cg_write_stamps = nullptr;
+#endif
 // Persistent closed-form writer.  Waves work independently on 2^super_shift(cap)-event
 // output slices, handed out by ticket.  A wave keeps a window of 64
 // consecutive runs (one coalesced round of loads, staged in its LDS slice;
@@ -601,6 +621,11 @@ __global__ __launch_bounds__(kWriteWaves * 64, CG_WRITE_WPE) void k_write_cf(
 
   const int G = p.G;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#ifdef CG_DIAG
+  int64_t* const stamp = cg_write_stamps ? cg_write_stamps + 4 * (int64_t(blockIdx.x) * kWriteWaves + wave) : nullptr;
+  const int64_t st_start = stamp ? int64_t(wall_clock64()) : 0;
+  int64_t st_slices = 0;
+#endif
   WinRun* win = win_all[wave];
   const int64_t E = run_off[nruns];
   if (E > cap) return;  // output buffer too small: host grows it and relaunches
@@ -647,13 +672,19 @@ __global__ __launch_bounds__(kWriteWaves * 64, CG_WRITE_WPE) void k_write_cf(
   // waits on its own waves alone).  Tickets are taken one slice ahead so the atomic's latency
   // hides under the current slice.
   const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
+#if CG_WRITE_GRP_XCD
+  // every group spans the 8 XCDs (blocks b..b+7 of one dispatch round share a
+  // group): a group's slices then advance at the chip's average rate
+  const int grp = int((blockIdx.x >> 3) % unsigned(ng));
+#else
   const int grp = int(blockIdx.x % unsigned(ng));
+#endif
   unsigned int* tickets = reinterpret_cast<unsigned int*>(chunk_run + (cap >> sh) + 2);
   int cur = grp, hops = 0;  // the group whose slices this wave takes, groups left behind
   // (same-box A/B, profiles/r02_ab_steal.json: config 4 with 16384-event
   // slices 23.7 vs 24.5 ms; config 2 with 2048-event slices 1.03 vs 0.99 ms:
   // moving on only pays with the large slices)
-  const bool steal = sh == CG_SUPER_SHIFT_LARGE;
+  const bool steal = CG_WRITE_STEAL_SMALL || sh == CG_SUPER_SHIFT_LARGE;
   // One ticket per atomic (same-box A/B, profiles/r02_ab_writer_lw.json:
   // taking 2/4/8 per atomic loses more to the coarser tail than it saves).
   auto take = [&]() -> int64_t {
@@ -667,6 +698,10 @@ __global__ __launch_bounds__(kWriteWaves * 64, CG_WRITE_WPE) void k_write_cf(
   };
   for (int64_t c = take(); c < nsup;) {
     const int64_t c_next = take();
+#ifdef CG_DIAG
+    st_slices++;
+    if (stamp && c_next >= nsup && lane == 0) stamp[3] = int64_t(wall_clock64());
+#endif
     // slice start: a multiple of 64, so every store below is a whole 512 B block
     int64_t pos = um ? umap[2 * c] : c << sh;
     const int64_t S1 = um ? umap[2 * c + 2] : (E - pos < sup ? E : pos + sup);
@@ -749,6 +784,13 @@ __global__ __launch_bounds__(kWriteWaves * 64, CG_WRITE_WPE) void k_write_cf(
     if (pd.blk >= 0 && pd.blk + lane < S1) put(times + pd.blk + lane, pd.val);
     c = c_next;
   }
+#ifdef CG_DIAG
+  if (stamp && lane == 0) {
+    stamp[0] = st_start;
+    stamp[1] = int64_t(wall_clock64());
+    stamp[2] = st_slices;
+  }
+#endif
 }
 
 
@@ -1049,12 +1091,32 @@ void launch_chunk_map(const int64_t* run_off, int64_t nruns, int64_t cap, int64_
   launch_chunk_map_u(run_off, nruns, cap, chunk_run, st);
 }
 
+#ifdef CG_DIAG
+int64_t* g_stamp_buf = nullptr;
+int g_stamp_waves = 0;
+#endif
+
 void launch_write_cf(const DSpec* specs, const PlanArgs& p, const int64_t* run_anchor,
                      const int32_t* run_count, const uint32_t* run_dmask, const int64_t* run_off,
                      int64_t nruns, int64_t* chunk_run, int64_t cap, int64_t* times,
                      int n_blocks, hipStream_t st) {
   const size_t lds = size_t(p.G) * sizeof(Segment);
 #ifdef CG_DIAG
+  static const bool stamps = getenv("CG_WRITE_STAMPS") != nullptr;
+  if (stamps) {  // the per-wave stamps of this launch (read by cg_diag_write_stamps)
+    static int64_t* buf = nullptr;
+    static int cap_waves = 0;
+    const int waves = n_blocks * kWriteWaves;
+    if (waves > cap_waves) {
+      if (buf) (void)hipFree(buf);
+      (void)hipMalloc(&buf, size_t(waves) * 32);
+      cap_waves = waves;
+      (void)hipMemcpyToSymbol(HIP_SYMBOL(cg_write_stamps), &buf, sizeof buf);
+    }
+    (void)hipMemsetAsync(buf, 0, size_t(waves) * 32, st);
+    g_stamp_buf = buf;
+    g_stamp_waves = waves;
+  }
   // the diagnostic library only (`make diag`): store-ceiling probes and the
   // experimental loader/writer split replace the writer when asked for
   // (CG_WRITE_PROBE / CG_WRITE_VARIANT, cg_diag.hip)
@@ -1077,3 +1139,16 @@ void launch_write_walk(const DSpec* specs, int64_t R, const PlanArgs& p, const i
 
 
 }  // namespace cg
+
+#ifdef CG_DIAG
+// the diagnostic library's per-wave stamps of the last k_write_cf launch
+// (CG_WRITE_STAMPS=1): 4 int64 per wave {start, end, slices, dry}; returns the
+// number of waves (0 when stamps are off), after a device sync
+extern "C" int cg_diag_write_stamps(int64_t* out, int64_t max_waves) {
+  if (!cg::g_stamp_buf) return 0;
+  (void)hipDeviceSynchronize();
+  const int64_t n = std::min<int64_t>(cg::g_stamp_waves, max_waves);
+  (void)hipMemcpy(out, cg::g_stamp_buf, size_t(n) * 32, hipMemcpyDeviceToHost);
+  return int(n);
+}
+#endif

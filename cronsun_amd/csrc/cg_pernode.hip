@@ -605,6 +605,12 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 #ifndef CG_NODE_MAJOR_ORDERED
 #define CG_NODE_MAJOR_ORDERED 0
 #endif
+// ticket groups across the 8 XCDs, as k_write_cf's (same box,
+// profiles/r06_ab_node_writer_groups.txt: config 3 174.9 -> 170.7 ms per
+// step, node writer 152.1 -> 146.7; pernode equal)
+#ifndef CG_NODE_GRP_XCD
+#define CG_NODE_GRP_XCD 1
+#endif
 constexpr int kNodeMajorDefault = CG_NODE_MAJOR;
 constexpr int kNodeMajorOrdered = CG_NODE_MAJOR_ORDERED;  // the time-order writer (packed words / 16-bit offsets)
 
@@ -631,7 +637,11 @@ __global__ __launch_bounds__(256) void k_node_write(
   if (seg_pos[NK] > cap) return;  // output too small: the host grows it and relaunches
   const uint64_t le = (2ull << lane) - 1ull;  // lanes <= this one
   const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
+#if CG_NODE_GRP_XCD
+  const int grp = int((blockIdx.x >> 3) % unsigned(ng));  // every group across the 8 XCDs (cf. k_write_cf)
+#else
   const int grp = int(blockIdx.x % unsigned(ng));
+#endif
   auto take = [&]() -> int64_t {
     unsigned int t = 0;
     if (lane == 0) t = atomicAdd(tickets + grp * kTicketStride, 1u);
