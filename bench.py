@@ -314,7 +314,14 @@ def main():
             shard_info = {"lo": lo, "hi": hi}
         shard_info["global_rules"] = total
         if pn and not args.window:
-            W = 3600 if R <= 2_500_000 else 1800  # a window's node lists within HBM
+            # 1-h windows: a 10M-rule rank's window holds ~10 G node events (120
+            # GB of lists), within HBM beside the three window sets' records;
+            # the per-window side chain (rule infos, segment records over all
+            # 920 M pairs) is then paid 168 times per step instead of 336.
+            # Time order past 2^20 rules per rank keeps 30-min windows: their
+            # 32-s slabs fit k_ot_mid's chunks (64-s slabs of a 1-h window
+            # would go to k_ot_big's two reads)
+            W = 1800 if (args.time_order and R > (1 << 20)) else 3600
 
         def spec_of(i):  # local rule i of this rank's range
             return base_specs[(shard_lo + i) % base_n]
