@@ -318,10 +318,11 @@ def main():
             # GB of lists), within HBM beside the three window sets' records;
             # the per-window side chain (rule infos, segment records over all
             # 920 M pairs) is then paid 168 times per step instead of 336.
-            # Time order past 2^20 rules per rank keeps 30-min windows: their
-            # 32-s slabs fit k_ot_mid's chunks (64-s slabs of a 1-h window
-            # would go to k_ot_big's two reads)
-            W = 1800 if (args.time_order and R > (1 << 20)) else 3600
+            # Time order past 2^20 rules per rank takes 2048-s windows: 64
+            # slabs of 32 s (the tile sort's 64 slab digits), which fit
+            # k_ot_mid's chunks (64-s slabs of a 1-h window would go to
+            # k_ot_big's two reads), in 296 windows per 7 days
+            W = 2048 if (args.time_order and R > (1 << 20)) else 3600
 
         def spec_of(i):  # local rule i of this rank's range
             return base_specs[(shard_lo + i) % base_n]

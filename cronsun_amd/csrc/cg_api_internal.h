@@ -232,6 +232,8 @@ struct cg_ctx {
   // histograms/offsets, and the second buffers of the ping-pong
   DBuf<int32_t> ts_cnt, ts_tile_node, ts_hist, node_rule2;
   DBuf<int64_t> ts_base, ts_off, node_time2, ts_node_off;
+  DBuf<int64_t> ts_start;  // per tile its first list position; [T] = the lists' end
+  DBuf<int32_t> ts_hi;     // per tile the high rule bits (rule >> 20) all its events share
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
@@ -285,6 +287,7 @@ struct cg_ctx {
     seg_nrec.release(); recs.release();
     rule_info.release();
     ts_cnt.release(); ts_tile_node.release(); ts_hist.release(); node_rule2.release();
+    ts_start.release(); ts_hi.release();
     ts_base.release(); ts_off.release(); node_time2.release(); ts_node_off.release();
     mr_rb.release(); mr_tp.release(); mr_t.release(); mr_r.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);
@@ -340,14 +343,24 @@ bool pn_async_pending(const cg_ctx* c);  // an asynchronous expansion not yet wa
 // in_mode: what the writer left in c->node_time / c->node_rule -- kInTimes
 // int64 times + rules; kIn16 16-bit offsets t - t0 - 1 + rules
 // (k_node_write<.., kOut16>); kInPacked one word per event, offset << 20 |
-// rule, in c->node_rule (k_node_write<.., kOutPacked>; rules < 2^20)
+// (rule & 0xFFFFF), in c->node_rule (k_node_write<.., kOutPacked>; rules <
+// 2^24: past 2^20 the tiles are cut where rule >> 20 changes and carry it)
 constexpr int kInTimes = 0, kIn16 = 1, kInPacked = 2;
-// the time-order writer may emit kInPacked for R rules (indices < 2^20)
+// the time-order writer may emit kInPacked for R rules (indices < 2^24)
 bool pn_pack_ok(int64_t R);
+// where every node's list crosses a multiple of 2^20 in rule index: the
+// (node, band) segment offsets seg_pos [N*K+1] of bands of B rules (B a power
+// of two <= 2^20, so 2^20 / B bands per block of 2^20 rules); null seg_pos:
+// no cuts (rule indices < 2^20)
+struct TileCut {
+  const int64_t* seg_pos = nullptr;
+  int32_t K = 1, B = 1;
+  int64_t R = 0;
+};
 // err: a device word the kernels set when a sorted chunk is out of (time,
 // rule) order (the sorts' ranks rest on lane-ordered LDS atomics; checked)
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
-                        hipStream_t st, int in_mode, int64_t* err);
+                        hipStream_t st, int in_mode, int64_t* err, const TileCut& cut = TileCut());
 constexpr const char* kOrderCheckMsg =
     "time-order pass: a sorted chunk came out of (time, rule) order (its LDS-atomic ranks were not in lane order)";
 // the mapped pinned per-node result words: [0] node events, [1] size error, [2] order check

@@ -675,7 +675,8 @@ __global__ __launch_bounds__(kWriteWaves * 64, CG_WRITE_WPE) void k_write_cf(
 #if CG_WRITE_GRP_XCD
   // every group spans the 8 XCDs (blocks b..b+7 of one dispatch round share a
   // group): a group's slices then advance at the chip's average rate
-  const int grp = int((blockIdx.x >> 3) % unsigned(ng));
+  // (only when the grid gives every group a block that way)
+  const int grp = int(gridDim.x >= 8u * unsigned(ng) ? (blockIdx.x >> 3) % unsigned(ng) : blockIdx.x % unsigned(ng));
 #else
   const int grp = int(blockIdx.x % unsigned(ng));
 #endif

@@ -230,6 +230,62 @@ constexpr int kOtSlabBits = 6;               // slab = offset >> kOtSlabBits (64
 constexpr int kOtSlabs = 4096 >> kOtSlabBits;
 constexpr int kOtPre = kOtSlabs + 1;          // pre row per tile
 constexpr int kOtMaxTiles = 256;              // portion list capacity
+// rule indices up to 2^24 in the packed words: the words hold rule & 0xFFFFF
+// and every tile's rules share rule >> 20 (ts_hi); the merges rebuild the
+// rule from its tile
+constexpr int kOtHiBits = 4;
+constexpr uint32_t kOtLowMask = (1u << kOtRuleBits) - 1u;
+
+// The tiles of the tile sort: every node's list cut into kOtTile-event tiles,
+// restarting at each multiple of 2^20 in rule index (the lists are
+// rule-major, so those are H - 1 cut positions per node, found from the
+// (node, band) segment offsets: bph bands of 2^20 / bph rules per block).
+struct OtCut {
+  const int64_t* seg_pos;  // null: no cuts (H = 1)
+  int32_t K, bph, H;
+};
+// the first position of node n's events with rule >= h << 20 (0 <= h <= H)
+__device__ __forceinline__ int64_t ot_cut_pos(const OtCut& c, const int64_t* node_off, int32_t n, int h) {
+  if (c.H <= 1) return h == 0 ? node_off[n] : node_off[n + 1];
+  const int64_t k = int64_t(h) * c.bph;
+  return c.seg_pos[int64_t(n) * c.K + (k < c.K ? k : c.K)];
+}
+// tiles per node; none at all when the lists exceed the buffers' capacity
+__global__ void k_ot_tile_count(const int64_t* __restrict__ node_off, int32_t N, int64_t cap, OtCut cut,
+                                int32_t* __restrict__ cnt) {
+  const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (n >= N) return;
+  int32_t t = 0;
+  if (node_off[N] <= cap) {
+    int64_t a = ot_cut_pos(cut, node_off, int32_t(n), 0);
+    for (int h = 0; h < cut.H; h++) {
+      const int64_t b = ot_cut_pos(cut, node_off, int32_t(n), h + 1);
+      t += int32_t((b - a + kOtTile - 1) / kOtTile);
+      a = b;
+    }
+  }
+  cnt[n] = t;
+}
+// per tile: its node, first position and rule >> 20; ts_start[T] = the end
+__global__ void k_ot_tiles(const int64_t* __restrict__ tile_base, const int64_t* __restrict__ node_off, int32_t N,
+                           OtCut cut, int32_t* __restrict__ tile_node, int64_t* __restrict__ ts_start,
+                           int32_t* __restrict__ ts_hi) {
+  const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
+  if (n >= N) return;
+  int64_t t = tile_base[n];
+  if (n == N - 1) ts_start[tile_base[N]] = node_off[N];
+  if (tile_base[n + 1] == t) return;
+  int64_t a = ot_cut_pos(cut, node_off, int32_t(n), 0);
+  for (int h = 0; h < cut.H; h++) {
+    const int64_t b = ot_cut_pos(cut, node_off, int32_t(n), h + 1);
+    for (int64_t p = a; p < b; p += kOtTile, t++) {
+      tile_node[t] = int32_t(n);
+      ts_start[t] = p;
+      ts_hi[t] = h;
+    }
+    a = b;
+  }
+}
 
 template <int NW>
 __device__ __forceinline__ void ot_sync() {
@@ -472,7 +528,8 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
                                                   const int64_t* __restrict__ node_off, int64_t t0,
                                                   uint16_t* __restrict__ toff_out, int32_t* __restrict__ rule_out,
                                                   int32_t* __restrict__ pre, const int64_t* __restrict__ n_tiles,
-                                                  int64_t* __restrict__ err, int sb) {
+                                                  int64_t* __restrict__ err, int sb,
+                                                  const int64_t* __restrict__ ts_start) {
   constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
   constexpr uint32_t kLow = (1u << IB) - 1u;
   __shared__ OtRank<4, 64> s;
@@ -481,7 +538,7 @@ __global__ __launch_bounds__(256, PACK ? CG_OT_TILE_WPE : 4) void k_ot_tile(cons
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t t = blockIdx.x;
   if (t >= *n_tiles) return;  // the grid may be an upper bound (pipelined windows)
-  const TileRange r = tile_range(t, tile_node, tile_base, node_off, kOtTile);
+  const TileRange r{ts_start[t], ts_start[t + 1]};  // never more than kOtTile events
   const int n = int(r.hi - r.lo);
   const int ebase = w * (64 * kOtItems);
   const uint32_t* __restrict__ tlo = reinterpret_cast<const uint32_t*>(time);  // low words: offsets < 4096
@@ -659,15 +716,22 @@ __device__ __forceinline__ void ot_owners(const int32_t* ps, int Q, int32_t c0, 
 // instead of two, and no 64-bit address arithmetic per item
 // PIN: the source is one array of packed words offset << 20 | rule (rin; tin
 // unused), 4 B per event instead of 2 + 4
-template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems, bool BUF = false, bool PIN = false>
+// HX (with PIN; rule indices past 2^20): the words hold rule & 0xFFFFF and
+// portion q's tile adds ph[q] << 20.  PACK keys become (offset - hx_lo) << 24
+// | rule (a run of at most 256 s: the key order is still the (time, rule)
+// order); otherwise rl[] gets the whole rule
+template <bool RULES, int SEARCH = 0, bool PACK = false, int IT = kOtItems, bool BUF = false, bool PIN = false,
+          bool HX = false>
 __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                           const int32_t* ps, const int32_t* psrc, const int32_t* own,
                                           int32_t c0, int n_el, uint32_t (&key)[IT], int32_t* rl, int Q = 0,
-                                          uint32_t n_src = 0) {
+                                          uint32_t n_src = 0, const int32_t* ph = nullptr, uint32_t hx_lo = 0) {
+  static_assert(!HX || PIN, "high rule bits come with packed words");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ebase = w * (64 * IT);
   uint32_t tv[IT];
   int32_t rv[IT];
+  uint32_t hq[HX ? IT : 1];  // HX: the element's tile's rule >> 20, shifted
   __amdgpu_buffer_rsrc_t ra, rb;
   if constexpr (BUF) {
     constexpr int kRsrcWord3 = 0x00020000;  // gfx9 raw buffer: 32-bit data format, no swizzle
@@ -699,6 +763,7 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
       q = SEARCH ? ot_find(ps, Q, c0 + ec) : own[ot_pad(ec)];
     }
     const uint32_t src = SEARCH == 2 ? uint32_t(qs + (c0 + ec - qa)) : uint32_t(psrc[q] + (c0 + ec - ps[q]));
+    if constexpr (HX) hq[j] = uint32_t(ph[q]) << kOtRuleBits;
     if constexpr (PIN) {  // one word: split below
       rv[j] = BUF ? __builtin_amdgcn_raw_buffer_load_b32(rb, int(src * 4u), 0, 0) : rin[src];
     } else if constexpr (BUF) {
@@ -719,7 +784,14 @@ __device__ __forceinline__ void ot_gather(const uint16_t* __restrict__ tin, cons
 #pragma unroll
   for (int j = 0; j < IT; j++) {
     const int e = ebase + j * 64 + lane;
-    if (PACK) {
+    if constexpr (HX) {
+      if (PACK) {
+        key[j] = e < n_el ? ((tv[j] - hx_lo) << (kOtRuleBits + kOtHiBits)) | hq[j] | uint32_t(rv[j]) : 0u;
+      } else {
+        key[j] = e < n_el ? (tv[j] << kOtIdxBits) | uint32_t(e) : 0u;
+        if (RULES && e < n_el) rl[e] = int32_t(hq[j] | uint32_t(rv[j]));
+      }
+    } else if (PACK) {
       key[j] = e < n_el ? (tv[j] << kOtRuleBits) | uint32_t(rv[j]) : 0u;
     } else {
       key[j] = e < n_el ? (tv[j] << kOtIdxBits) | uint32_t(e) : 0u;
@@ -783,28 +855,31 @@ __global__ __launch_bounds__(64) void k_ot_slabs(const int64_t* __restrict__ til
 // the node's tile-sorted offsets and rules): the M tiles' portions
 // (portion(q, &src) -> count, thread q's tile; src node-relative), gathered,
 // sorted in LDS by rel = offset - lo (`passes` 8-bit passes) and stored at
-// tout_o / rout_o in (time, rule) order.  Ends synchronised.
-template <int NW, bool PACK, int IT, bool PIN, class Portion>
+// tout_o / rout_o in (time, rule) order.  n_src: the node's events (M <=
+// kOtMaxTiles tiles).  HX: rules past 2^20 (portion q's tile adds ph[q] <<
+// 20; keys rel << 24 | rule, one pass: rel < 256).  Ends synchronised.
+template <int NW, bool PACK, int IT, bool PIN, bool HX, class Portion>
 __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_n, const int32_t* __restrict__ rin_n,
                                                int M, int n_el, uint32_t lo, int passes, Portion&& portion,
                                                int64_t t0, int64_t* __restrict__ tout_o,
                                                int32_t* __restrict__ rout_o, OtRank<NW, 256>& s, uint32_t* pk,
                                                int32_t* rl, int32_t* ps, int32_t* psrc, int32_t* wsum,
-                                               int64_t* __restrict__ err) {
+                                               int64_t* __restrict__ err, uint32_t n_src, const int32_t* ph) {
   int32_t* own = reinterpret_cast<int32_t*>(pk);
   uint32_t key[IT];
   ot_portions<NW>(M, portion, ps, psrc, wsum);
-  const uint32_t n_src = uint32_t(M) * kOtTile;  // the node's tiles (M <= kOtMaxTiles)
   // each element's portion by search + walk, raw buffer loads
-  ot_gather<true, 2, PACK, IT, true, PIN>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M, n_src);
-  constexpr int IB = PACK ? kOtRuleBits : kOtIdxBits;
-  ot_sort<NW, 256, false, IB, IT>(key, n_el, lo, 0, passes, pk, s);
+  ot_gather<true, 2, PACK, IT, true, PIN, HX>(tin_n, rin_n, ps, psrc, own, 0, n_el, key, rl, M, n_src, ph, lo);
+  constexpr int IB = HX ? kOtRuleBits + kOtHiBits : (PACK ? kOtRuleBits : kOtIdxBits);
+  ot_sort<NW, 256, false, IB, IT>(key, n_el, HX ? 0u : lo, 0, passes, pk, s);
+  const int64_t tb = t0 + 1 + (HX ? int64_t(lo) : 0);
+  constexpr uint32_t kRuleMask = HX ? (1u << (kOtRuleBits + kOtHiBits)) - 1u : kOtLowMask;
   bool bad = false;
   for (int p = threadIdx.x; p < n_el; p += 64 * NW) {
     const uint32_t v = pk[p];
-    __builtin_nontemporal_store(t0 + 1 + int64_t(v >> IB), tout_o + p);
+    __builtin_nontemporal_store(tb + int64_t(v >> IB), tout_o + p);
     if (PACK) {
-      __builtin_nontemporal_store(int32_t(v & ((1u << kOtRuleBits) - 1u)), rout_o + p);
+      __builtin_nontemporal_store(int32_t(v & kRuleMask), rout_o + p);
       const uint32_t u = ot_prev(pk, p, v);
       if (p > 0) bad |= u >= v;  // (time, rule) order of the chunk: the words ascend
     } else {
@@ -830,7 +905,9 @@ __device__ __forceinline__ void ot_merge_chunk(const uint16_t* __restrict__ tin_
 // 1.6 % faster on pernode and equal on config 3, profiles/r04_ab_dense_2048.txt).  A slab of more than a chunk is queued: to k_ot_mid when it
 // fits k_ot_mid's chunk (mid / mid_n), else to k_ot_big (big / big_n);
 // entries (node << 8 | slab).
-template <int NW, bool PACK, int IT = kOtItems, bool DYN = false, bool PIN = false>  // DYN: nodes by ticket (persistent grid)
+// HX: rule indices past 2^20 (tiles cut where rule >> 20 changes, ts_hi per
+// tile): runs of at most 256 s, so a key holds rel << 24 | rule.
+template <int NW, bool PACK, int IT = kOtItems, bool DYN = false, bool PIN = false, bool HX = false>  // DYN: nodes by ticket (persistent grid)
 __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERGE_WPE) : 4) void k_ot_merge(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                        const int64_t* __restrict__ tile_base,
                                                        const int64_t* __restrict__ node_off,
@@ -841,10 +918,13 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
                                                        int64_t* __restrict__ mid, unsigned* __restrict__ mid_n,
                                                        int64_t* __restrict__ mid2, unsigned* __restrict__ mid2_n,
                                                        int64_t e_lo, int64_t e_hi, unsigned* __restrict__ ticket,
-                                                       int64_t* __restrict__ err, int sb) {
+                                                       int64_t* __restrict__ err, int sb,
+                                                       const int64_t* __restrict__ ts_start,
+                                                       const int32_t* __restrict__ ts_hi) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
   constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems, kMid2Chunk = 64 * kOtMid2Waves * kOtItems;
   __shared__ OtRank<NW, 256> s;
+  __shared__ int32_t ph[HX ? kOtMaxTiles : 1];  // HX: rule >> 20 of tile q
   __shared__ uint32_t pk[kChunk + kChunk / 32];  // the owner list while gathering (padded), then the sorted words
   __shared__ int32_t rl[PACK ? 1 : kChunk];
   __shared__ int32_t ps[kOtMaxTiles + 1];
@@ -865,11 +945,12 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
   const int64_t e_n = node_off[n + 1] - lo_n;
   if (e_n < e_lo || e_n >= e_hi) continue;  // the other merge launch's node
   if (M == 1) {  // one tile: already in order
+    const uint32_t hi = HX ? uint32_t(ts_hi[ta]) << kOtRuleBits : 0u;
     for (int64_t p = threadIdx.x; p < e_n; p += kThreads) {
       const uint32_t w = uint32_t(rin[lo_n + p]);  // PIN: a packed word
       const int64_t off = PIN ? int64_t(w >> kOtRuleBits) : int64_t(tin[lo_n + p]);
       __builtin_nontemporal_store(t0 + 1 + off, tout + lo_n + p);
-      __builtin_nontemporal_store(PIN ? int32_t(w & ((1u << kOtRuleBits) - 1u)) : int32_t(w), rout + lo_n + p);
+      __builtin_nontemporal_store(PIN ? int32_t(hi | (w & kOtLowMask)) : int32_t(w), rout + lo_n + p);
     }
     continue;
   }
@@ -878,12 +959,13 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
     continue;
   }
   for (int j = threadIdx.x; j <= kOtSlabs; j += kThreads) slab_off[j] = slab_tab[int64_t(n) * kOtPre + j];
+  if (HX && threadIdx.x < M) ph[threadIdx.x] = ts_hi[ta + threadIdx.x];
   ot_sync<NW>();
   // the longest run of whole slabs [j0, j1) that fits one chunk (j1 == j0: a
-  // slab of more than a chunk)
+  // slab of more than a chunk); HX: and spans at most 256 s
   auto run_end = [&](int j0) {
     int j1 = j0;
-    while (j1 < kOtSlabs && slab_off[j1 + 1] - slab_off[j0] <= kChunk)
+    while (j1 < kOtSlabs && (!HX || ((j1 + 1 - j0) << sb) <= 256) && slab_off[j1 + 1] - slab_off[j0] <= kChunk)
       j1++;
     return j1;
   };
@@ -892,6 +974,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
   static_assert(kOtMaxTiles <= kThreads, "one tile per thread");
   const int q_own = threadIdx.x;
   const int32_t* __restrict__ pq = pre + (ta + (q_own < M ? q_own : 0)) * kOtPre;
+  const int32_t qs = int32_t(ts_start[ta + (q_own < M ? q_own : 0)] - lo_n);  // tile q's first event, node-relative
   int ja = 0, jb = run_end(0);
   int32_t pa = pq[0], pb = pq[jb];
   while (ja < kOtSlabs) {
@@ -911,14 +994,14 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
       // rel = offset - the run's first second (< 64 * (jb - ja)): one 8-bit
       // pass for up to 4 slabs
       const int64_t o = lo_n + slab_off[ja];
-      ot_merge_chunk<NW, PACK, IT, PIN>(
+      ot_merge_chunk<NW, PACK, IT, PIN, HX>(
           tin + lo_n, rin + lo_n, int(M), int(slab_off[jb] - slab_off[ja]), uint32_t(ja) << sb,
           ((jb - ja) << sb) > 256 ? 2 : 1,
           [&](int q, int32_t* src) {
-            *src = q * kOtTile + pa;  // q == q_own
+            *src = qs + pa;  // q == q_own
             return pb - pa;
           },
-          t0, tout + o, rout + o, s, pk, rl, ps, psrc, wsum, err);
+          t0, tout + o, rout + o, s, pk, rl, ps, psrc, wsum, err, uint32_t(e_n), ph);
     }
     ja = ja2;
     jb = jb2;
@@ -931,7 +1014,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
 // The slabs k_ot_merge queued for a bigger chunk (more than its own, at most
 // 64 * kOtMidWaves * kOtItems events), one per workgroup turn: the same
 // gather + one-pass LDS sort with NW waves (a slab of 64 s: one 8-bit pass).
-template <int NW, bool PACK, int IT = kOtItems, bool PIN = false>
+template <int NW, bool PACK, int IT = kOtItems, bool PIN = false, bool HX = false>
 __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                     const int64_t* __restrict__ tile_base,
                                                     const int64_t* __restrict__ node_off,
@@ -940,9 +1023,11 @@ __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_
                                                     int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                     const int64_t* __restrict__ mid,
                                                     const unsigned* __restrict__ mid_n, int64_t* __restrict__ err,
-                                                    int sb) {
+                                                    int sb, const int64_t* __restrict__ ts_start,
+                                                    const int32_t* __restrict__ ts_hi) {
   constexpr int kChunk = 64 * NW * IT;
   __shared__ OtRank<NW, 256> s;
+  __shared__ int32_t ph[HX ? kOtMaxTiles : 1];
   __shared__ uint32_t pk[kChunk + kChunk / 32];
   __shared__ int32_t rl[PACK ? 1 : kChunk];
   __shared__ int32_t ps[kOtMaxTiles + 1];
@@ -961,29 +1046,33 @@ __global__ __launch_bounds__(64 * NW, CG_OT_MID_WPE) void k_ot_mid(const uint16_
       if (threadIdx.x == 0) atomicOr(reinterpret_cast<unsigned long long*>(err), 1ull);
       continue;
     }
-    ot_merge_chunk<NW, PACK, IT, PIN>(
+    if (HX && threadIdx.x < M) ph[threadIdx.x] = ts_hi[ta + threadIdx.x];
+    ot_merge_chunk<NW, PACK, IT, PIN, HX>(
         tin + lo_n, rin + lo_n, int(M), int(n_el), uint32_t(j) << sb, 1,
         [&](int q, int32_t* src) {
           const int32_t* pt = pre + (ta + q) * kOtPre;
-          *src = q * kOtTile + pt[j];
+          *src = int32_t(ts_start[ta + q] - lo_n) + pt[j];
           return pt[j + 1] - pt[j];
         },
-        t0, tout + lo_n + a, rout + lo_n + a, s, pk, rl, ps, psrc, wsum, err);
+        t0, tout + lo_n + a, rout + lo_n + a, s, pk, rl, ps, psrc, wsum, err,
+        uint32_t(node_off[n + 1] - lo_n), ph);
   }
 }
 
 // The slabs k_ot_merge queued, one per workgroup turn: the slab's
 // histogram of its 16 seconds over all its portions first, then its chunks
 // in order, each sorted in LDS and stored at its seconds' running bases.
-template <bool PIN>
+template <bool PIN, bool HX = false>
 __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin, const int32_t* __restrict__ rin,
                                                  const int64_t* __restrict__ tile_base,
                                                  const int64_t* __restrict__ node_off,
                                                  const int32_t* __restrict__ pre, int64_t t0,
                                                  int64_t* __restrict__ tout, int32_t* __restrict__ rout,
                                                  const int64_t* __restrict__ big, const unsigned* __restrict__ big_n,
-                                                 int64_t* __restrict__ err, int sb) {
+                                                 int64_t* __restrict__ err, int sb, const int64_t* __restrict__ ts_start,
+                                                 const int32_t* __restrict__ ts_hi) {
   __shared__ OtRank<4, 64> s;
+  __shared__ int32_t ph[HX ? kOtMaxTiles : 1];
   __shared__ uint32_t pk[kOtTile + kOtTile / 32];
   __shared__ int32_t rl[kOtTile];
   __shared__ int32_t ps[kOtMaxTiles + 1];
@@ -1000,13 +1089,16 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
     const int32_t n = int32_t(big[task] >> 8);
     const int j = int(big[task] & 255);
     const int64_t ta = tile_base[n], M = tile_base[n + 1] - ta, lo_n = node_off[n];
-    // portions of tiles [ga, ga + gm): per tile its events of slab j
+    // portions of tiles [ga, ga + gm): per tile its events of slab j,
+    // sources relative to tile ga's first event
     auto list = [&](int64_t ga, int64_t gm) {
+      if (HX && threadIdx.x < gm) ph[threadIdx.x] = ts_hi[ta + ga + threadIdx.x];
+      const int64_t g0 = ts_start[ta + ga];
       ot_portions<4>(
           int(gm),
           [&](int q, int32_t* src) {
             const int32_t* pt = pre + (ta + ga + q) * kOtPre;
-            *src = q * kOtTile + pt[j];
+            *src = int32_t(ts_start[ta + ga + q] - g0) + pt[j];
             return pt[j + 1] - pt[j];
           },
           ps, psrc, wsum);
@@ -1028,8 +1120,9 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
       for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
-        ot_gather<false, 0, false, kOtItems, false, PIN>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc,
-                                                         own, c0, n_el, key, rl);
+        const int64_t g0 = ts_start[ta + ga];
+        ot_gather<false, 0, false, kOtItems, false, PIN, HX>(tin + g0, rin + g0, ps, psrc, own, c0, n_el, key, rl, 0,
+                                                             0, ph);
 #pragma unroll
         for (int jj = 0; jj < kOtItems; jj++)
           if (ebase + jj * 64 + lane < n_el) atomicAdd(&hist[(key[jj] >> kOtIdxBits) & kSec], 1);
@@ -1054,8 +1147,9 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
       for (int32_t c0 = 0; c0 < n_grp; c0 += kOtTile) {
         const int n_el = n_grp - c0 < kOtTile ? int(n_grp - c0) : kOtTile;
         ot_owners<4>(ps, Q, c0, n_el, own, wsum);
-        ot_gather<true, 0, false, kOtItems, false, PIN>(tin + lo_n + ga * kOtTile, rin + lo_n + ga * kOtTile, ps, psrc,
-                                                        own, c0, n_el, key, rl);
+        const int64_t g0 = ts_start[ta + ga];
+        ot_gather<true, 0, false, kOtItems, false, PIN, HX>(tin + g0, rin + g0, ps, psrc, own, c0, n_el, key, rl, 0, 0,
+                                                            ph);
         ot_sort<4, 64, false>(key, n_el, uint32_t(j) << sb, 0, 1, pk, s);
         bool bad = false;
         for (int p = threadIdx.x; p < n_el; p += 256) {
@@ -1086,8 +1180,9 @@ int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads
 // (k_ot_tile over the writer's lists), order_tail (slab offsets, k_ot_merge, k_ot_big).
 namespace {
 
-int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipStream_t st, int64_t* Tmax) {
-  *Tmax = cap / kOtTile + N + 1;
+int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipStream_t st, int64_t* Tmax,
+                const OtCut& cut) {
+  *Tmax = cap / kOtTile + int64_t(N) * cut.H + 1;
   const int64_t toff_words = (cap + 3) / 4;  // 16-bit offsets in the int64 second buffer
   // ts_off: [k_ot_big queue N*kOtSlabs][big, mid, dense-node, mid2 counters: 2 words][slab_tab N*kOtPre]
   // [k_ot_mid queue N*kOtSlabs][its 16-wave form's queue N*kOtSlabs]
@@ -1095,18 +1190,20 @@ int order_setup(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, hipS
   // growing a buffer frees the old one: earlier windows' kernels finish first
   if (c->ts_cnt.cap < size_t(N) || c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(*Tmax) ||
       c->ts_hist.cap < size_t(*Tmax * kOtPre) || c->node_time2.cap < size_t(toff_words) ||
-      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->scan_tmp.cap < scan_temp_bytes(N))
+      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->scan_tmp.cap < scan_temp_bytes(N) ||
+      c->ts_start.cap < size_t(*Tmax + 1) || c->ts_hi.cap < size_t(*Tmax))
     HIPCHK(hipStreamSynchronize(st));
   int rc;
   if ((rc = c->ts_cnt.ensure(N)) || (rc = c->ts_base.ensure(int64_t(N) + 1)) || (rc = c->ts_tile_node.ensure(*Tmax)) ||
       (rc = c->ts_hist.ensure(*Tmax * kOtPre)) || (rc = c->node_time2.ensure(toff_words)) ||
-      (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) ||
-      (rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N)))))
+      (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) || (rc = c->ts_start.ensure(*Tmax + 1)) ||
+      (rc = c->ts_hi.ensure(*Tmax)) || (rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N)))))
     return rc;
-  hipLaunchKernelGGL(k_ts_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, node_off, N, kOtTile, cap, c->ts_cnt.p);
+  hipLaunchKernelGGL(k_ot_tile_count, dim3(gridn(N, 256)), dim3(256), 0, st, node_off, N, cap, cut, c->ts_cnt.p);
   launch_scan(c->ts_cnt.p, c->ts_base.p, N, c->scan_tmp.p, st);
-  hipLaunchKernelGGL(k_ts_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, N, c->ts_tile_node.p);
-  return CG_OK;
+  hipLaunchKernelGGL(k_ot_tiles, dim3(gridn(N, 256)), dim3(256), 0, st, c->ts_base.p, node_off, N, cut,
+                     c->ts_tile_node.p, c->ts_start.p, c->ts_hi.p);
+  return cg_hip_check(hipGetLastError(), "time-order tiles");
 }
 
 // Slab width 2^sb seconds for a window of H <= 4096 s: 64 s, or 32 s when the
@@ -1122,8 +1219,10 @@ int ot_slab_bits(int64_t H) { return H <= 2048 ? kOtSlabBits - 1 : kOtSlabBits; 
 #define CG_OT_DENSE_PER_SLAB 2048  // average events per 64-s slab above which a node takes the 8-wave merge
 #endif
 // pin: the tiles were stored as packed words offset << 20 | rule (in node_rule2)
+// pack: the tiles hold packed words (rule indices < 2^20, or hx); hx: rule
+// indices past 2^20 (tiles cut where rule >> 20 changes, ts_hi)
 int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st, int64_t* err,
-               int64_t R, bool pin, int sb) {
+               bool pack, bool pin, bool hx, int sb) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
   // [0] big, [1] mid, [2] the dense merge's node ticket, [3] mid2
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
@@ -1136,7 +1235,6 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   // nodes' merge runs on its own stream beside the sparse one (few dense
   // nodes after all the sparse ones would run as a tail at low occupancy)
   const int64_t dense_min = int64_t(CG_OT_DENSE_PER_SLAB) * std::max<int64_t>(1, (H + 63) / 64);
-  const bool pack = R <= (int64_t(1) << kOtRuleBits);
   hipLaunchKernelGGL(k_ot_slabs, dim3(unsigned(N)), dim3(64), 0, st, c->ts_base.p, c->ts_hist.p, N, slab_tab);
   if (!c->st_ot) {  // created together: the ctx holds all three or none
     hipStream_t so = nullptr;
@@ -1160,10 +1258,11 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
     hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtDenseWaves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
-                       dense_min, INT64_MAX, big_n + 2, err, sb);
+                       dense_min, INT64_MAX, big_n + 2, err, sb, c->ts_start.p, c->ts_hi.p);
     hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
-                       mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err, sb);
+                       mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err, sb, c->ts_start.p,
+                       c->ts_hi.p);
     // k_ot_mid's queue is filled by the 4-wave merge only (the 8-wave merge's
     // chunk holds any slab of <= 8192 events).  Its blocks find no room
     // beside the dense merge (whose persistent grid holds every CU's VGPRs),
@@ -1174,14 +1273,18 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
     (void)hipStreamWaitEvent(c->st_ot, c->ot_fork, 0);
     hipLaunchKernelGGL(mid_k, dim3(unsigned(cus * 3)), dim3(64 * kOtMidWaves), 0, c->st_ot,
                        toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p,
-                       c->node_rule.p, mid, big_n + 1, err, sb);
+                       c->node_rule.p, mid, big_n + 1, err, sb, c->ts_start.p, c->ts_hi.p);
     (void)hipEventRecord(c->ot_join, c->st_ot);
     (void)hipStreamWaitEvent(st, c->ot_join, 0);
     hipLaunchKernelGGL(mid2_k, dim3(unsigned(cus)), dim3(64 * kOtMid2Waves), 0, st, toff, c->node_rule2.p,
                          c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
-                         big_n + 3, err, sb);
+                         big_n + 3, err, sb, c->ts_start.p, c->ts_hi.p);
   };
-  if (pack && pin)
+  if (hx)
+    merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true, true>,
+           k_ot_merge<kOtDenseWaves, true, kOtDenseItems, true, true, true>,
+           k_ot_mid<kOtMidWaves, true, kOtItems, true, true>, k_ot_mid<kOtMid2Waves, true, kOtItems, true, true>);
+  else if (pack && pin)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,
            k_ot_merge<kOtDenseWaves, true, kOtDenseItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,
            k_ot_mid<kOtMid2Waves, true, kOtItems, true>);
@@ -1194,40 +1297,53 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   auto big = [&](auto k) {
     hipLaunchKernelGGL(k, dim3(unsigned(std::max(1, c->write_blocks))), dim3(256), 0, st, toff, c->node_rule2.p,
                        c->ts_base.p, node_off, c->ts_hist.p, t0, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
-                       err, sb);
+                       err, sb, c->ts_start.p, c->ts_hi.p);
   };
-  pin ? big(k_ot_big<true>) : big(k_ot_big<false>);
+  hx ? big(k_ot_big<true, true>) : (pin ? big(k_ot_big<true>) : big(k_ot_big<false>));
   return cg_hip_check(hipGetLastError(), "time-order kernels");
 }
 
 }  // namespace
 
 // The tile sort + merge of the per-node lists already in c->node_time /
-// c->node_rule (node offsets node_off[N+1] on the device): used by
-// cg_node_result_order_by_time.
+// c->node_rule (node offsets node_off[N+1] on the device): the writer's
+// packed words / 16-bit offsets, or (cg_node_result_order_by_time) int64
+// times.  Packed words of rule indices past 2^20 (in_mode kInPacked) need the
+// lists' band offsets (cut): their tiles are cut where rule >> 20 changes.
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
-                        hipStream_t st, int in_mode, int64_t* err) {
+                        hipStream_t st, int in_mode, int64_t* err, const TileCut& cut) {
   if (N == 0 || cap == 0) return CG_OK;
+  const bool low = c->pn_R <= (int64_t(1) << kOtRuleBits);
+  const bool hx = in_mode == kInPacked && !low;
+  OtCut oc{nullptr, 1, 1, 1};
+  if (hx) {
+    if (!cut.seg_pos || cut.B <= 0 || (int64_t(1) << kOtRuleBits) % cut.B != 0 ||
+        c->pn_R > (int64_t(1) << (kOtRuleBits + kOtHiBits)))
+      return cg_fail(CG_EINVAL, "time order: packed lists past 2^20 rules need band offsets of bands dividing 2^20");
+    oc = OtCut{cut.seg_pos, cut.K, int32_t((int64_t(1) << kOtRuleBits) / cut.B),
+               int32_t((c->pn_R + (int64_t(1) << kOtRuleBits) - 1) >> kOtRuleBits)};
+  }
   int64_t Tmax = 0;
-  int rc = order_setup(c, node_off, N, cap, st, &Tmax);
+  int rc = order_setup(c, node_off, N, cap, st, &Tmax, oc);
   if (rc) return rc;
   uint16_t* toff = reinterpret_cast<uint16_t*>(c->node_time2.p);
-  // the tiles stored as packed words when every rule index is below 2^20
-  const bool pack = c->pn_R <= (int64_t(1) << kOtRuleBits);
+  // the tiles stored as packed words when every rule index is below 2^20, or
+  // (hx) as the writer's words with the high bits per tile
+  const bool pack = low || hx;
   const int sb = ot_slab_bits(H);
   auto tile = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(unsigned(Tmax)), dim3(256), 0, st, c->node_time.p, c->node_rule.p, c->ts_tile_node.p,
-                       c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p, c->ts_base.p + N, err, sb);
+                       c->ts_base.p, node_off, t0, toff, c->node_rule2.p, c->ts_hist.p, c->ts_base.p + N, err, sb,
+                       c->ts_start.p);
   };
   if (in_mode == kInPacked) {
-    if (!pack) return cg_fail(CG_EINVAL, "time order: packed lists need rule indices below 2^20");
     tile(k_ot_tile<2, true>);
   } else if (in_mode == kIn16) {
-    pack ? tile(k_ot_tile<1, true>) : tile(k_ot_tile<1, false>);
+    low ? tile(k_ot_tile<1, true>) : tile(k_ot_tile<1, false>);
   } else {
-    pack ? tile(k_ot_tile<0, true>) : tile(k_ot_tile<0, false>);
+    low ? tile(k_ot_tile<0, true>) : tile(k_ot_tile<0, false>);
   }
-  return order_tail(c, node_off, N, t0, H, st, err, c->pn_R, pack, sb);
+  return order_tail(c, node_off, N, t0, H, st, err, pack, pack, hx, sb);  // packed tiles: packed words in node_rule2
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
@@ -1249,7 +1365,7 @@ extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   return rc;
 }
 
-bool pn_pack_ok(int64_t R) { return R <= (int64_t(1) << kOtRuleBits); }
+bool pn_pack_ok(int64_t R) { return R <= (int64_t(1) << (kOtRuleBits + kOtHiBits)); }
 
 bool order_lsd_only() {
   static const bool lsd_only = getenv("CG_ORDER_LSD") != nullptr;
@@ -1275,7 +1391,10 @@ int order_by_time_locked(cg_ctx* c, int in_mode) {
     if ((rc = pn_ensure_res(c))) return rc;
     c->pn_res_host[2] = 0;
     (void)hipEventRecord(c->pev[0], st);
-    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, H, st, in_mode, c->pn_res_dev + 2))) return rc;
+    TileCut cut;  // the writer's packed words past 2^20 rules: tiles cut at the band offsets of this result
+    if (in_mode == kInPacked) cut = TileCut{c->seg_pos.p, c->pn_K, c->pn_B, c->pn_R};
+    if ((rc = order_merge_enqueue(c, c->node_off.p, N, En, c->pn_t0, H, st, in_mode, c->pn_res_dev + 2, cut)))
+      return rc;
     (void)hipEventRecord(c->pev[1], st);
     if ((rc = cg_hip_check(hipStreamSynchronize(st), "sync"))) return rc;
     if (c->pn_res_host[2]) return cg_fail(CG_EHIP, kOrderCheckMsg);

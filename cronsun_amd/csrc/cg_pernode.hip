@@ -638,7 +638,9 @@ __global__ __launch_bounds__(256) void k_node_write(
   const uint64_t le = (2ull << lane) - 1ull;  // lanes <= this one
   const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
 #if CG_NODE_GRP_XCD
-  const int grp = int((blockIdx.x >> 3) % unsigned(ng));  // every group across the 8 XCDs (cf. k_write_cf)
+  // every group across the 8 XCDs (cf. k_write_cf), when the grid gives
+  // every group a block that way (a small grid: one group per block)
+  const int grp = int(gridDim.x >= 8u * unsigned(ng) ? (blockIdx.x >> 3) % unsigned(ng) : blockIdx.x % unsigned(ng));
 #else
   const int grp = int(blockIdx.x % unsigned(ng));
 #endif
@@ -681,7 +683,7 @@ __global__ __launch_bounds__(256) void k_node_write(
     int32_t* __restrict__ orl = out_rule + abase;
     auto put = [&](int32_t q, int64_t val, int32_t rv) {
       if constexpr (OUT == kInPacked) {
-        out_store<V>(orl + q, int32_t((uint32_t(val - t0 - 1) << 20) | uint32_t(rv)));
+        out_store<V>(orl + q, int32_t((uint32_t(val - t0 - 1) << 20) | (uint32_t(rv) & 0xFFFFFu)));  // rule >> 20: per tile
         return;
       }
       if constexpr (OUT == kIn16) out_store<V>(o16 + q, uint16_t(val - t0 - 1));
@@ -1165,11 +1167,13 @@ __global__ void k_band_max(const int64_t* __restrict__ off, int64_t R, int32_t B
 // balance them (else every XCD's blocks walk the bands in order)
 int32_t seg_xcd_groups(int32_t K) { return CG_SEG_XCD > 1 && K >= 4 * CG_SEG_XCD ? CG_SEG_XCD : 1; }
 
+// (at most 2^20 rules: the time-order pass cuts its tiles at multiples of
+// 2^20 in rule index, found at band boundaries)
 int32_t band_rules(int64_t R, int64_t E) {
   const double per_rule = double(std::max<int64_t>(E, 1)) * 8.0 / double(std::max<int64_t>(R, 1));
   int64_t B = int64_t(double(CG_BAND_BYTES) / per_rule);
   int64_t p = 1024;
-  while (p < B && p < R) p <<= 1;
+  while (p < B && p < R && p < (int64_t(1) << 20)) p <<= 1;
   return int32_t(std::max<int64_t>(p, 1024));
 }
 
@@ -1541,7 +1545,8 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
                            dim3(256), 0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p,
                            a.times.p, N, K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p,
                            kNodeMajorOrdered);
-      if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, t1 - t0, st, in_mode, a.res_dev + 2)))
+      if ((rc = order_merge_enqueue(c, a.node_off.p, N, node_cap, t0, t1 - t0, st, in_mode, a.res_dev + 2,
+                                    TileCut{a.seg_pos.p, K, B, R})))
         return rc;
     } else {
       hipLaunchKernelGGL((k_node_write<0, kInTimes>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),

@@ -285,13 +285,15 @@ def progression_rules(R, n_nodes):
     from cronsun_amd.engine import RulesIn
     nids = np.stack([np.arange(R) % n_nodes, (7 * np.arange(R) + 1) % n_nodes], 1)
     nids = np.sort(nids, 1)
-    keep = [sorted(set(p)) for p in nids.tolist()]
+    same = nids[:, 0] == nids[:, 1]  # one node: listed once
     nid_off = np.zeros(R + 1, np.int64)
-    nid_off[1:] = np.cumsum([len(k) for k in keep])
+    nid_off[1:] = np.cumsum(np.where(same, 1, 2))
+    keep = np.ones((R, 2), bool)
+    keep[:, 1] = ~same
     z = np.zeros(R + 1, np.int64)
     return RulesIn(n_nodes, 0, R, R, group_off=np.zeros(1, np.int64), group_nodes=np.zeros(0, np.int32),
                    group_exists=np.zeros(0, np.uint8), rule_job=np.arange(R, dtype=np.int32), nid_off=nid_off,
-                   nids=np.concatenate([np.array(k, np.int32) for k in keep]), gid_off=z,
+                   nids=nids[keep].astype(np.int32), gid_off=z,
                    gids=np.zeros(0, np.int32), ex_off=z, ex=np.zeros(0, np.int32),
                    job_pause=np.zeros(R, np.uint8))
 
@@ -570,26 +572,31 @@ def test_per_node_bands_past_2_30_fires():
     e2.close()
 
 
-@pytest.mark.parametrize("writer", ["pass", "direct"])
-def test_per_node_time_ordered_over_2_20_rules(writer):
-    """More than 2^20 rules: the time order cannot pack (offset, rule) into one
-    32-bit word, so the writer emits 16-bit offsets + rules ("direct") or the
-    pass reads the int64 lists ("pass"), and the tile sort and merges keep an
-    LDS rule array -- the path every smaller test skips.  1.1 M rules on 64
-    nodes, 134 every-second rules (all on nodes 0 and 1: ~8.6 k events per
-    64-s slab there, the dense merge and k_ot_mid's 16-wave form, whose
-    16384-event chunks need 14 index bits) and 1100 every-10-s rules among
-    never-firing ones, 10 minutes; four nodes' lists against the oracle's,
-    sorted by (time, rule)."""
+@pytest.mark.parametrize("writer,R", [("pass", (1 << 20) + 50_000), ("direct", (1 << 20) + 50_000),
+                                      ("direct", (1 << 24) + 50_000)])
+def test_per_node_time_ordered_over_2_20_rules(writer, R):
+    """More than 2^20 rules: (offset, rule) no longer fits one 32-bit word.
+    "direct" below 2^24 rules: the writer's packed words hold rule & 0xFFFFF,
+    the tiles are cut where rule >> 20 changes (at band boundaries) and carry
+    those bits, and the merges rebuild the rule from the tile (keys rel << 24
+    | rule).  "direct" past 2^24: 16-bit offsets + rules, the tile sort and
+    merges keep an LDS rule array; "pass": the separate pass over the int64
+    lists (unpacked).  134 every-second rules per 2^20 (all on nodes 0 and 1:
+    ~8.6 k events per 64-s slab there, the dense merge and k_ot_mid's 16-wave
+    form, whose 16384-event chunks need 14 index bits) and every-10-s rules
+    every 1000 rules among never-firing ones, 10 minutes; four nodes' lists
+    (each across every block of 2^20 rules) against the oracle's, sorted by
+    (time, rule)."""
     from cronsun_amd.engine import Engine
-    R, N = (1 << 20) + 50_000, 64
+    N = 64
     kinds = ["0 0 0 1 1 *", "* * * * * *", "*/10 * * * * *"]
     kind = np.zeros(R, np.int64)
     kind[::8192] = 1
     kind[1::1000] = 2
-    specs = [kinds[k] for k in kind.tolist()]
-    arr, status = cron.parse_batch(specs, threads=16)
+    karr, status = cron.parse_batch(kinds, threads=1)
     assert not np.any(status)
+    a = np.ascontiguousarray(np.ctypeslib.as_array(karr)[kind])  # rule i = kinds[kind[i]]
+    arr = (karr._type_ * R).from_buffer(a)
     rin = progression_rules(R, N)
     t0 = synth.T0_2026 + 20 * DAY + 123  # January 25: the yearly rules never fire
     t1 = t0 + 600
