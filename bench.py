@@ -74,7 +74,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def pmc_traffic(tag, rules, events, kernels, per, scale=1):
+def pmc_traffic(tag, rules, events, kernels, per, scale=1, windows=None):
     """HBM bytes of one timed interval, from the newest committed rocprofv3
     PMC summary profiles/rNN_pmc_traffic[_<tag>][_vK].json (written by
     tools/pmc_traffic.py from FETCH_SIZE / WRITE_SIZE passes) measured on the
@@ -98,6 +98,8 @@ def pmc_traffic(tag, rules, events, kernels, per, scale=1):
                 d = json.load(f)
             if d.get("rules") != rules or d.get("events") != events:
                 continue
+            if windows is not None and d.get("windows", windows) != windows:
+                continue  # another windowing of the same step: other bytes per launch
             ks = d["kernels"]
             n_per = ks[per]["calls"]
             tot = sum(v["hbm_bytes_per_launch"] * v["calls"] for k, v in ks.items()
@@ -318,11 +320,12 @@ def main():
             # GB of lists), within HBM beside the three window sets' records;
             # the per-window side chain (rule infos, segment records over all
             # 920 M pairs) is then paid 168 times per step instead of 336.
-            # Time order past 2^20 rules per rank takes 2048-s windows: 64
-            # slabs of 32 s (the tile sort's 64 slab digits), which fit
-            # k_ot_mid's chunks (64-s slabs of a 1-h window would go to
-            # k_ot_big's two reads), in 296 windows per 7 days
-            W = 2048 if (args.time_order and R > (1 << 20)) else 3600
+            # Time order past 2^20 rules per rank keeps 30-min windows: their
+            # 32-s slabs fit k_ot_mid's chunks (64-s slabs of a 1-h window
+            # would go to k_ot_big's two reads).  2048-s windows (64 slabs of
+            # 32 s, 296 windows) measured the same: 15.56 vs 15.49 s per step,
+            # more slabs past k_ot_mid's chunk (profiles/r06_pmc_traffic_config4pn_order_2048.json)
+            W = 1800 if (args.time_order and R > (1 << 20)) else 3600
 
         def spec_of(i):  # local rule i of this rank's range
             return base_specs[(shard_lo + i) % base_n]
@@ -729,7 +732,7 @@ def main():
         tag = {"pernode": "pernode", "config3": "config3", "config4": "config4pn"}[wl] + \
             ("_order" if args.time_order else "")
         if args.zone == "UTC" and xmode == 0:
-            traffic_src = pmc_traffic(tag, R, E, kernels, "k_node_write", scale=nw)
+            traffic_src = pmc_traffic(tag, R, E, kernels, "k_node_write", scale=nw, windows=nw)
     else:
         algo_bytes = R * SPEC_BYTES + E * 8 + (R + 1) * 8   # per rank, per launch
         kname, ksec = "k_write_cf", kt[3] / 1e3

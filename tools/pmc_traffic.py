@@ -103,6 +103,8 @@ def main():
         b = json.loads(line)
         res["rules"] = b["config"]["rules_per_gpu"]
         res["events"] = b["config"]["events_per_gpu_step"]
+        if "windows" in b["config"]:
+            res["windows"] = b["config"]["windows"]
         res["bench"] = {k: b[k] for k in ("value", "ms_per_step", "kernel_ms", "roofline")}
     ks = kernel_stats(a.kt) if a.kt else {}
     fe = counters(a.fetch, "FETCH_SIZE") if a.fetch else {}
