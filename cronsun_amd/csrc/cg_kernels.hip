@@ -584,6 +584,10 @@ __global__ void k_chunk_map(const int64_t* __restrict__ run_off, int64_t nruns, 
 // Across the XCDs: dry within 40 us, idle 3.3 %, k_write_cf 0.980 -> 0.946 ms
 // (same box, profiles/r06_ab_writer_groups.txt; moving on to other groups
 // when dry, CG_WRITE_STEAL_SMALL, gains nothing on top).
+#ifndef CG_WRITE_GROUPS_SMALL
+#define CG_WRITE_GROUPS_SMALL 8
+#endif
+constexpr int kWriteGroupsSmall = CG_WRITE_GROUPS_SMALL < kTicketGroups ? CG_WRITE_GROUPS_SMALL : kTicketGroups;
 #ifndef CG_WRITE_GRP_XCD
 #define CG_WRITE_GRP_XCD 1
 #endif
@@ -671,7 +675,13 @@ __global__ __launch_bounds__(kWriteWaves * 64, CG_WRITE_WPE) void k_write_cf(
   // group has run out moves on to the next group's counter (no group's tail
   // waits on its own waves alone).  Tickets are taken one slice ahead so the atomic's latency
   // hides under the current slice.
-  const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
+  // 8 ticket groups for small slices, 32 for large ones (same-box A/B,
+  // profiles/r06_ab_ticket_groups.txt and r06_ab_ticket_groups_pn.txt: config 2
+  // writer 0.957 -> 0.941 ms with 8 instead of 32; config 4's large slices,
+  // which move on to other groups, 26.0 -> 26.6 ms with 8).  Fewer groups of
+  // more blocks each progress at closer rates, so they run dry closer together.
+  const int groups = sh == CG_SUPER_SHIFT_LARGE ? kTicketGroups : kWriteGroupsSmall;
+  const int ng = int(gridDim.x) < groups ? int(gridDim.x) : groups;
 #if CG_WRITE_GRP_XCD
   // every group spans the 8 XCDs (blocks b..b+7 of one dispatch round share a
   // group): a group's slices then advance at the chip's average rate

@@ -608,6 +608,12 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 // ticket groups across the 8 XCDs, as k_write_cf's (same box,
 // profiles/r06_ab_node_writer_groups.txt: config 3 174.9 -> 170.7 ms per
 // step, node writer 152.1 -> 146.7; pernode equal)
+// 8 ticket groups (same-box A/B, profiles/r06_ab_ticket_groups_pn.txt:
+// pernode node writer 2.45 -> 2.29 ms with 8 instead of 32, config 3 -1.5 %)
+#ifndef CG_NODE_GROUPS
+#define CG_NODE_GROUPS 8
+#endif
+constexpr int kNodeGroups = CG_NODE_GROUPS < kTicketGroups ? CG_NODE_GROUPS : kTicketGroups;
 #ifndef CG_NODE_GRP_XCD
 #define CG_NODE_GRP_XCD 1
 #endif
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(256) void k_node_write(
   const int64_t NK = int64_t(N) * K;
   if (seg_pos[NK] > cap) return;  // output too small: the host grows it and relaunches
   const uint64_t le = (2ull << lane) - 1ull;  // lanes <= this one
-  const int ng = gridDim.x < kTicketGroups ? int(gridDim.x) : kTicketGroups;
+  const int ng = int(gridDim.x) < kNodeGroups ? int(gridDim.x) : kNodeGroups;
 #if CG_NODE_GRP_XCD
   // every group across the 8 XCDs (cf. k_write_cf), when the grid gives
   // every group a block that way (a small grid: one group per block)
