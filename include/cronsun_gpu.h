@@ -467,8 +467,8 @@ int cg_node_csr_place(cg_ctx* ctx, int32_t n_nodes, const int64_t* d_src_node_of
  * place into (time, rule) order -- equal times by global rule index, which
  * for job-ID-range shards is rank order -- the list one scheduler over all
  * jobs would hold.  Works through a scratch copy of node groups of at most
- * budget_bytes / 12 events (a larger node alone); world <= 64.  Returns after
- * the merge (stream synchronised). */
+ * budget_bytes / 12 events (a larger node alone; never more than the events
+ * being merged); world <= 64.  Returns after the merge (stream synchronised). */
 int cg_node_csr_merge_ranks(cg_ctx* ctx, int32_t n_nodes, int32_t world, const int64_t* run_bounds,
                             int64_t* d_time, int32_t* d_rule, int64_t budget_bytes);
 
@@ -538,7 +538,11 @@ int cg_expand_per_node_wait(cg_ctx* ctx, int64_t* n_events, int64_t* n_events_al
  *                       node's slices into one (time, rule)-ordered list
  *                       (cg_node_csr_merge_ranks), the byTime list of one
  *                       scheduler over every job; ranks mixing the two orders
- *                       are refused.  The payload moves in chunks of whole
+ *                       are refused, and so are time-ordered results of more
+ *                       than 64 ranks or whose rule_base does not ascend with
+ *                       the rank among the ranks holding events (the merge
+ *                       breaks time ties by rank), on every rank before any
+ *                       transfer.  The payload moves in chunks of whole
  *                       node ranges (a node larger than the budget in parts)
  *                       whose peer bytes (12 B per event) stay within
  *                       budget_bytes (the smallest any rank passes; at least
