@@ -894,8 +894,21 @@ def launch_ranks(args):
     return p.wait()
 
 
-def gather_check(eng, dist, world, rank, backend, loc, zone, t0, dev, cdev, restore_order=0, rules_per_rank=50_000,
-                 n_nodes=200, window=600, n_check=24, seed=0x5EED + 91):
+def gather_check(eng, dist, world, rank, *args, **kw):
+    """_gather_check, with a failure reported in the record ({"verified":
+    False, "error": ...}) instead of ending the run: the timed line above it
+    stays.  The library's calls return the same status on every rank, so the
+    ranks fail at the same point and meet at the closing barrier."""
+    try:
+        return _gather_check(eng, dist, world, rank, *args, **kw)
+    except Exception as e:  # noqa: BLE001 -- reported, then the barrier
+        log(f"[rank {rank}] gather check failed: {e!r}")
+        dist.barrier()
+        return {"verified": False, "error": repr(e)[:800]} if rank == 0 else None
+
+
+def _gather_check(eng, dist, world, rank, backend, loc, zone, t0, dev, cdev, restore_order=0, rules_per_rank=50_000,
+                  n_nodes=200, window=600, n_check=24, seed=0x5EED + 91):
     """N > 1, after the timed region: the multi-rank exchange of the per-node
     view, run and verified.  A pernode-shaped job set (`rules_per_rank` jobs
     per rank in job-ID ranges, `n_nodes` nodes, the light spec mix), one
