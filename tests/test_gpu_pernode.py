@@ -628,3 +628,44 @@ def test_per_node_time_ordered_over_2_20_rules(writer, R):
         assert np.array_equal(time[a:b], exp_t[order]), n
         assert np.array_equal(rule[a:b], exp_r[order]), n
 
+
+
+def test_per_node_time_ordered_over_2_20_rules_big_slabs():
+    """Packed words past 2^20 rules through k_ot_big: ~610 every-second rules
+    spread over 1.1 M rules (every block of 2^20 holds some), all on both of
+    2 nodes, over a 1-h window: each node holds ~2.2 M events in more than
+    kOtMaxTiles tiles (every slab to k_ot_big) and 64-s slabs of ~39 k events;
+    the tiles are cut where rule >> 20 changes and k_ot_big rebuilds the rule
+    from each portion's tile.  Both nodes' whole lists against the oracle's,
+    sorted by (time, rule)."""
+    from cronsun_amd.engine import Engine
+    R, N = (1 << 20) + 50_000, 2
+    kinds = ["0 0 0 1 1 *", "* * * * * *"]
+    kind = np.zeros(R, np.int64)
+    kind[7::1800] = 1
+    karr, status = cron.parse_batch(kinds, threads=1)
+    assert not np.any(status)
+    a = np.ascontiguousarray(np.ctypeslib.as_array(karr)[kind])
+    arr = (karr._type_ * R).from_buffer(a)
+    rin = progression_rules(R, N)
+    t0 = synth.T0_2026 + 20 * DAY + 123
+    t1 = t0 + 3600
+    eng = Engine(0)
+    try:
+        sp = eng.upload_c(arr, R)
+        dr = eng.upload_rules(rin)
+        eng.set_node_order(_lib.NODE_ORDER_TIME)
+        E, _ = eng.expand_per_node_rules_device(sp, product_zone("UTC"), t0, t1, dr, _lib.EXCLUDE_NONE)
+        off, time, rule = eng.node_result(N, E)
+    finally:
+        eng.set_node_order(_lib.NODE_ORDER_RULE)
+        eng.close()
+    fire = np.nonzero(kind == 1)[0]
+    assert (fire >> 20).max() == 1 and (fire >> 20).min() == 0  # both blocks of 2^20 rules
+    exp_t = np.tile(np.arange(t0 + 1, t1 + 1, dtype=np.int64)[:, None], (1, len(fire))).ravel()
+    exp_r = np.tile(fire.astype(np.int32), t1 - t0)  # (time, rule) order: every second, rules ascending
+    for n in range(N):
+        a_, b_ = int(off[n]), int(off[n + 1])
+        assert b_ - a_ == len(exp_t) > 256 * 4096, n
+        assert np.array_equal(time[a_:b_], exp_t), n
+        assert np.array_equal(rule[a_:b_], exp_r), n
