@@ -234,11 +234,6 @@ struct cg_ctx {
   DBuf<int64_t> ts_base, ts_off, node_time2, ts_node_off;
   DBuf<int64_t> ts_start;  // per tile its first list position; [T] = the lists' end
   DBuf<int32_t> ts_hi;     // per tile the high rule bits (rule >> 20) all its events share
-  // time order by buckets: chunks per node, their base, first segments,
-  // per-(chunk, slab) counts and destinations, the two writer passes' tickets
-  DBuf<int32_t> ob_ccnt, ob_chunk, ob_cnt, ob_dest;
-  DBuf<int64_t> ob_cbase;
-  DBuf<uint32_t> ob_tickets;
   int64_t pn_t0 = 0, pn_t1 = 0;  // window of the last per-node result
   RulesStore rules;  // rule set of the host-array entry points (re-uploaded per call)
   int64_t pn_E = 0, pn_nnz = 0, pn_N = 0;
@@ -293,7 +288,6 @@ struct cg_ctx {
     rule_info.release();
     ts_cnt.release(); ts_tile_node.release(); ts_hist.release(); node_rule2.release();
     ts_start.release(); ts_hi.release();
-    ob_ccnt.release(); ob_chunk.release(); ob_cnt.release(); ob_dest.release(); ob_cbase.release(); ob_tickets.release();
     ts_base.release(); ts_off.release(); node_time2.release(); ts_node_off.release();
     mr_rb.release(); mr_tp.release(); mr_t.release(); mr_r.release();
     if (pn_res_host) (void)hipHostFree(pn_res_host);
@@ -367,13 +361,6 @@ struct TileCut {
 // rule) order (the sorts' ranks rest on lane-ordered LDS atomics; checked)
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
                         hipStream_t st, int in_mode, int64_t* err, const TileCut& cut = TileCut());
-// time order by buckets (cg_pernode.hip k_node_bucket; rule indices < 2^20):
-// the merges' buffers for N nodes, the merges over c->node_rule2's bucketed
-// words, the slab width (2^bits s) of a window of H s
-int order_bucket_buffers(cg_ctx* c, int32_t N, int64_t cap, hipStream_t st);
-int order_bucket_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st,
-                      int64_t* err);
-int order_slab_bits(int64_t H);
 constexpr const char* kOrderCheckMsg =
     "time-order pass: a sorted chunk came out of (time, rule) order (its LDS-atomic ranks were not in lane order)";
 // the mapped pinned per-node result words: [0] node events, [1] size error, [2] order check

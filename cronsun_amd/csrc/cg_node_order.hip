@@ -920,7 +920,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
                                                        int64_t e_lo, int64_t e_hi, unsigned* __restrict__ ticket,
                                                        int64_t* __restrict__ err, int sb,
                                                        const int64_t* __restrict__ ts_start,
-                                                       const int32_t* __restrict__ ts_hi, int bucket) {
+                                                       const int32_t* __restrict__ ts_hi) {
   constexpr int kThreads = 64 * NW, kChunk = kThreads * IT;
   constexpr int kMidChunk = 64 * kOtMidWaves * kOtItems, kMid2Chunk = 64 * kOtMid2Waves * kOtItems;
   __shared__ OtRank<NW, 256> s;
@@ -944,7 +944,7 @@ __global__ __launch_bounds__(64 * NW, PACK ? (DYN ? CG_OT_DENSE_WPE : CG_OT_MERG
   if (M == 0) continue;
   const int64_t e_n = node_off[n + 1] - lo_n;
   if (e_n < e_lo || e_n >= e_hi) continue;  // the other merge launch's node
-  if (M == 1 && !bucket) {  // one tile: already in order (bucketed lists: one unsorted "tile" per node)
+  if (M == 1) {  // one tile: already in order
     const uint32_t hi = HX ? uint32_t(ts_hi[ta]) << kOtRuleBits : 0u;
     for (int64_t p = threadIdx.x; p < e_n; p += kThreads) {
       const uint32_t w = uint32_t(rin[lo_n + p]);  // PIN: a packed word
@@ -1222,7 +1222,7 @@ int ot_slab_bits(int64_t H) { return H <= 2048 ? kOtSlabBits - 1 : kOtSlabBits; 
 // pack: the tiles hold packed words (rule indices < 2^20, or hx); hx: rule
 // indices past 2^20 (tiles cut where rule >> 20 changes, ts_hi)
 int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st, int64_t* err,
-               bool pack, bool pin, bool hx, int sb, bool bucket = false) {
+               bool pack, bool pin, bool hx, int sb) {
   const uint16_t* toff = reinterpret_cast<const uint16_t*>(c->node_time2.p);
   // [0] big, [1] mid, [2] the dense merge's node ticket, [3] mid2
   unsigned* big_n = reinterpret_cast<unsigned*>(c->ts_off.p + int64_t(N) * kOtSlabs);
@@ -1258,11 +1258,11 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
     hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtDenseWaves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
-                       dense_min, INT64_MAX, big_n + 2, err, sb, c->ts_start.p, c->ts_hi.p, int(bucket));
+                       dense_min, INT64_MAX, big_n + 2, err, sb, c->ts_start.p, c->ts_hi.p);
     hipLaunchKernelGGL(m4, dim3(unsigned(N)), dim3(64 * kOtMergeWaves), 0, st, toff, c->node_rule2.p, c->ts_base.p,
                        node_off, c->ts_hist.p, N, t0, slab_tab, c->node_time.p, c->node_rule.p, c->ts_off.p, big_n,
                        mid, big_n + 1, mid2, big_n + 3, int64_t(0), dense_min, nullptr, err, sb, c->ts_start.p,
-                       c->ts_hi.p, int(bucket));
+                       c->ts_hi.p);
     // k_ot_mid's queue is filled by the 4-wave merge only (the 8-wave merge's
     // chunk holds any slab of <= 8192 events).  Its blocks find no room
     // beside the dense merge (whose persistent grid holds every CU's VGPRs),
@@ -1345,29 +1345,6 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
   }
   return order_tail(c, node_off, N, t0, H, st, err, pack, pack, hx, sb);  // packed tiles: packed words in node_rule2
 }
-
-// The bucket path (cg_pernode.hip, order_buckets_enqueue): the buffers of
-// the merges (queues and slab tables, the per-node pre rows and one-tile-per-
-// node views) for N nodes, and the merges over the bucketed words in
-// c->node_rule2 (rule indices < 2^20).
-int order_bucket_buffers(cg_ctx* c, int32_t N, int64_t cap, hipStream_t st) {
-  const int64_t tab = 3 * int64_t(N) * kOtSlabs + 2 + int64_t(N) * kOtPre;
-  if (c->ts_base.cap < size_t(N + 1) || c->ts_tile_node.cap < size_t(N) || c->ts_hist.cap < size_t(int64_t(N) * kOtPre) ||
-      c->node_rule2.cap < size_t(cap) || c->ts_off.cap < size_t(tab) || c->ts_start.cap < size_t(N + 1) ||
-      c->ts_hi.cap < size_t(N))
-    HIPCHK(hipStreamSynchronize(st));  // growing frees the old buffers: earlier windows' kernels first
-  int rc;
-  if ((rc = c->ts_base.ensure(int64_t(N) + 1)) || (rc = c->ts_tile_node.ensure(N)) ||
-      (rc = c->ts_hist.ensure(int64_t(N) * kOtPre)) || (rc = c->node_rule2.ensure(cap)) || (rc = c->ts_off.ensure(tab)) ||
-      (rc = c->ts_start.ensure(int64_t(N) + 1)) || (rc = c->ts_hi.ensure(N)))
-    return rc;
-  return CG_OK;
-}
-int order_bucket_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_t H, hipStream_t st,
-                      int64_t* err) {
-  return order_tail(c, node_off, N, t0, H, st, err, true, true, false, ot_slab_bits(H), true);
-}
-int order_slab_bits(int64_t H) { return ot_slab_bits(H); }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {
   if (!c) return cg_fail(CG_EINVAL, "cg_node_result_order_by_time: null");

@@ -617,12 +617,6 @@ constexpr int kNodeGroups = CG_NODE_GROUPS < kTicketGroups ? CG_NODE_GROUPS : kT
 #ifndef CG_NODE_GRP_XCD
 #define CG_NODE_GRP_XCD 1
 #endif
-// time order of rule indices < 2^20 by slab buckets (k_node_bucket) instead
-// of the packed writer + tile sort
-#ifndef CG_ORDER_BUCKETS
-#define CG_ORDER_BUCKETS 0
-#endif
-constexpr bool kOrderBuckets = CG_ORDER_BUCKETS != 0;
 constexpr int kNodeMajorDefault = CG_NODE_MAJOR;
 constexpr int kNodeMajorOrdered = CG_NODE_MAJOR_ORDERED;  // the time-order writer (packed words / 16-bit offsets)
 
@@ -630,7 +624,7 @@ constexpr int kNodeMajorOrdered = CG_NODE_MAJOR_ORDERED;  // the time-order writ
 // output position order, 64-event blocks at a time: put(q, val, rv) for the
 // lanes whose position q (relative to the 64-aligned abase) is in the
 // segment -- the whole block, or the lanes inside the segment at its edges.
-// The body of k_node_write and of the time-order bucket writer.
+// The body of k_node_write (the bucket writer of commit 7beb946 shared it).
 //   runs   a block one record owns entirely (no record starts inside it) is
 //          stored straight from that record: a progression's fires are
 //          t0 + x + p * stride, so a run of such blocks costs two stores and
@@ -817,191 +811,6 @@ __global__ __launch_bounds__(256) void k_node_write(
       if (!(V & 8)) out_store<V>(orl + q, rv);
     };
     node_segment<V>(p0, nrec, q_lo, q_hi, tb, recs, t0, marks, tag, le, put);
-  }
-}
-
-// ---- time order by buckets (rule indices < 2^20, windows <= 4096 s) ----
-//
-// Each node's list is written straight into its slab buckets (slab =
-// (t - t0 - 1) >> sb, 64 per window) as packed words offset << 20 | rule,
-// every bucket in (time-slab, then rule-major) order, so one LDS sort per
-// slab run (the merges, reading one contiguous range) finishes the (time,
-// rule) order: 4 B written per event before the final 12 B, where the writer
-// + tile sort wrote and read the words twice.  The buckets' order comes from
-// chunks: runs of consecutive (node, band) segments of one node holding about
-// kObChunk events, each written by one wave in position order.
-//   k_ob_chunk_count / k_ob_chunks   chunks per node, and each chunk's first
-//                                    segment (chunk_seg[C] = N*K)
-//   k_node_bucket<0>                 per chunk its events per slab (the
-//                                    writer's generation, no stores)
-//   k_ob_scan                        per node, one wave (lane = slab): each
-//                                    chunk's first position in every bucket,
-//                                    and the node's slab offsets (pre row)
-//   k_node_bucket<1>                 the words into the buckets: per block a
-//                                    lane's rank in its slab = the LDS cursor
-//                                    it adds 1 to (lanes of one ds_add_rtn on
-//                                    one address are served in lane order,
-//                                    tools/lds_atomic_order.hip; the merges
-//                                    check the final order)
-constexpr int kObChunk = 8192;
-#ifndef CG_OB_NT
-#define CG_OB_NT 0
-#endif
-__global__ void k_ob_chunk_count(const int64_t* __restrict__ seg_pos, int32_t N, int32_t K, int64_t cap,
-                                 int32_t* __restrict__ cnt) {
-  const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (n >= N) return;
-  const int64_t* sp = seg_pos + n * K;
-  int32_t c = 0;
-  if (seg_pos[int64_t(N) * K] <= cap && sp[K] > sp[0]) {
-    int64_t acc = 0;
-    for (int32_t k = 0; k < K; k++) {
-      const int64_t e = sp[k + 1] - sp[k];
-      if (k == 0 || acc + e > kObChunk) {  // a new chunk (the first one, or this segment would overflow)
-        if (k > 0 && acc == 0) {  // an empty chunk so far: keep filling it
-          acc = e;
-          continue;
-        }
-        c++;
-        acc = e;
-      } else {
-        acc += e;
-      }
-    }
-  }
-  cnt[n] = c;
-}
-__global__ void k_ob_chunks(const int64_t* __restrict__ seg_pos, int32_t N, int32_t K,
-                            const int64_t* __restrict__ chunk_base, int32_t* __restrict__ chunk_seg) {
-  const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (n >= N) return;
-  int64_t c = chunk_base[n];
-  if (n == N - 1) chunk_seg[chunk_base[N]] = N * K;  // the last chunk's end
-  if (chunk_base[n + 1] == c) return;
-  const int64_t* sp = seg_pos + n * K;
-  int64_t acc = 0;
-  for (int32_t k = 0; k < K; k++) {
-    const int64_t e = sp[k + 1] - sp[k];
-    if (k == 0 || acc + e > kObChunk) {
-      if (k > 0 && acc == 0) {
-        acc = e;
-        continue;
-      }
-      chunk_seg[c++] = int32_t(n * K + k);
-      acc = e;
-    } else {
-      acc += e;
-    }
-  }
-}
-
-// MODE 0: per chunk its events per slab -> cnt[c * 64 + slab]; MODE 1: the
-// packed words of chunk c into out_words[node start + dest[c * 64 + slab] +
-// rank] (dest node-relative, k_ob_scan).  One chunk per wave task, by ticket.
-template <int MODE>
-__global__ __launch_bounds__(256) void k_node_bucket(
-    const int64_t* __restrict__ seg_pair, const int64_t* __restrict__ seg_pos,
-    const int32_t* __restrict__ seg_nrec, const PairRec* __restrict__ recs, int64_t t0,
-    const int64_t* __restrict__ rule_off, const int64_t* __restrict__ times, int32_t N, int32_t K,
-    int32_t B, int64_t cap, const int32_t* __restrict__ chunk_seg, const int64_t* __restrict__ n_chunks,
-    uint32_t* __restrict__ tickets, int32_t* __restrict__ cnt, const int32_t* __restrict__ dest,
-    int32_t* __restrict__ out_words, int sb) {
-  __shared__ uint32_t marks_all[4][128];
-  __shared__ int32_t cur_all[4][64];  // per wave: the chunk's running position in each bucket
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* marks = marks_all[wave];
-  int32_t* cur = cur_all[wave];
-  marks[lane] = 0u;
-  uint32_t tag = 0;
-  const int64_t NK = int64_t(N) * K;
-  if (seg_pos[NK] > cap) return;
-  const int64_t C = *n_chunks;
-  const uint64_t le = (2ull << lane) - 1ull;
-  const int ng = int(gridDim.x) < kNodeGroups ? int(gridDim.x) : kNodeGroups;
-  const int grp = int(gridDim.x >= 8u * unsigned(ng) ? (blockIdx.x >> 3) % unsigned(ng) : blockIdx.x % unsigned(ng));
-  auto take = [&]() -> int64_t {
-    unsigned int t = 0;
-    if (lane == 0) t = atomicAdd(tickets + grp * kTicketStride, 1u);
-    return grp + int64_t(ng) * int64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(t))));
-  };
-  for (int64_t c = take(); c < C; c = take()) {
-    const int32_t s0 = chunk_seg[c], s1 = chunk_seg[c + 1];
-    const int64_t n = s0 / K;
-    const int64_t node_start = seg_pos[n * K];
-    cur[lane] = MODE == 0 ? 0 : dest[c * 64 + lane];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    int32_t* __restrict__ ow = out_words + node_start;
-    for (int32_t s = s0; s < s1; s++) {
-      const int64_t o0 = seg_pos[s], o1 = seg_pos[s + 1];
-      if (o0 == o1) continue;
-      const int64_t p0 = seg_pair[s];
-      const int32_t nrec = seg_nrec[s];
-      const int64_t band_lo = rule_off[int64_t(s - n * K) * B];
-      const int64_t abase = o0 & ~int64_t(63);
-      const int32_t q_lo = int32_t(o0 - abase), q_hi = q_lo + int32_t(o1 - o0);
-      auto put = [&](int32_t, int64_t val, int32_t rv) {
-        const uint32_t off = uint32_t(val - t0 - 1);
-        const int32_t pos = atomicAdd(cur + (off >> sb), 1);
-        // plain stores: a bucket's lines fill in pieces across blocks and are
-        // combined in L2 before they reach HBM (nontemporal stores of the
-        // pieces wrote partial lines: 16.9 ms instead of ~2 on pernode)
-        if constexpr (MODE == 1) {
-#if CG_OB_NT
-          __builtin_nontemporal_store(int32_t((off << 20) | uint32_t(rv)), ow + pos);
-#else
-          ow[pos] = int32_t((off << 20) | uint32_t(rv));
-#endif
-        }
-      };
-      node_segment<0>(p0, nrec, q_lo, q_hi, times + band_lo, recs, t0, marks, tag, le, put);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (MODE == 0) cnt[c * 64 + lane] = cur[lane];
-  }
-}
-
-// per node, one wave (lane = slab): dest[c * 64 + s] = the node-relative
-// first position of chunk c's events of slab s (the buckets in slab order,
-// the chunks in order inside each), pre[n * 65 + s] = the slab offsets
-__global__ __launch_bounds__(64) void k_ob_scan(const int32_t* __restrict__ cnt, const int64_t* __restrict__ chunk_base,
-                                                int32_t N, int32_t* __restrict__ dest, int32_t* __restrict__ pre) {
-  const int32_t n = blockIdx.x;
-  if (n >= N) return;
-  const int lane = threadIdx.x;
-  const int64_t c0 = chunk_base[n], c1 = chunk_base[n + 1];
-  int32_t run = 0;
-  for (int64_t c = c0; c < c1; c++) {
-    const int32_t v = cnt[c * 64 + lane];
-    dest[c * 64 + lane] = run;
-    run += v;
-  }
-  int32_t inc = run;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
-  const int32_t base = inc - run;
-  for (int64_t c = c0; c < c1; c++) dest[c * 64 + lane] += base;
-  pre[int64_t(n) * 65 + lane] = base;
-  if (lane == 63) pre[int64_t(n) * 65 + 64] = inc;
-}
-
-// the merges' view of bucketed lists: one "tile" per node (tile_base[n] = n,
-// its first position node_off[n], rule >> 20 = 0)
-__global__ void k_ob_tiles(const int64_t* __restrict__ node_off, int32_t N, int64_t cap, int64_t* __restrict__ tile_base,
-                           int64_t* __restrict__ ts_start, int32_t* __restrict__ ts_hi, int32_t* __restrict__ tile_node) {
-  const int64_t n = blockIdx.x * int64_t(blockDim.x) + threadIdx.x;
-  if (n > N) return;
-  tile_base[n] = node_off[N] > cap ? 0 : n;  // past the capacity: no node has a tile (nothing was written)
-  ts_start[n] = node_off[n];
-  if (n < N) {
-    ts_hi[n] = 0;
-    tile_node[n] = int32_t(n);
   }
 }
 
@@ -1193,59 +1002,6 @@ int gridn(int64_t n, int threads, int cap) {
   int64_t b = (n + threads - 1) / threads;
   if (b < 1) b = 1;
   return int(std::min<int64_t>(b, cap));
-}
-
-// Time order by buckets (k_node_bucket, above): the window's (node, band)
-// segments and records -> every node's list in (time, rule) order in
-// c->node_time / c->node_rule, enqueued on st without a host sync (buffers
-// sized from the output capacity cap; chunk counts and grids are upper bounds
-// trimmed on the device).  Rule indices < 2^20; windows <= 4096 s.
-struct BucketArgs {
-  const int64_t *seg_pair, *seg_pos;
-  const int32_t* seg_nrec;
-  const PairRec* recs;
-  const int64_t *rule_off, *times, *node_off;
-  int32_t N, K, B;
-  int64_t cap, t0, H;
-  int blocks;  // the writer passes' persistent grid
-};
-int order_buckets_enqueue(cg_ctx* c, const BucketArgs& a, hipStream_t st, int64_t* err) {
-  if (a.N == 0 || a.cap == 0) return CG_OK;
-  const int32_t N = a.N;
-  const int64_t Cmax = 2 * (a.cap / kObChunk) + N + 1;
-  if (c->ob_ccnt.cap < size_t(N) || c->ob_cbase.cap < size_t(N + 1) || c->ob_chunk.cap < size_t(Cmax + 1) ||
-      c->ob_cnt.cap < size_t(Cmax * 64) || c->ob_dest.cap < size_t(Cmax * 64) || c->scan_tmp.cap < scan_temp_bytes(N))
-    HIPCHK(hipStreamSynchronize(st));  // growing frees the old buffers: earlier windows' kernels first
-  int rc;
-  if ((rc = c->ob_ccnt.ensure(N)) || (rc = c->ob_cbase.ensure(int64_t(N) + 1)) || (rc = c->ob_chunk.ensure(Cmax + 1)) ||
-      (rc = c->ob_cnt.ensure(Cmax * 64)) || (rc = c->ob_dest.ensure(Cmax * 64)) ||
-      (rc = c->ob_tickets.ensure(2 * kTicketGroups * kTicketStride)) ||
-      (rc = c->scan_tmp.ensure(std::max(c->scan_tmp.cap, scan_temp_bytes(N)))) ||
-      (rc = order_bucket_buffers(c, N, a.cap, st)))
-    return rc;
-  const int sb = order_slab_bits(a.H);
-  uint32_t* tk0 = c->ob_tickets.p;
-  uint32_t* tk1 = tk0 + kTicketGroups * kTicketStride;
-  HIPCHK(hipMemsetAsync(tk0, 0, 2 * kTicketGroups * kTicketStride * 4, st));
-  hipLaunchKernelGGL(k_ob_chunk_count, dim3(gridn(N, 256, 1 << 30)), dim3(256), 0, st, a.seg_pos, N, a.K, a.cap,
-                     c->ob_ccnt.p);
-  launch_scan(c->ob_ccnt.p, c->ob_cbase.p, N, c->scan_tmp.p, st);
-  hipLaunchKernelGGL(k_ob_chunks, dim3(gridn(N, 256, 1 << 30)), dim3(256), 0, st, a.seg_pos, N, a.K, c->ob_cbase.p,
-                     c->ob_chunk.p);
-  const int64_t* n_chunks = c->ob_cbase.p + N;
-  const dim3 grid(unsigned(std::max(1, a.blocks))), block(256);
-  hipLaunchKernelGGL(k_node_bucket<0>, grid, block, 0, st, a.seg_pair, a.seg_pos, a.seg_nrec, a.recs, a.t0, a.rule_off,
-                     a.times, N, a.K, a.B, a.cap, c->ob_chunk.p, n_chunks, tk0, c->ob_cnt.p, c->ob_dest.p,
-                     c->node_rule2.p, sb);
-  hipLaunchKernelGGL(k_ob_scan, dim3(unsigned(N)), dim3(64), 0, st, c->ob_cnt.p, c->ob_cbase.p, N, c->ob_dest.p,
-                     c->ts_hist.p);
-  hipLaunchKernelGGL(k_node_bucket<1>, grid, block, 0, st, a.seg_pair, a.seg_pos, a.seg_nrec, a.recs, a.t0, a.rule_off,
-                     a.times, N, a.K, a.B, a.cap, c->ob_chunk.p, n_chunks, tk1, c->ob_cnt.p, c->ob_dest.p,
-                     c->node_rule2.p, sb);
-  hipLaunchKernelGGL(k_ob_tiles, dim3(gridn(int64_t(N) + 1, 256, 1 << 30)), dim3(256), 0, st, a.node_off, N, a.cap,
-                     c->ts_base.p, c->ts_start.p, c->ts_hi.p, c->ts_tile_node.p);
-  if ((rc = cg_hip_check(hipGetLastError(), "time-order buckets"))) return rc;
-  return order_bucket_tail(c, a.node_off, N, a.t0, a.H, st, err);
 }
 
 template <class T>
@@ -1556,16 +1312,11 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   const bool off16 = c->node_order == CG_NODE_ORDER_TIME && t1 - t0 <= 4096 && variant == 0 && !order_lsd_only();
   // packed words (offset << 20 | rule) when every rule index fits 20 bits
   const int in_mode = !off16 ? kInTimes : (pn_pack_ok(R) ? kInPacked : kIn16);
-  // rule indices < 2^20: the lists go straight into slab buckets (the bucket
-  // writer and the merges, after the window's size is known)
-  const bool bucket = kOrderBuckets && in_mode == kInPacked && R <= (int64_t(1) << 20);
   c->pn_res_host[2] = 0;
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
-    if (bucket) {
-      // nothing written here: the buckets below, once En is known
-    } else if (NK > 0 && cap > 0 && off16) {
+    if (NK > 0 && cap > 0 && off16) {
       if (in_mode == kInPacked)
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
                            dim3(256), 0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,
@@ -1596,11 +1347,6 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     if (c->pn_res_host[1] != 0)
       return cg_fail(CG_ERANGE, "per-node output: " + std::to_string(B) + " consecutive rules fire more than 2^30 "
                                 "times in this window (the writer's 32-bit band indices; narrow the time window)");
-    if (bucket) {
-      if ((rc = c->node_time.ensure(std::max<int64_t>(En, 1))) || (rc = c->node_rule.ensure(std::max<int64_t>(En, 1))))
-        return rc;
-      break;
-    }
     if (En <= cap) break;
     // grow the output, reset the tickets the first launch consumed, rerun
     if ((rc = c->node_time.ensure(En)) || (rc = c->node_rule.ensure(En))) return rc;
@@ -1620,24 +1366,6 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   c->pn_cache_mode = mode;
   *n_events = En;
   *nnz_out = nnz;
-  if (bucket) {  // the bucket writer + the merges; if they fail nothing is readable
-    const BucketArgs ba{c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, c->offsets.p, c->times.p, c->node_off.p,
-                        N, K, B, En, t0, t1 - t0, nw_blocks};
-    (void)hipEventRecord(c->pev[0], st);
-    rc = order_buckets_enqueue(c, ba, st, c->pn_res_dev + 2);
-    (void)hipEventRecord(c->pev[1], st);
-    if (!rc) rc = cg_hip_check(hipStreamSynchronize(st), "sync");
-    if (!rc && c->pn_res_host[2]) rc = cg_fail(CG_EHIP, kOrderCheckMsg);
-    if (rc) {
-      c->pn_E = 0;
-      c->pn_valid = false;
-      *n_events = 0;
-      return rc;
-    }
-    (void)hipEventElapsedTime(&c->kt[12], c->pev[0], c->pev[1]);
-    c->pn_time_ordered = true;
-    return CG_OK;
-  }
   // (time, rule) order: the tile sort + merge (or, past 4096 s, the LSD
   // passes) after the writer; if it fails nothing is readable (the lists may
   // hold the writer's 16-bit offsets)
@@ -1839,11 +1567,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     // wave slots beside this writer instead of waiting for it to retire
     static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-    if (timed && kOrderBuckets && R <= (int64_t(1) << 20)) {  // bucket writer + merges on the same stream
-      const BucketArgs ba{c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, a.rm.offsets.p, a.times.p, a.node_off.p,
-                          N, K, B, node_cap, t0, t1 - t0, nw_blocks};
-      if ((rc = order_buckets_enqueue(c, ba, st, a.res_dev + 2))) return rc;
-    } else if (timed) {  // packed words (or 16-bit offsets), then the tile sort + merge on the same stream
+    if (timed) {  // packed words (or 16-bit offsets), then the tile sort + merge on the same stream
       const int in_mode = pn_pack_ok(R) ? kInPacked : kIn16;
       if (in_mode == kInPacked)
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
