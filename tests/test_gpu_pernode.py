@@ -669,3 +669,56 @@ def test_per_node_time_ordered_over_2_20_rules_big_slabs():
         assert b_ - a_ == len(exp_t) > 256 * 4096, n
         assert np.array_equal(time[a_:b_], exp_t), n
         assert np.array_equal(rule[a_:b_], exp_r), n
+
+
+@pytest.mark.parametrize("seed,window", [(1, 600), (2, 1800), (3, 3600)])
+def test_time_order_packed_high_bits_equals_unpacked_pass(seed, window):
+    """Differential check of the packed time order past 2^20 rules (tiles cut
+    where rule >> 20 changes, the merges rebuild the rule from the tile) against
+    the independent unpacked path (rule-major int64 lists, then
+    cg_node_result_order_by_time: 16-bit offsets + LDS rule arrays), on every
+    node's whole list: a random count of rules between 2^20 and 2^21 (the
+    config-2 mix, tiled), 37 nodes, 10-min / 30-min / 1-h windows (16-, 32-
+    and 64-s slabs)."""
+    from cronsun_amd.engine import Engine
+    rng = np.random.default_rng(seed)
+    R, N = (1 << 20) + int(rng.integers(1, 1 << 20)), 37
+    base = synth.spec_mix(50_000, seed=100 + seed, mix=synth.MIX_CONFIG2)
+    barr, status = cron.parse_batch(base, threads=16)
+    assert not np.any(status)
+    pick = rng.integers(0, len(base), R)  # rule r = base[pick[r]]
+    a = np.ascontiguousarray(np.ctypeslib.as_array(barr)[pick])
+    arr = (barr._type_ * R).from_buffer(a)
+    rin = progression_rules(R, N)
+    t0 = synth.T0_2026 + int(rng.integers(0, 300)) * DAY + int(rng.integers(0, 86400))
+    eng = Engine(0)
+    try:
+        sp = eng.upload_c(arr, R)
+        dr = eng.upload_rules(rin)
+        eng.set_node_order(_lib.NODE_ORDER_TIME)
+        E1, _ = eng.expand_per_node_rules_device(sp, product_zone("UTC"), t0, t0 + window, dr, _lib.EXCLUDE_NONE)
+        got = eng.node_result(N, E1)
+        eng.set_node_order(_lib.NODE_ORDER_RULE)
+        E2, _ = eng.expand_per_node_rules_device(sp, product_zone("UTC"), t0, t0 + window, dr, _lib.EXCLUDE_NONE)
+        eng.node_order_by_time()
+        ref = eng.node_result(N, E2)
+    finally:
+        eng.set_node_order(_lib.NODE_ORDER_RULE)
+        eng.close()
+    assert E1 == E2 > 1_000_000
+    for x, y in zip(got, ref):
+        assert np.array_equal(x, y)
+    # and two nodes against the oracle's lists sorted by (time, rule)
+    off, time, rule = got
+    parsed = [O.parse(sp_)[0] for sp_ in base]
+    r_all = np.arange(R)
+    for n in (0, 19):
+        rules_n = r_all[(r_all % N == n) | ((7 * r_all + 1) % N == n)]
+        oarr = O.sched_array([parsed[i] for i in pick[rules_n].tolist()])
+        eo, et = O.expand_batch(oarr, t0, t0 + window, oracle_zone("UTC"), threads=16)
+        exp_t, exp_p = O.node_list(eo, et, list(range(len(rules_n))))
+        exp_r = rules_n[exp_p]
+        order = np.lexsort((exp_r, exp_t))
+        a_, b_ = int(off[n]), int(off[n + 1])
+        assert np.array_equal(time[a_:b_], exp_t[order]), n
+        assert np.array_equal(rule[a_:b_], exp_r[order]), n
