@@ -134,7 +134,6 @@ struct PnAsyncSet {
   DBuf<PairRec> recs;
   DBuf<uint32_t> tickets;
   DBuf<char> seg_tmp;
-  DBuf<uint16_t> slab_grid;  // the slab writer's grid rows (k_rule_info)
   int64_t* res_host = nullptr;  // {En, error}: mapped pinned, written by the records / node offsets
   int64_t* res_dev = nullptr;
   hipEvent_t side_done = nullptr, written = nullptr, nw0 = nullptr, nw1 = nullptr;
@@ -145,7 +144,7 @@ struct PnAsyncSet {
   void release() {
     rm.release();
     times.release(); seg_cnt.release(); seg_pos.release(); node_off.release(); seg_nrec.release();
-    rule_info.release(); recs.release(); tickets.release(); seg_tmp.release(); slab_grid.release();
+    rule_info.release(); recs.release(); tickets.release(); seg_tmp.release();
     if (res_host) (void)hipHostFree(res_host);
     res_host = res_dev = nullptr;
     for (hipEvent_t* e : {&side_done, &written, &nw0, &nw1})
@@ -228,7 +227,6 @@ struct cg_ctx {
   DBuf<int32_t> seg_nrec;
   DBuf<PairRec> recs;  // per-call segment records (k_seg_records)
   DBuf<RuleInfo> rule_info;  // per-call, per rule (k_rule_info)
-  DBuf<uint16_t> slab_grid;  // per-call grid rows of the slab writer (k_rule_info)
   DBuf<uint32_t> pn_tickets;
   // time-order pass (cg_node_order.hip): node-aligned tiles, per-pass
   // histograms/offsets, and the second buffers of the ping-pong
@@ -363,33 +361,6 @@ struct TileCut {
 // rule) order (the sorts' ranks rest on lane-ordered LDS atomics; checked)
 int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t cap, int64_t t0, int64_t H,
                         hipStream_t st, int in_mode, int64_t* err, const TileCut& cut = TileCut());
-// The (time, rule)-ordered lists written straight from the segment records
-// (k_node_slab, cg_node_order.hip) instead of the packed writer + tile sort +
-// merge: windows <= 4096 s, rule indices < 2^24, at most 256 bands, and (unless
-// CG_ORDER_SLAB=1) nodes of at most CG_SLAB_PAIRS_PER_NODE pairs on average.
-// ticket: a zeroed device word (the writer's first ticket); err as below.
-// grid rows: per rule (R x G uint16, G = slab_grid_points(H)), its fires
-// before each point min(c * kSlGrid, H), written by k_rule_info for the rules
-// whose fires are not a progression (the others' rows are not written)
-constexpr int kSlGrid = 16;
-inline int32_t slab_grid_points(int64_t H) { return int32_t((H + kSlGrid - 1) / kSlGrid + 1); }
-struct SlabIn {
-  const int64_t* seg_pair;
-  const int32_t* seg_nrec;
-  const int64_t* seg_pos;
-  const PairRec* recs;
-  const int64_t* rule_off;
-  const int64_t* times;
-  int64_t t0, H, cap;
-  int32_t N, K, B;
-  uint32_t* ticket;
-  int64_t* err;
-  int64_t* out_time;
-  int32_t* out_rule;
-  const uint16_t* grid;
-};
-bool slab_order_ok(int64_t R, int64_t H, int32_t K, int64_t nnz, int32_t N);
-int slab_order_enqueue(cg_ctx* c, hipStream_t st, const SlabIn& in);
 constexpr const char* kOrderCheckMsg =
     "time-order pass: a sorted chunk came out of (time, rule) order (its LDS-atomic ranks were not in lane order)";
 // the mapped pinned per-node result words: [0] node events, [1] size error, [2] order check

@@ -1169,344 +1169,6 @@ __global__ __launch_bounds__(256) void k_ot_big(const uint16_t* __restrict__ tin
   }
 }
 
-// ---- windows <= 4096 s, rule indices < 2^24: the lists in (time, rule)
-// order straight from the segment records (k_node_slab)
-//
-// The writer + tile sort + merge above move every event three times (4 B
-// packed word out, 4 B in and out of the tile sort, 4 B in and 12 B out of the
-// merge).  Here one workgroup per node (nodes by ticket) walks the node's
-// window in slabs of at most 256 seconds holding at most kSlCap events, and
-// for each slab
-//   count   every record's fires inside [A, B): a progression's by one
-//           division per bound, other records' by a binary search of their
-//           fire list (the rule-major times); a slab over the cap is halved
-//           (down to one second, which is written in rule order directly)
-//   expand  the records' fires of the slab into LDS in rule order, a record
-//           column of a wave at a time (owner by a 6-step search over the
-//           wave's prefix), as packed words (second - A) << 24 | rule
-//   sort    one stable 8-bit LDS counting pass (ot_sort) by the second
-//   store   the slab's 12 B per event, coalesced, with the order check
-// so each event is written once (12 B) and read never; the records (16 B per
-// non-empty pair) are re-read per slab from L2.  Records are held in
-// registers a batch of kSlBatch at a time (thread t: records t*RPT ..
-// t*RPT+RPT-1, so a block scan of the threads' sums gives every record's
-// place in rule order).
-constexpr int kSlWaves = 8;
-#ifndef CG_SLAB_ITEMS
-#define CG_SLAB_ITEMS 16
-#endif
-constexpr int kSlItems = CG_SLAB_ITEMS;  // events per thread of a slab
-#ifndef CG_SLAB_RPT
-#define CG_SLAB_RPT 4
-#endif
-constexpr int kSlRpt = CG_SLAB_RPT;  // records per thread of a batch
-constexpr int kSlMaxSegs = 256;      // (node, band) segments per node held in LDS
-constexpr int kSlRuleBits = 24;
-constexpr int kSlMaxWidth = 256;     // seconds per slab: the sort's 8-bit digit
-#ifndef CG_SLAB_NOSEARCH
-#define CG_SLAB_NOSEARCH 0
-#endif
-#ifndef CG_SLAB_WPE
-#define CG_SLAB_WPE 4  // min waves per SIMD: two 8-wave blocks per CU
-#endif
-#ifndef CG_SLAB_PAIRS_PER_NODE
-#define CG_SLAB_PAIRS_PER_NODE 32768
-#endif
-
-struct SlabArgs {
-  const int64_t* seg_pair;
-  const int32_t* seg_nrec;
-  const int64_t* seg_pos;
-  const PairRec* recs;
-  const int64_t* rule_off;
-  const int64_t* times;
-  int64_t t0, cap;
-  int32_t N, K, B, H;
-  uint32_t* ticket;
-  int64_t* err;
-  int64_t* out_time;
-  int32_t* out_rule;
-  const uint16_t* grid;  // rows of slab_grid_points(H) per rule (k_rule_info)
-  int32_t G;
-};
-
-// A record's fires in the window: fire i at offset (t - t0 - 1) v + i * st
-// (st != 0), or times[v + i] (st == 0)
-struct SlRec {
-  int32_t rule, st, cnt;
-  int64_t v;
-};
-
-// ceil(num / d) for 0 < num < 2^14, 1 <= d < num (f32 quotient, corrected)
-__device__ __forceinline__ int32_t sl_ceil_div(int32_t num, int32_t d) {
-  int32_t q = int32_t(ceilf(float(num) / float(d)));
-  if (q * d < num) q++;
-  else if ((q - 1) * d >= num) q--;
-  return q;
-}
-
-// the record's fires at offsets < T (T in [0, H])
-__device__ __forceinline__ int32_t sl_before(const SlRec& r, const int64_t* __restrict__ times, int64_t tb,
-                                             int32_t T) {
-  if (r.cnt <= 0) return 0;
-  if (r.st != 0) {
-    const int32_t num = T - int32_t(r.v);
-    if (num <= 0) return 0;
-    const int32_t q = r.st >= num ? 1 : sl_ceil_div(num, r.st);
-    return q < r.cnt ? q : r.cnt;
-  }
-#if CG_SLAB_NOSEARCH  // diagnostic timing only (wrong lists): no fire-list search
-  return int32_t(int64_t(r.cnt) * T / 4096);
-#endif
-  int32_t lo = 0, hi = r.cnt;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (times[r.v + mid] - tb < T) lo = mid + 1;
-    else hi = mid;
-  }
-  return lo;
-}
-
-template <int NW>
-__device__ __forceinline__ int32_t sl_block_excl(int32_t v, int32_t* red, int32_t* total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int32_t inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int32_t y = __shfl_up(inc, o, 64);
-    if (lane >= o) inc += y;
-  }
-  if (lane == 63) red[w] = inc;
-  __syncthreads();
-  int32_t base = 0, all = 0;
-#pragma unroll
-  for (int ww = 0; ww < NW; ww++) {
-    const int32_t x = red[ww];
-    base += ww < w ? x : 0;
-    all += x;
-  }
-  __syncthreads();
-  *total = all;
-  return base + inc - v;
-}
-
-template <int NW, int IT, int RPT>
-__global__ __launch_bounds__(64 * NW, CG_SLAB_WPE) void k_node_slab(SlabArgs a) {
-  constexpr int NT = 64 * NW, CAP = NT * IT, BATCH = NT * RPT;
-  __shared__ OtRank<NW, 256> s;
-  __shared__ uint32_t buf[CAP];  // the slab in rule order, then (ot_sort) in (second, rule) order
-  __shared__ int64_t s_pr[kSlMaxSegs], s_bl[kSlMaxSegs];
-  __shared__ int32_t s_rp[kSlMaxSegs + 1], s_nr[kSlMaxSegs], s_sz[kSlMaxSegs];
-  __shared__ int32_t s_red[NW];
-  __shared__ int32_t s_node;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int32_t K = a.K, H = a.H;
-  if (a.seg_pos[int64_t(a.N) * K] > a.cap) return;  // output too small: the host grows it and relaunches
-  const int64_t tb = a.t0 + 1;
-  const int64_t* __restrict__ times = a.times;
-  bool bad = false;
-  for (;;) {
-    __syncthreads();  // the previous node's LDS reads are done
-    if (tid == 0) s_node = int32_t(atomicAdd(a.ticket, 1u));
-    __syncthreads();
-    const int32_t n = s_node;
-    if (n >= a.N) break;
-    const int64_t s0 = int64_t(n) * K;
-    const int64_t o_lo = a.seg_pos[s0], L = a.seg_pos[s0 + K] - o_lo;
-    if (L == 0) continue;
-    if (L > INT32_MAX) {
-      bad = true;
-      continue;
-    }
-    for (int k = tid; k < K; k += NT) {
-      s_pr[k] = a.seg_pair[s0 + k];
-      s_nr[k] = a.seg_nrec[s0 + k];
-      s_sz[k] = int32_t(a.seg_pos[s0 + k + 1] - a.seg_pos[s0 + k]);
-      s_bl[k] = a.rule_off[int64_t(k) * a.B];
-    }
-    __syncthreads();
-    if (tid == 0) {
-      int32_t acc = 0;
-      for (int k = 0; k < K; k++) {
-        s_rp[k] = acc;
-        acc += s_nr[k];
-      }
-      s_rp[K] = acc;
-    }
-    __syncthreads();
-    const int32_t nR = s_rp[K];
-    const int nb = (nR + BATCH - 1) / BATCH;
-    int64_t* __restrict__ ot = a.out_time + o_lo;
-    int32_t* __restrict__ orl = a.out_rule + o_lo;
-    // record r of the node (r < nR; else an empty view)
-    auto load = [&](int32_t r, SlRec& o) {
-      o.cnt = 0;
-      o.rule = 0;
-      o.st = 1;
-      o.v = 0;
-      if (r >= nR) return;
-      int lo = 0, hi = K - 1;  // the last segment whose first record is <= r (empty segments share it)
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_rp[mid] <= r) lo = mid;
-        else hi = mid - 1;
-      }
-      const int32_t li = r - s_rp[lo];
-      const int64_t slot = s_pr[lo] + li;
-      const PairRec pr = a.recs[slot];
-      const int32_t nd = li + 1 < s_nr[lo] ? a.recs[slot + 1].dst : s_sz[lo];
-      o.rule = pr.rule;
-      o.st = pr.st;
-      o.cnt = nd - pr.dst;
-      o.v = pr.st != 0 ? int64_t(pr.x) + int64_t(pr.dst) * pr.st - 1 : s_bl[lo] + int64_t(pr.x) + pr.dst;
-    };
-    SlRec rc[RPT];
-    int32_t ia[RPT], cc[RPT];
-    auto load_batch = [&](int b) {
-#pragma unroll
-      for (int i = 0; i < RPT; i++) load(b * BATCH + tid * RPT + i, rc[i]);
-    };
-    // ia, cc: each record's fires before A and inside [A, B_): progressions
-    // by division; the others from their rule's grid row when A and B_ are
-    // grid points (every slab of >= kSlGrid s), else by binary search
-    auto counts = [&](int32_t A_, int32_t B_) {
-      const bool ga = A_ % kSlGrid == 0 || A_ == H, gb = B_ % kSlGrid == 0 || B_ == H;
-      const int32_t ca = A_ == H ? a.G - 1 : A_ / kSlGrid, cb = B_ == H ? a.G - 1 : B_ / kSlGrid;
-      uint32_t xa[RPT], xb[RPT];
-#pragma unroll
-      for (int i = 0; i < RPT; i++) {  // every lane loads (row 0 for progressions): all in flight at once
-        const int64_t row = rc[i].st == 0 ? int64_t(rc[i].rule) * a.G : 0;
-        xa[i] = a.grid[row + ca];
-        xb[i] = a.grid[row + cb];
-      }
-#pragma unroll
-      for (int i = 0; i < RPT; i++) {
-        int32_t x, y;
-        if (rc[i].st != 0 || rc[i].cnt == 0) {
-          x = sl_before(rc[i], times, tb, A_);
-          y = sl_before(rc[i], times, tb, B_);
-        } else {
-          x = ga ? int32_t(xa[i]) : sl_before(rc[i], times, tb, A_);
-          y = gb ? int32_t(xb[i]) : sl_before(rc[i], times, tb, B_);
-        }
-        ia[i] = x;
-        cc[i] = y - x;
-      }
-    };
-    // slab width: a power of two <= 256 s aiming at ~60 % of the cap
-    int32_t wdt = 1;
-    {
-      const int64_t want = int64_t(CAP) * 3 / 5 * H / L;
-      while (wdt < kSlMaxWidth && int64_t(wdt) * 2 <= want) wdt <<= 1;
-    }
-    int32_t A = 0, S = 0;
-    // slab ends on the grid (a multiple of kSlGrid, or H) unless narrower
-    auto slab_end = [&](int32_t w_) {
-      int32_t e = A + w_;
-      if (w_ >= kSlGrid) e -= e % kSlGrid;
-      if (e <= A) e = A + 1;
-      return e < H ? e : H;
-    };
-    while (A < H && S < L) {
-      int32_t Bn = slab_end(wdt);
-      int32_t nj = 0;
-      for (;;) {  // count; halve a slab over the cap (down to one second)
-        int32_t tsum = 0;
-        for (int b = 0; b < nb; b++) {
-          load_batch(b);
-          counts(A, Bn);
-#pragma unroll
-          for (int i = 0; i < RPT; i++) tsum += cc[i];
-        }
-        int32_t tot;
-        (void)sl_block_excl<NW>(tsum, s_red, &tot);
-        nj = tot;
-        if (nj <= CAP || Bn - A == 1) break;
-        wdt = (Bn - A) >> 1;
-        Bn = slab_end(wdt);
-      }
-      const bool heavy = nj > CAP;  // one second: rule order is its final order
-      int32_t done = 0;             // events of the earlier batches
-      for (int b = 0; b < nb; b++) {
-        if (nb > 1) {
-          load_batch(b);
-          counts(A, Bn);
-        }
-        int32_t tsum = 0;
-#pragma unroll
-        for (int i = 0; i < RPT; i++) tsum += cc[i];
-        int32_t btot;
-        int32_t P = done + sl_block_excl<NW>(tsum, s_red, &btot);
-        done += btot;
-#pragma unroll
-        for (int i = 0; i < RPT; i++) {  // record column i of every lane, the wave's lanes sharing the fires
-          const int32_t c = cc[i];
-          int32_t inc = c;
-#pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
-          }
-          const int32_t T = __shfl(inc, 63, 64);
-          const int32_t pre = inc - c;
-          const int32_t dbase = P - pre, ibase = ia[i] - pre;
-          P += c;
-          for (int32_t f0 = 0; f0 < T; f0 += 64) {
-            const int32_t f = f0 + lane;
-            int j = 0;  // the lane holding fire f: the last lane whose prefix is <= f
-#pragma unroll
-            for (int st = 32; st; st >>= 1) {
-              const int32_t pj = __shfl(pre, j + st, 64);
-              if (pj <= f) j += st;
-            }
-            const int32_t db = __shfl(dbase, j, 64), ib = __shfl(ibase, j, 64);
-            const int32_t sj = __shfl(rc[i].st, j, 64), rj = __shfl(rc[i].rule, j, 64);
-            const int64_t vj = int64_t((uint64_t(uint32_t(__shfl(int(uint64_t(rc[i].v) >> 32), j, 64))) << 32) |
-                                       uint32_t(__shfl(int(uint32_t(uint64_t(rc[i].v))), j, 64)));
-            const int32_t fi = ib + f;
-            int32_t o = sj != 0 ? int32_t(vj) + fi * sj : 0;
-            if (__ballot(f < T && sj == 0)) {  // gathered fires, waited for here
-              if (f < T && sj == 0) o = int32_t(times[vj + fi] - tb);
-            }
-            if (f < T) {
-              if (heavy) {
-                __builtin_nontemporal_store(tb + o, ot + S + db + f);
-                __builtin_nontemporal_store(rj, orl + S + db + f);
-              } else {
-                buf[db + f] = (uint32_t(o - A) << kSlRuleBits) | uint32_t(rj);
-              }
-            }
-          }
-        }
-      }
-      __syncthreads();  // the slab is in buf
-      if (!heavy) {
-        uint32_t key[IT];
-#pragma unroll
-        for (int jj = 0; jj < IT; jj++) {
-          const int e = w * (64 * IT) + jj * 64 + lane;
-          key[jj] = e < nj ? buf[e] : 0u;
-        }
-        ot_sort<NW, 256, false, kSlRuleBits, IT>(key, nj, 0u, 0, 1, buf, s);
-        for (int p = tid; p < nj; p += NT) {
-          const uint32_t v = buf[p];
-          __builtin_nontemporal_store(tb + A + int64_t(v >> kSlRuleBits), ot + S + p);
-          __builtin_nontemporal_store(int32_t(v & ((1u << kSlRuleBits) - 1u)), orl + S + p);
-          // a rule fires at most once a second: (second, rule) strictly ascending
-          const uint32_t u = ot_prev(buf, p, v);
-          bad |= p > 0 && u >= v;
-        }
-      }
-      S += nj;
-      A = Bn;
-      if (nj * 3 < CAP && wdt < kSlMaxWidth) wdt <<= 1;
-      __syncthreads();  // buf read before the next slab's expansion
-    }
-    bad |= S != int32_t(L);
-  }
-  if (__ballot(bad) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(a.err), 1ull);
-}
-
 int gridn(int64_t n, int threads) { return int(std::max<int64_t>(1, (n + threads - 1) / threads)); }
 
 
@@ -1682,24 +1344,6 @@ int order_merge_enqueue(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t c
     low ? tile(k_ot_tile<0, true>) : tile(k_ot_tile<0, false>);
   }
   return order_tail(c, node_off, N, t0, H, st, err, pack, pack, hx, sb);  // packed tiles: packed words in node_rule2
-}
-
-bool slab_order_ok(int64_t R, int64_t H, int32_t K, int64_t nnz, int32_t N) {
-  const char* e = getenv("CG_ORDER_SLAB");  // 0: never, 1: whenever it applies (A/B; read per call)
-  const int env = e ? atoi(e) : -1;
-  if (env == 0 || order_lsd_only()) return false;
-  if (R > (int64_t(1) << kSlRuleBits) || H <= 0 || H > 4096 || K < 1 || K > kSlMaxSegs || N < 1) return false;
-  // nodes of many pairs re-read many records per slab: the tile sort + merge
-  return env == 1 || nnz <= int64_t(N) * CG_SLAB_PAIRS_PER_NODE;
-}
-
-int slab_order_enqueue(cg_ctx* c, hipStream_t st, const SlabIn& in) {
-  const int cus = std::max(1, c->write_blocks / kWriteBlocksPerCU);
-  SlabArgs a{in.seg_pair, in.seg_nrec, in.seg_pos, in.recs, in.rule_off, in.times, in.t0, in.cap,
-             in.N, in.K, in.B, int32_t(in.H), in.ticket, in.err, in.out_time, in.out_rule,
-             in.grid, slab_grid_points(in.H)};
-  hipLaunchKernelGGL((k_node_slab<kSlWaves, kSlItems, kSlRpt>), dim3(unsigned(cus * 2)), dim3(64 * kSlWaves), 0, st, a);
-  return cg_hip_check(hipGetLastError(), "k_node_slab");
 }
 
 extern "C" int cg_node_result_order_by_time(cg_ctx* c) {

@@ -311,8 +311,7 @@ inline int64_t rule_info_slots(int64_t R) { return std::max<int64_t>(R, 1); }
 __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ rule_off,
                                                     const int64_t* __restrict__ times, int64_t R, int64_t t0,
                                                     int32_t B, int64_t cap, RuleInfo* __restrict__ info,
-                                                    int64_t* __restrict__ err, uint16_t* __restrict__ grid,
-                                                    int32_t G, int32_t H) {
+                                                    int64_t* __restrict__ err) {
   __shared__ int64_t off[kApRules + 1];
   __shared__ int64_t step[kApRules];
   __shared__ int32_t ok[kApRules];
@@ -368,37 +367,13 @@ __global__ __launch_bounds__(256) void k_rule_info(const int64_t* __restrict__ r
     }
   }
   __syncthreads();
-  bool prog = false;
   if (tid < nr) {
     const int64_t rel = first - t0, s = step[tid];
-    prog = cnt > 0 && ok[tid] && rel >= 0 && rel <= INT32_MAX && s > 0 && s <= INT32_MAX;
+    const bool prog = cnt > 0 && ok[tid] && rel >= 0 && rel <= INT32_MAX && s > 0 && s <= INT32_MAX;
     // counts and band-relative indices are < 2^30 (k_seg_records checks the
     // band span and fails the call otherwise)
     info[r0 + tid] = RuleInfo{int32_t(cnt), int32_t(off[tid] - band_lo),
                               prog ? int32_t(rel) : 0, prog ? int32_t(s) : 0};
-  }
-  if (grid == nullptr) return;
-  // the slab writer's grid rows (k_node_slab): for every rule whose fires are
-  // not a progression, its fires before each point min(c * kSlGrid, H) of the
-  // window (c < G), by binary searches of its fire list
-  __shared__ int32_t s_list[kApRules];
-  __shared__ int32_t s_nl;
-  if (tid == 0) s_nl = 0;
-  __syncthreads();
-  if (tid < nr && cnt > 0 && !prog) s_list[atomicAdd(&s_nl, 1)] = tid;
-  __syncthreads();
-  const int nl = s_nl;
-  for (int q = tid; q < nl * G; q += blockDim.x) {
-    const int li = q / G, cg = q - li * G;
-    const int r = s_list[li];
-    const int64_t want = t0 + 1 + (int64_t(cg) * kSlGrid < H ? int64_t(cg) * kSlGrid : H);
-    int64_t lo = off[r], hi = off[r + 1];
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (times[mid] < want) lo = mid + 1;
-      else hi = mid;
-    }
-    grid[(r0 + r) * G + cg] = uint16_t(lo - off[r]);
   }
 }
 
@@ -1299,15 +1274,9 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
       (rc = c->rule_info.ensure(rule_info_slots(R))))
     return rc;
   c->pn_res_host[1] = 0;  // error flag (nothing of this ctx is in flight here)
-  // (time, rule) order straight from the records (k_node_slab, its grid rows
-  // from k_rule_info), no order pass after
-  const bool slab = c->node_order == CG_NODE_ORDER_TIME && slab_order_ok(R, t1 - t0, K, nnz, N);
-  const int32_t G = slab_grid_points(t1 - t0);
-  if (slab && (rc = c->slab_grid.ensure(std::max<int64_t>(R, 1) * G))) return rc;
   if (R > 0)
     hipLaunchKernelGGL(k_rule_info, dim3(unsigned((R + kApRules - 1) / kApRules)), dim3(256), 0, st,
-                       c->offsets.p, c->times.p, R, t0, B, int64_t(c->times.cap), c->rule_info.p, c->pn_res_dev + 1,
-                       slab ? c->slab_grid.p : nullptr, G, int32_t(std::min<int64_t>(t1 - t0, INT32_MAX)));
+                       c->offsets.p, c->times.p, R, t0, B, int64_t(c->times.cap), c->rule_info.p, c->pn_res_dev + 1);
   if (NK > 0)
     hipLaunchKernelGGL(k_seg_records, dim3(gridn(NK, 4, 256 * 64)), dim3(256), 0, st, c->seg_pair.p,
                        c->nt_rule.p, c->offsets.p, c->rule_info.p, N, K, B, R, c->seg_cnt.p, c->seg_nrec.p,
@@ -1347,13 +1316,7 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   int64_t En = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     const int64_t cap = int64_t(std::min(c->node_time.cap, c->node_rule.cap));
-    if (NK > 0 && cap > 0 && slab) {
-      if ((rc = slab_order_enqueue(c, st, SlabIn{c->seg_pair.p, c->seg_nrec.p, c->seg_pos.p, c->recs.p, c->offsets.p,
-                                                 c->times.p, t0, t1 - t0, cap, N, K, B, c->pn_tickets.p,
-                                                 c->pn_res_dev + 2, c->node_time.p, c->node_rule.p,
-                                                 c->slab_grid.p})))
-        return rc;
-    } else if (NK > 0 && cap > 0 && off16) {
+    if (NK > 0 && cap > 0 && off16) {
       if (in_mode == kInPacked)
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),
                            dim3(256), 0, st, c->seg_pair.p, c->seg_pos.p, c->seg_nrec.p, c->recs.p, t0, c->offsets.p,
@@ -1406,17 +1369,6 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
   // (time, rule) order: the tile sort + merge (or, past 4096 s, the LSD
   // passes) after the writer; if it fails nothing is readable (the lists may
   // hold the writer's 16-bit offsets)
-  if (slab) {
-    c->kt[12] = 0.f;
-    if (c->pn_res_host[2] != 0) {
-      c->pn_E = 0;
-      c->pn_valid = false;
-      *n_events = 0;
-      return cg_fail(CG_EHIP, kOrderCheckMsg);
-    }
-    c->pn_time_ordered = true;
-    return CG_OK;
-  }
   if (c->node_order == CG_NODE_ORDER_TIME) {
     if ((rc = order_by_time_locked(c, in_mode))) {
       c->pn_E = 0;
@@ -1563,9 +1515,6 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     return cg_fail(CG_EINVAL, "pipelined per-node windows in time order: windows of at most 4096 s");
   bool empty = false;
   if ((rc = async_count_scan(c, a.rm, s, z, t0, t1, rm_cap, &empty))) return rc;
-  const bool slab = timed && slab_order_ok(R, t1 - t0, K, nnz, N);
-  const int32_t G = slab_grid_points(t1 - t0);
-  if (slab && (rc = a.slab_grid.ensure(std::max<int64_t>(R, 1) * G))) return rc;
   if ((rc = a.times.ensure(std::max<int64_t>(rm_cap, 1))) || (rc = a.rule_info.ensure(rule_info_slots(R))) ||
       (rc = a.seg_cnt.ensure(std::max<int64_t>(NK, 1))) || (rc = a.seg_pos.ensure(NK + 1)) ||
       (rc = a.seg_nrec.ensure(std::max<int64_t>(NK, 1))) || (rc = a.recs.ensure(std::max<int64_t>(nnz, 1))) ||
@@ -1595,8 +1544,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
                         a.times.p, sc);
     if (R > 0)
       hipLaunchKernelGGL(k_rule_info, dim3(unsigned((R + kApRules - 1) / kApRules)), dim3(256), 0, sc,
-                         a.rm.offsets.p, a.times.p, R, t0, B, rm_cap, a.rule_info.p, a.res_dev + 1,
-                         slab ? a.slab_grid.p : nullptr, G, int32_t(t1 - t0));
+                         a.rm.offsets.p, a.times.p, R, t0, B, rm_cap, a.rule_info.p, a.res_dev + 1);
   }
   if (NK > 0) {
     if (!empty)
@@ -1619,13 +1567,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     // wave slots beside this writer instead of waiting for it to retire
     static const int per_cu = std::max(1, node_write_blocks_per_cu() - 2);
     const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
-    if (slab) {  // (time, rule) order straight from the records
-      if ((rc = slab_order_enqueue(c, st, SlabIn{c->seg_pair.p, a.seg_nrec.p, a.seg_pos.p, a.recs.p, a.rm.offsets.p,
-                                                 a.times.p, t0, t1 - t0, node_cap, N, K, B, a.tickets.p,
-                                                 a.res_dev + 2, c->node_time.p, c->node_rule.p,
-                                                 a.slab_grid.p})))
-        return rc;
-    } else if (timed) {  // packed words (or 16-bit offsets), then the tile sort + merge on the same stream
+    if (timed) {  // packed words (or 16-bit offsets), then the tile sort + merge on the same stream
       const int in_mode = pn_pack_ok(R) ? kInPacked : kIn16;
       if (in_mode == kInPacked)
         hipLaunchKernelGGL((k_node_write<0, kInPacked>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))),

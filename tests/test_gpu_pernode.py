@@ -1,8 +1,5 @@
 """Rule -> node resolution and per-node fire lists on the GPU vs the oracle's
 restatement of Job.Cmds / GetJobNodes (job.go:591-630, web/job.go:222-257)."""
-import contextlib
-import os
-
 import numpy as np
 import pytest
 
@@ -18,21 +15,6 @@ DAY = 86400
 def eng():
     from cronsun_amd.engine import Engine
     return Engine(0)
-
-
-@contextlib.contextmanager
-def slab_writer(on):
-    """CG_ORDER_SLAB (read by the library per call): 1 the slab writer wherever
-    it applies, 0 the packed writer + tile sort + merge."""
-    old = os.environ.get("CG_ORDER_SLAB")
-    os.environ["CG_ORDER_SLAB"] = "1" if on else "0"
-    try:
-        yield
-    finally:
-        if old is None:
-            del os.environ["CG_ORDER_SLAB"]
-        else:
-            os.environ["CG_ORDER_SLAB"] = old
 
 
 def oracle_jobset(rin):
@@ -235,15 +217,12 @@ def test_transpose_cache_keyed_by_rule_set_and_mode(eng):
 def _ordered_per_node(eng, writer, scheds, zone, t0, t1, rin):
     """The per-node result in (time, rule) order: "pass" = rule-major lists,
     then cg_node_result_order_by_time; "direct" = cg_set_node_order(TIME)
-    (the order inside the per-node call: the slab writer k_node_slab where it
-    applies); "tiles" = the same with the packed writer + tile sort + merge
-    (CG_ORDER_SLAB=0).  Returns the rule-major node offsets and the ordered
-    CSR."""
-    if writer in ("direct", "tiles"):
+    (the pass inside the per-node call).  Returns the rule-major node offsets
+    and the ordered CSR."""
+    if writer == "direct":
         eng.set_node_order(_lib.NODE_ORDER_TIME)
         try:
-            with slab_writer(writer == "direct"):
-                node_off, time, rule = eng.expand_per_node(scheds, zone, t0, t1, rin, _lib.EXCLUDE_NONE)
+            node_off, time, rule = eng.expand_per_node(scheds, zone, t0, t1, rin, _lib.EXCLUDE_NONE)
         finally:
             eng.set_node_order(_lib.NODE_ORDER_RULE)
         assert eng.node_order_by_time() == 0.0  # already ordered: nothing to do
@@ -255,7 +234,7 @@ def _ordered_per_node(eng, writer, scheds, zone, t0, t1, rin):
     return node_off, off2, time2, rule2
 
 
-@pytest.mark.parametrize("writer", ["pass", "direct", "tiles"])
+@pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("zone,t0,secs", [("UTC", synth.T0_2026 + 64 * DAY, 3600), ("UTC", synth.T0_2026, 25 * 3600),
                                           ("America/New_York", 1772953200 - 12 * 3600, 24 * 3600),
                                           ("America/New_York", 1772953200 - 1800, 4096),
@@ -319,7 +298,7 @@ def progression_rules(R, n_nodes):
                    job_pause=np.zeros(R, np.uint8))
 
 
-@pytest.mark.parametrize("writer", ["pass", "direct", "tiles"])
+@pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("R,N,secs,star_every", [(1200, 3, 3600, 13), (2600, 2, 4096, 2), (64, 1, 61, 3),
                                                  (12000, 1, 120, 1), (40, 1, 4096, 10**9), (200, 1, 3600, 2),
                                                  (1200, 1, 1800, 1), (2600, 2, 2048, 2)])
@@ -369,7 +348,7 @@ def test_per_node_time_ordered_big_nodes(eng, writer, R, N, secs, star_every):
         assert 4096 < node_off[1] < 2 * 4096 and node_off[1] < 64 * 4096 // 8
 
 
-@pytest.mark.parametrize("writer", ["pass", "direct", "tiles"])
+@pytest.mark.parametrize("writer", ["pass", "direct"])
 @pytest.mark.parametrize("case", ["mid", "dense", "mid2"])
 @pytest.mark.parametrize("secs", [3600, 1800])
 def test_per_node_time_ordered_slab_classes(eng, writer, case, secs):
