@@ -1181,6 +1181,9 @@ int transpose_locked(cg_ctx* c, int64_t nnz, int32_t N) {
 // Rules per band: the band's rule-major fire lists (E_band * 8 B) should sit
 // in one XCD's 4 MiB L2 beside the write stream; a power of two, so the
 // cached segment bounds stay valid across windows of similar volume.
+#ifndef CG_BAND_MIN_RULES
+#define CG_BAND_MIN_RULES 32768  // rules per band at least (profiles/r06_ab_band_floor.txt: config 3 146-151 -> 144 ms)
+#endif
 #ifndef CG_BAND_BYTES
 #define CG_BAND_BYTES (1536 * 1024)
 #endif
@@ -1206,7 +1209,7 @@ int32_t seg_xcd_groups(int32_t K) { return CG_SEG_XCD > 1 && K >= 4 * CG_SEG_XCD
 int32_t band_rules(int64_t R, int64_t E) {
   const double per_rule = double(std::max<int64_t>(E, 1)) * 8.0 / double(std::max<int64_t>(R, 1));
   int64_t B = int64_t(double(CG_BAND_BYTES) / per_rule);
-  int64_t p = 1024;
+  int64_t p = CG_BAND_MIN_RULES;
   while (p < B && p < R && p < (int64_t(1) << 20)) p <<= 1;
   return int32_t(std::max<int64_t>(p, 1024));
 }
