@@ -39,8 +39,8 @@ Workloads (`--workload`, default config2 -- the headline line):
            10M rules x 7-day horizon"): config 3's node model (10k nodes, 500
            groups) over the config-4 rule set, per-node lists of the rank's
            job-ID range streamed in pipelined windows (`--window`, default
-           1 h for a rank of <= 2.5M rules, else 30 min, so a window's lists
-           fit HBM); a step = the whole 7 days; the per-node counts of every
+           90 min for a rank of > 5M rules, else 1 h; 30 min in time order past
+           2^20 rules; a window's lists fit HBM); a step = the whole 7 days; the per-node counts of every
            window all-gathered at N > 1 (cg_comm_node_offsets with --lib-comm).
   config3  config 3 as specified: 1M jobs x 10k nodes, the config-2 spec mix,
            24 h -> per-node lists, streamed in 1 h windows (`--window`; the
@@ -316,16 +316,18 @@ def main():
             shard_info = {"lo": lo, "hi": hi}
         shard_info["global_rules"] = total
         if pn and not args.window:
-            # 1-h windows: a 10M-rule rank's window holds ~10 G node events (120
-            # GB of lists), within HBM beside the three window sets' records;
-            # the per-window side chain (rule infos, segment records over all
-            # 920 M pairs) is then paid 168 times per step instead of 336.
+            # 90-min windows for a rank of > 5M rules (10M: ~14.5 G node events,
+            # 173 GB of lists, within HBM beside the three window sets'
+            # records), else 1 h: the per-window side chain (rule infos,
+            # segment records over all ~930 M pairs, ~8.4 ms) is paid 112 times
+            # per step instead of 168 (336 at 30 min): 5.16 vs 5.37 s per step
+            # on one box, 80 min 5.35 (profiles/r06_ab_config4pn_windows.txt).
             # Time order past 2^20 rules per rank keeps 30-min windows: their
             # 32-s slabs fit k_ot_mid's chunks (64-s slabs of a 1-h window
             # would go to k_ot_big's two reads).  2048-s windows (64 slabs of
             # 32 s, 296 windows) measured the same: 15.56 vs 15.49 s per step,
             # more slabs past k_ot_mid's chunk (profiles/r06_pmc_traffic_config4pn_order_2048.json)
-            W = 1800 if (args.time_order and R > (1 << 20)) else 3600
+            W = 1800 if (args.time_order and R > (1 << 20)) else (5400 if R > 5_000_000 else 3600)
 
         def spec_of(i):  # local rule i of this rank's range
             return base_specs[(shard_lo + i) % base_n]
