@@ -597,8 +597,9 @@ __device__ __forceinline__ void out_store(T* p, T v) {
 // segments of one node in turn: the concurrent write fronts stay in a few
 // nodes' lists).  Rule-ordered lists are written node-major (same-box A/B,
 // profiles/r05_ab_writer_order.txt: config 3 150.4 -> 146.9 ms, pernode
-// -3 %, config 4 per node -2 %); the time-order writer's packed words
-// band-major (node-major: config 3 in time order +1 %, pernode equal).
+// -3 %, config 4 per node -2 %) unless a node has many bands (node_major_for);
+// the time-order writer's packed words band-major (node-major: config 3 in
+// time order +1 %, pernode equal).
 #ifndef CG_NODE_MAJOR
 #define CG_NODE_MAJOR 1
 #endif
@@ -618,6 +619,15 @@ constexpr int kNodeGroups = CG_NODE_GROUPS < kTicketGroups ? CG_NODE_GROUPS : kT
 #define CG_NODE_GRP_XCD 1
 #endif
 constexpr int kNodeMajorDefault = CG_NODE_MAJOR;
+// rule-ordered lists with many bands per node go band-major: a node-major
+// sweep of K bands spreads the gathers over every band's fire lists, while
+// band-major keeps one band's in L2 (same-box A/B, profiles/r06_ab_writer_order_bands.txt:
+// config 4 per node, K = 305, 5 windows 201.8-203.4 -> 195.8-197.3 ms; config 3
+// and pernode, K = 31, stay node-major: 140.4 vs 152.6 ms, 3.14-3.18 vs 3.20)
+#ifndef CG_NODE_BAND_MAJOR_K
+#define CG_NODE_BAND_MAJOR_K 128
+#endif
+inline int node_major_for(int32_t K) { return K >= CG_NODE_BAND_MAJOR_K ? 0 : kNodeMajorDefault; }
 constexpr int kNodeMajorOrdered = CG_NODE_MAJOR_ORDERED;  // the time-order writer (packed words / 16-bit offsets)
 
 // One (node, band) segment's events from its records (k_seg_records), in
@@ -1305,7 +1315,8 @@ int per_node_locked(cg_ctx* c, const cg_specs* s, const cg_zone* z, int64_t t0, 
     return e ? atoi(e) : kNodeMajorDefault;
   }();
 #else
-  constexpr int variant = 0, node_major = kNodeMajorDefault;
+  constexpr int variant = 0;
+  const int node_major = node_major_for(K);
   static const int per_cu = node_write_blocks_per_cu();
 #endif
   const int nw_blocks = c->write_blocks / kWriteBlocksPerCU * per_cu;
@@ -1588,7 +1599,7 @@ int cg_expand_per_node_rules_device_async(cg_ctx* c, const cg_specs* s, const cg
     } else {
       hipLaunchKernelGGL((k_node_write<0, kInTimes>), dim3(unsigned(std::min<int64_t>(NK / 4 + 1, nw_blocks))), dim3(256),
                          0, st, c->seg_pair.p, a.seg_pos.p, a.seg_nrec.p, a.recs.p, t0, a.rm.offsets.p, a.times.p, N,
-                         K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, kNodeMajorDefault);
+                         K, B, node_cap, a.tickets.p, c->node_time.p, c->node_rule.p, node_major_for(K));
     }
   }
   (void)hipEventRecord(a.nw1, st);
