@@ -218,11 +218,13 @@ constexpr int kOtMid2Waves = 16;  // its 16-wave form (slabs of <= 16384 events;
 #define CG_OT_DENSE_WAVES 8
 #endif
 constexpr int kOtDenseWaves = CG_OT_DENSE_WAVES;  // the dense nodes' merge: waves per block (8 or 16)
+constexpr int kOtDenseWavesHx = 16;                // its form past 2^20 rules (order_tail)
 #ifndef CG_OT_DENSE_ITEMS
 #define CG_OT_DENSE_ITEMS 16
 #endif
 constexpr int kOtDenseItems = CG_OT_DENSE_ITEMS;  // its events per thread of a chunk
-static_assert(64 * kOtMid2Waves * kOtItems <= (1 << kOtIdxBits) && 64 * kOtDenseWaves * kOtDenseItems <= (1 << kOtIdxBits),
+static_assert(64 * kOtMid2Waves * kOtItems <= (1 << kOtIdxBits) && 64 * kOtDenseWaves * kOtDenseItems <= (1 << kOtIdxBits) &&
+                  64 * kOtDenseWavesHx * kOtDenseItems <= (1 << kOtIdxBits),
               "every chunk's element index fits the packed words' index bits");
 static_assert(kOtMergeWaves <= 8 && 12 + kOtIdxBits <= 32, "packed words");
 constexpr uint32_t kOtIdxMask = (1u << kOtIdxBits) - 1u;
@@ -1253,9 +1255,9 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
   HIPCHK(hipEventRecord(c->ot_fork, st));
   HIPCHK(hipStreamWaitEvent(c->st_ot, c->ot_fork, 0));
   // rule indices below 2^20: (offset, rule) packed in one word
-  auto merges = [&](auto m4, auto m8, auto mid_k, auto mid2_k) {
+  auto merges = [&](auto m4, auto m8, auto mid_k, auto mid2_k, int dense_waves = kOtDenseWaves) {
     // the dense merge: a persistent grid (2 blocks per CU) taking nodes by ticket
-    hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * kOtDenseWaves), 0,
+    hipLaunchKernelGGL(m8, dim3(unsigned(std::min<int64_t>(N, int64_t(cus) * CG_OT_DENSE_BPC))), dim3(64 * dense_waves), 0,
                        c->st_ot, toff, c->node_rule2.p, c->ts_base.p, node_off, c->ts_hist.p, N, t0, slab_tab,
                        c->node_time.p, c->node_rule.p, c->ts_off.p, big_n, mid, big_n + 1, mid2, big_n + 3,
                        dense_min, INT64_MAX, big_n + 2, err, sb, c->ts_start.p, c->ts_hi.p);
@@ -1280,10 +1282,16 @@ int order_tail(cg_ctx* c, const int64_t* node_off, int32_t N, int64_t t0, int64_
                          c->ts_base.p, node_off, c->ts_hist.p, t0, slab_tab, c->node_time.p, c->node_rule.p, mid2,
                          big_n + 3, err, sb, c->ts_start.p, c->ts_hi.p);
   };
+  // past 2^20 rules (config 4 per node: every node dense, 32-s slabs of ~9 k
+  // events) the dense merge runs 16 waves, a 16384-event chunk, so those slabs
+  // skip k_ot_mid<16>'s separate pass: 5 windows 195.1-203.3 vs 201.2-208.7 ms;
+  // with 8 waves config 3 is equal and pernode 12 % faster
+  // (profiles/r06_ab_dense_merge_waves.txt)
   if (hx)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true, true>,
-           k_ot_merge<kOtDenseWaves, true, kOtDenseItems, true, true, true>,
-           k_ot_mid<kOtMidWaves, true, kOtItems, true, true>, k_ot_mid<kOtMid2Waves, true, kOtItems, true, true>);
+           k_ot_merge<kOtDenseWavesHx, true, kOtDenseItems, true, true, true>,
+           k_ot_mid<kOtMidWaves, true, kOtItems, true, true>, k_ot_mid<kOtMid2Waves, true, kOtItems, true, true>,
+           kOtDenseWavesHx);
   else if (pack && pin)
     merges(k_ot_merge<kOtMergeWaves, true, kOtMergeItems, false, true>,
            k_ot_merge<kOtDenseWaves, true, kOtDenseItems, true, true>, k_ot_mid<kOtMidWaves, true, kOtItems, true>,
